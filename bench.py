@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the path-tracing hot path (BASELINE.json metric), Cornell box.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
+
+One step = one frame: every rank renders its 8-row stripes of the frame with the HIP kernel
+(rvcp_render_shard_async), the stripes are gathered to rank 0 over RCCL (torch.distributed
+'nccl' backend) and rank 0 assembles the frame on the device.  Scene and camera are uploaded
+once, before timing (inputs resident in HBM).
+
+Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
+  c3: Cornell 1024x1024 SPP=30.  For N>1 the frame grows with N at fixed SPP
+      (side = round8(1024*sqrt(N))), so per-GPU work stays ~C3: "scaling": "weak".
+  c2: Cornell 384x384 SPP=10 (README benchmark row).
+  c4: Cornell 2048x2048 SPP=64, fixed frame sharded over N GPUs ("scaling": "strong").
+  c5: Cornell + 100k random triangles, 1024x1024 SPP=30.
+
+Rank 0 prints ONE JSON line.  `roofline` uses the BASELINE.md definition: algorithmic bytes
+= traversals x F x 36 B per launch over the kernel's HIP-event time; `cpu_baseline` times the
+scalar C++ oracle (oracle/rvcp_oracle.c, the CPU re-execution of the same kernel) on a
+bounded sample of the workload, on rank 0 at N=1 only.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (spec)
+FLOP_PER_TEST = 52
+
+
+def workload(name, n_gpus):
+    if name == "c3":
+        side = 1024 if n_gpus == 1 else int(round(1024 * math.sqrt(n_gpus) / 8.0)) * 8
+        return dict(workload="cornell_1024sq_spp30" if n_gpus == 1 else
+                    f"cornell_{side}sq_spp30_weak", W=side, H=side, spp=30, extra_tris=0,
+                    scaling="weak")
+    if name == "c2":
+        return dict(workload="cornell_384sq_spp10", W=384, H=384, spp=10, extra_tris=0,
+                    scaling="strong")
+    if name == "c4":
+        return dict(workload="cornell_2048sq_spp64", W=2048, H=2048, spp=64, extra_tris=0,
+                    scaling="strong")
+    if name == "c5":
+        return dict(workload="cornell_plus_100k_tris_1024sq_spp30", W=1024, H=1024, spp=30,
+                    extra_tris=100000, scaling="strong")
+    raise SystemExit(f"unknown workload {name}")
+
+
+def cpu_baseline(sc, cfg_kw, W, H, threads):
+    """Time the CPU oracle (scalar C++ re-execution) on every 8th row of the workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import rvcp_amd
+    O.build()
+    cfg = rvcp_amd.abi.make_config(**cfg_kw)
+    arrays = dict(materials=sc.aligned_materials(), vertices=sc.mesh.aligned_vertices(),
+                  faces=sc.mesh.aligned_faces(), lum_face_ids=sc.luminous_face_ids())
+    push = sc.push_constant(123.0)
+    rows = list(range(0, H, 8))
+    O.render(arrays, push, cfg, W, H, rect=(0, H // 2, min(W, 64), 1), threads=threads,
+             want_linear=False)                                   # warm-up (page-in, threads)
+    if len(arrays["faces"]) > 1000:          # C5 on CPU: 128^2 SPP=1 frame only
+        t0 = time.perf_counter()
+        O.render(arrays, push, rvcp_amd.abi.make_config(**dict(cfg_kw, spp=1)), 128, 128,
+                 threads=threads, want_linear=False)
+        dt = time.perf_counter() - t0
+        return dict(value=128 * 128 / dt / 1e6, unit="Msamples/s", cores=threads, kind="port",
+                    sample="128x128 SPP=1 frame of the same scene", seconds=round(dt, 3))
+    t0 = time.perf_counter()
+    for y in rows:
+        O.render(arrays, push, cfg, W, H, rect=(0, y, W, 1), threads=threads, want_linear=False)
+    dt = time.perf_counter() - t0
+    samples = len(rows) * W * cfg_kw["spp"]
+    return dict(value=samples / dt / 1e6, unit="Msamples/s", cores=threads, kind="port",
+                sample=f"every 8th row ({len(rows)} of {H}) of the {W}x{H} SPP={cfg_kw['spp']} "
+                       f"frame, {threads} threads", seconds=round(dt, 3))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    ap.add_argument("--save-frame", default="")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import rvcp_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    wl = workload(args.workload, world)
+    W, H, spp = wl["W"], wl["H"], wl["spp"]
+    sc = rvcp_amd.Scene.default()
+    if wl["extra_tris"]:
+        sc = rvcp_amd.scene.with_random_triangles(sc, wl["extra_tris"])
+    cfg_kw = dict(spp=spp, device=local_rank)
+    rt = rvcp_amd.RayTracer(**cfg_kw)
+    rt.upload_scene(sc)
+    push = sc.push_constant(123.0)
+    n_faces = len(sc.mesh.aligned_faces())
+
+    rows = rvcp_amd.shard_rows(H, rank, world)
+    slot = max(rvcp_amd.shard_rows(H, k, world) for k in range(world))
+    dev = torch.device("cuda", local_rank)
+    shard_buf = torch.zeros((slot, W), dtype=torch.int32, device=dev)
+    gathered = [torch.zeros((slot, W), dtype=torch.int32, device=dev) for _ in range(world)] \
+        if (world > 1 and rank == 0) else None
+    frame = torch.zeros((H, W), dtype=torch.int32, device=dev) if rank == 0 else None
+    gat_flat = torch.zeros((world, slot, W), dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        if world == 1:
+            rt.render_shard_async(push, W, H, 0, 1, frame.data_ptr(), stream=stream)
+            st = rt.sync_stats()
+            return st
+        rt.render_shard_async(push, W, H, rank, world, shard_buf.data_ptr(), stream=stream)
+        st = rt.sync_stats()
+        dist.gather(shard_buf, gathered if rank == 0 else None, dst=0)
+        if rank == 0:
+            for k in range(world):
+                gat_flat[k].copy_(gathered[k])
+            rt.assemble_frame_async(gat_flat.data_ptr(), slot, W, H, world, frame.data_ptr(),
+                                    stream=stream)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms, trav, trav_exec = [], 0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+        kernel_ms.append(float(st["kernel_ms"]))
+        trav += int(st["traversals"])
+        trav_exec += int(st["traversals_executed"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples_total = W * H * spp * args.steps
+    value = samples_total / elapsed / 1e6
+    ms_per_step = elapsed * 1000.0 / args.steps
+
+    # roofline for the dominant kernel (this rank's launches)
+    avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1000.0
+    bytes_per_launch = trav / args.steps * n_faces * 36
+    achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
+    tests_per_s = trav / args.steps * n_faces / avg_kernel_s
+    exec_tests_per_s = trav_exec / args.steps * n_faces / avg_kernel_s
+
+    if args.save_frame and rank == 0:
+        np.save(args.save_frame, frame.cpu().numpy().view(np.uint8).reshape(H, W, 4))
+
+    if rank == 0:
+        out = {
+            "metric": "Msamples/sec (pixels*SPP/s) + frame ms, Cornell Box 1024^2 SPP=30",
+            "value": round(value, 2),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "fps": round(1000.0 / ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": wl["scaling"],
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)",
+            "config": {"workload": wl["workload"], "width": W, "height": H, "spp": spp,
+                       "faces": n_faces, "parallelism": f"pixel-stripes x{world}",
+                       "gather": "rccl" if world > 1 else "none"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms": round(avg_kernel_s * 1000.0, 4),
+                         "definition": "traversals x F x 36 B per launch / kernel time "
+                                       "(BASELINE.md §2; reference-algorithm traversals)",
+                         "traversals_per_sample": round(trav / args.steps / (W * H * spp / world), 4)
+                         if world == 1 else None,
+                         "executed_traversal_frac": round(trav_exec / max(trav, 1), 4),
+                         "valu_tflops": round(tests_per_s * FLOP_PER_TEST / 1e12, 2),
+                         "valu_frac": round(tests_per_s * FLOP_PER_TEST / 1e12 / FP32_PEAK_TFLOPS, 4),
+                         "executed_tests_per_s": round(exec_tests_per_s, 1)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(sc, cfg_kw, W, H, threads)
+        print(json.dumps(out), flush=True)
+
+    rt.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

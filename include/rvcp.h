@@ -1,0 +1,237 @@
+/*
+ * rvcp.h -- C-ABI of librvcp, the MI355X (gfx950) replacement for the Vulkano compute
+ * pipeline of YXHXianYu/RVCP-Real-Time-Path-Tracer (`src/ray_tracer/vulkan.rs`).
+ *
+ * The hot path behind this ABI is the per-pixel path-tracing kernel that `src/ray_tracer`
+ * dispatches: `assets/shaders/ray_tracer_games101_branch.comp` (selected by
+ * `src/ray_tracer/shader.rs:12`).  Every struct below is byte-identical to the reference's
+ * Rust-side upload struct (`#[repr(C)]`, `BufferContents`), so a Rust caller can hand the
+ * same `Vec<Aligned*>` it used to give `Buffer::from_iter` straight to this library.
+ *
+ * Conventions
+ *   - All functions return 0 (RVCP_OK) on success and a negative RVCP_E_* code on failure.
+ *     Nothing aborts or throws across the ABI; `rvcp_last_error(ctx)` returns a message.
+ *   - A context is not thread-safe: use one context per host thread.
+ *   - Host pointers stay owned by the caller; the library copies what it needs.
+ *   - Pointers named `d_*` are HIP device pointers; `stream` is a `hipStream_t` (NULL = the
+ *     legacy default stream).
+ */
+#ifndef RVCP_H
+#define RVCP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------------------
+ * Upload structs (byte-identical to the reference; static_asserts in rvcp_layout_check.c)
+ * ------------------------------------------------------------------------------------- */
+
+/* == AlignedCamera, src/ray_tracer/scene/camera.rs:27-37 (64 B).
+ *    Shader view: struct Camera, ray_tracer_games101_branch.comp:37-44 (std430 push block). */
+typedef struct rvcp_camera {
+    float position[4];      /* xyz + pad (utils.rs:5-7 vec3_to_f32_4) */
+    float up[4];            /* xyz + pad */
+    float forward[3];
+    float t_near;
+    float t_far;
+    float vertical_fov;     /* degrees */
+    uint32_t _padding[2];
+} rvcp_camera_t;
+
+/* == PushConstant { camera: AlignedCamera, time: f32 }, src/ray_tracer/vulkan.rs:113-118
+ *    (68 B).  `time` is the RNG seed input (vulkan.rs:418-421 stamps unix_secs % 1000). */
+typedef struct rvcp_push_constant {
+    rvcp_camera_t camera;
+    float time;
+} rvcp_push_constant_t;
+
+/* == AlignedMaterial, src/ray_tracer/scene/material.rs:20-28 (32 B, std140 array stride).
+ *    ty: 0 Lambertian, 1 Metal, 2 Dielectric, 3 Light (material.rs:4-10). */
+typedef struct rvcp_material {
+    float albedo[3];        /* Le for lights */
+    uint32_t ty;
+    float fuzz;
+    float refraction_ratio;
+    uint32_t _padding[2];
+} rvcp_material_t;
+
+/* == AlignedVertex, src/ray_tracer/scene/mesh.rs:13-18 (32 B). */
+typedef struct rvcp_vertex {
+    float position[4];
+    float normal[4];
+} rvcp_vertex_t;
+
+/* == AlignedFace, src/ray_tracer/scene/mesh.rs:37-42 (16 B). */
+typedef struct rvcp_face {
+    uint32_t vertices[3];
+    uint32_t material_id;
+} rvcp_face_t;
+
+/* == AlignedSphere, src/ray_tracer/scene/sphere.rs:10-17 (32 B).  Accepted for ABI
+ *    completeness; the dispatched games101 kernel never reads spheres. */
+typedef struct rvcp_sphere {
+    float center[3];
+    float radius;
+    uint32_t material_id;
+    uint32_t _padding[3];
+} rvcp_sphere_t;
+
+/* == the 6 x u32 LengthBuffer, vulkan.rs:481-500 / ray_tracer_games101_branch.comp:58-65. */
+typedef struct rvcp_lengths {
+    uint32_t materials_len;
+    uint32_t spheres_len;
+    uint32_t vertices_len;
+    uint32_t faces_len;
+    uint32_t luminous_sphere_id_len;
+    uint32_t luminous_face_id_len;
+} rvcp_lengths_t;
+
+/* ---------------------------------------------------------------------------------------
+ * Configuration: the shader's compile-time #defines become runtime parameters with the
+ * same defaults (ray_tracer_games101_branch.comp:5-13).
+ * ------------------------------------------------------------------------------------- */
+enum {
+    RVCP_INTEGRATOR_GAMES101 = 0,     /* ray_trace_games101, the dispatched shader */
+};
+
+typedef struct rvcp_config {
+    int32_t device;                   /* HIP device ordinal */
+    int32_t integrator;               /* RVCP_INTEGRATOR_* */
+    uint32_t spp;                     /* SPP (:8) = 20 */
+    uint32_t max_bounces;             /* MAX_BOUNCES (:9) = 15 */
+    float attenuation_stop_eps;       /* ATTENUATION_STOP_EPS (:10) = 0.05 */
+    float ray_t_min;                  /* RAY_T_MIN (:11) = 0.01 */
+    float ray_t_max;                  /* RAY_T_MAX (:12) = 10000 */
+    float rr_probability;             /* RR_PROBABILITY (:13) = 0.8 */
+    float eps;                        /* EPS (:5) = 0.001 */
+    /* 1 (default) reproduces what the reference GPU reads from the std140 `uint v[100]`
+     * LuminousFaceIdBuffer that the host fills with tightly packed u32s
+     * (ray_tracer_games101_branch.comp:109-111 vs vulkan.rs:473-478): element i is
+     * ids[4*i] when 4*i < n_ids, else 0.  0 = the intended packed semantics. */
+    int32_t lum_id_std140_quirk;
+    uint32_t _reserved[6];
+} rvcp_config_t;
+
+/* Per-render statistics (all optional). */
+typedef struct rvcp_stats {
+    double kernel_ms;                 /* device time of the render kernel(s), HIP events */
+    uint64_t traversals;              /* scene traversals the reference algorithm performs
+                                         (get_intersection_with_scene calls) */
+    uint64_t traversals_executed;     /* traversals this kernel actually ran (primary hits
+                                         are reused across a pixel's samples) */
+    uint64_t samples;                 /* pixels * spp */
+    uint32_t faces;                   /* F, triangles tested per traversal */
+    uint32_t _reserved[3];
+} rvcp_stats_t;
+
+/* Layout checks: sizes/offsets the reference's Rust structs and std140/std430 blocks imply. */
+#ifdef __cplusplus
+#define RVCP_STATIC_ASSERT(c, m) static_assert(c, m)
+#else
+#define RVCP_STATIC_ASSERT(c, m) _Static_assert(c, m)
+#endif
+RVCP_STATIC_ASSERT(sizeof(rvcp_camera_t) == 64, "AlignedCamera is 64 B");
+RVCP_STATIC_ASSERT(offsetof(rvcp_camera_t, forward) == 32, "Camera.forward @32");
+RVCP_STATIC_ASSERT(offsetof(rvcp_camera_t, t_near) == 44, "Camera.t_near @44");
+RVCP_STATIC_ASSERT(offsetof(rvcp_camera_t, vertical_fov) == 52, "Camera.vertical_fov @52");
+RVCP_STATIC_ASSERT(sizeof(rvcp_push_constant_t) == 68, "PushConstant is 68 B");
+RVCP_STATIC_ASSERT(offsetof(rvcp_push_constant_t, time) == 64, "PushConstant.time @64");
+RVCP_STATIC_ASSERT(sizeof(rvcp_material_t) == 32, "AlignedMaterial is 32 B");
+RVCP_STATIC_ASSERT(offsetof(rvcp_material_t, ty) == 12, "Material.ty @12");
+RVCP_STATIC_ASSERT(offsetof(rvcp_material_t, refraction_ratio) == 20, "Material.ior @20");
+RVCP_STATIC_ASSERT(sizeof(rvcp_vertex_t) == 32, "AlignedVertex is 32 B");
+RVCP_STATIC_ASSERT(offsetof(rvcp_vertex_t, normal) == 16, "Vertex.normal @16");
+RVCP_STATIC_ASSERT(sizeof(rvcp_face_t) == 16, "AlignedFace is 16 B");
+RVCP_STATIC_ASSERT(sizeof(rvcp_sphere_t) == 32, "AlignedSphere is 32 B");
+RVCP_STATIC_ASSERT(sizeof(rvcp_lengths_t) == 24, "LengthBuffer is 24 B");
+
+typedef struct rvcp_ctx rvcp_ctx_t;
+
+/* Error codes */
+#define RVCP_OK               0
+#define RVCP_E_INVALID      (-1)   /* bad argument */
+#define RVCP_E_HIP          (-2)   /* HIP runtime error */
+#define RVCP_E_NO_SCENE     (-3)   /* render before upload */
+#define RVCP_E_UNSUPPORTED  (-4)
+#define RVCP_E_NOMEM        (-5)
+
+/* ---------------------------------------------------------------------------------------
+ * Entry points
+ * ------------------------------------------------------------------------------------- */
+
+/* Library version string. */
+const char *rvcp_version(void);
+
+/* Fill `cfg` with the reference's #define defaults.  Replaces nothing (the reference bakes
+ * them into the SPIR-V at `vulkano_shaders::shader!`, src/ray_tracer/shader.rs:9-14). */
+int rvcp_config_default(rvcp_config_t *cfg);
+
+/* Create a context on cfg->device.  Replaces pipeline creation:
+ * `Vk::create_compute_pipeline(device, ray_tracer_shader::load(device))`,
+ * src/ray_tracer/vulkan.rs:576-603 (called at :239-242). */
+int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx);
+
+/* Free the context and all device memory it owns. */
+int rvcp_destroy(rvcp_ctx_t *ctx);
+
+/* Last error message for `ctx` ("" if none).  ctx may be NULL (global create errors). */
+const char *rvcp_last_error(const rvcp_ctx_t *ctx);
+
+/* Upload a scene.  Replaces `Vk::create_descriptor_set_0s`, src/ray_tracer/vulkan.rs:454-574
+ * (bindings 1 LengthBuffer, 2 MaterialBuffer, 4 VertexBuffer, 5 FaceBuffer,
+ * 7 LuminousFaceIdBuffer).  `lum_face_ids` are the packed u32 ids the host computes at
+ * vulkan.rs:473-478; the std140 quirk is applied inside.  Spheres / luminous sphere ids
+ * (bindings 3 / 6 of ray_tracer.comp) may be NULL/0.  Face vertex indices and material
+ * ids are validated (the reference does not bound-check; out-of-range ids are an error). */
+int rvcp_upload_scene(rvcp_ctx_t *ctx,
+                      const rvcp_material_t *materials, uint32_t n_materials,
+                      const rvcp_vertex_t *vertices, uint32_t n_vertices,
+                      const rvcp_face_t *faces, uint32_t n_faces,
+                      const rvcp_sphere_t *spheres, uint32_t n_spheres,
+                      const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
+                      const uint32_t *lum_sphere_ids, uint32_t n_lum_sphere_ids);
+
+/* Render one full frame synchronously into host memory.  Replaces the per-frame
+ * `push_constants(...)` + `dispatch([W/8, H/8, 1])` + present of vulkan.rs:406-452 and
+ * :298-404.  out_rgba8: W*H*4 bytes, row-major, logical RGBA (the reference's swapchain was
+ * B8G8R8A8_UNORM, records/swapchain_image.txt:8), alpha 255.  out_linear_rgb (optional):
+ * W*H*3 floats, the pre-clamp, pre-gamma `color` of ray_tracer_games101_branch.comp:497.
+ * Unlike the reference, W and H need not be multiples of 8 (every pixel is rendered). */
+int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
+                uint32_t width, uint32_t height,
+                uint8_t *out_rgba8, float *out_linear_rgb, rvcp_stats_t *stats);
+
+/* Asynchronous shard render into device memory, for multi-GPU frame assembly.
+ * The frame is cut into 8-row stripes (the reference's 8x8 workgroup rows); stripe s is
+ * rendered by shard (s % shard_count).  This call renders the stripes of `shard_index`
+ * and packs them contiguously, in increasing stripe order, into d_rgba8
+ * (rvcp_shard_rows(H, idx, count) * W * 4 bytes) and optionally d_linear_rgb (rows*W*3
+ * floats).  Pixel values are bit-identical to a single-GPU render of the whole frame.
+ * Enqueued on `stream`; stats->kernel_ms/traversals are filled by rvcp_sync_stats(). */
+int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
+                            uint32_t width, uint32_t height,
+                            uint32_t shard_index, uint32_t shard_count,
+                            void *d_rgba8, void *d_linear_rgb, void *stream);
+
+/* Wait for the last async render of ctx and fetch its statistics. */
+int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats);
+
+/* Rows of an H-row frame owned by shard `shard_index` of `shard_count`. */
+uint32_t rvcp_shard_rows(uint32_t height, uint32_t shard_index, uint32_t shard_count);
+
+/* Assemble a frame on the device from gathered shard buffers.  d_gathered holds
+ * shard_count slots of `slot_rows` rows (slot_rows >= max shard rows) each, shard k's
+ * packed stripes at slot k.  Writes the W x H RGBA8 frame to d_frame.  Enqueued on stream. */
+int rvcp_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t slot_rows,
+                              uint32_t width, uint32_t height, uint32_t shard_count,
+                              void *d_frame, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RVCP_H */

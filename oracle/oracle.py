@@ -1,0 +1,111 @@
+"""ctypes wrapper of the CPU oracle (oracle/build/librvcp_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker.  The product path (librvcp.so) never uses it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "librvcp_oracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (gcc); returns the .so path."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.rvcp_oracle_sinf.argtypes = [ctypes.c_float]
+        L.rvcp_oracle_sinf.restype = ctypes.c_float
+        L.rvcp_oracle_gamma_u8.argtypes = [ctypes.c_float]
+        L.rvcp_oracle_gamma_u8.restype = ctypes.c_uint8
+        L.rvcp_oracle_gamma_threshold.argtypes = [ctypes.c_int]
+        L.rvcp_oracle_gamma_threshold.restype = ctypes.c_float
+        L.rvcp_oracle_rand_sequence.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                                ctypes.c_int, P]
+        L.rvcp_oracle_rand_sequence.restype = None
+        L.rvcp_oracle_intersect.argtypes = [P, P, P]
+        L.rvcp_oracle_intersect.restype = ctypes.c_int
+        L.rvcp_oracle_sample_ray.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_uint32, P]
+        L.rvcp_oracle_sample_ray.restype = None
+        u32 = ctypes.c_uint32
+        L.rvcp_oracle_render.argtypes = [P, u32, P, u32, P, u32, P, u32, P, P,
+                                         u32, u32, u32, u32, u32, u32, P, P, P, ctypes.c_int]
+        L.rvcp_oracle_render.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def sinf(x: float) -> float:
+    return float(lib().rvcp_oracle_sinf(ctypes.c_float(x)))
+
+
+def gamma_u8(c: float) -> int:
+    return int(lib().rvcp_oracle_gamma_u8(ctypes.c_float(c)))
+
+
+def rand_sequence(time: float, u: float, v: float, n: int) -> np.ndarray:
+    out = np.zeros(n + 1, dtype=np.float32)
+    lib().rvcp_oracle_rand_sequence(ctypes.c_float(time), ctypes.c_float(u), ctypes.c_float(v),
+                                    n, _ptr(out))
+    return out
+
+
+def intersect(ray, tri):
+    ray = np.ascontiguousarray(ray, dtype=np.float32)
+    tri = np.ascontiguousarray(tri, dtype=np.float32).reshape(9)
+    out = np.zeros(3, dtype=np.float32)
+    hit = lib().rvcp_oracle_intersect(_ptr(ray), _ptr(tri), _ptr(out))
+    return bool(hit), out
+
+
+def sample_ray(push, W, H, x, y) -> np.ndarray:
+    push = np.ascontiguousarray(push)
+    out = np.zeros(8, dtype=np.float32)
+    lib().rvcp_oracle_sample_ray(_ptr(push), W, H, x, y, _ptr(out))
+    return out
+
+
+def render(scene_arrays: dict, push, cfg, W, H, rect=None, threads=None, want_linear=True):
+    """Render with the oracle.  scene_arrays: materials/vertices/faces/lum_face_ids numpy
+    record arrays (scene.py dtypes); push: PUSH_DTYPE record; cfg: rvcp_config_t bytes
+    (numpy record of CONFIG_DTYPE).  Returns (linear [th,tw,3] f32 | None, rgba [th,tw,4] u8,
+    traversals)."""
+    x0, y0, tw, th = rect if rect is not None else (0, 0, W, H)
+    threads = threads or os.cpu_count() or 1
+    mats = np.ascontiguousarray(scene_arrays["materials"])
+    verts = np.ascontiguousarray(scene_arrays["vertices"])
+    faces = np.ascontiguousarray(scene_arrays["faces"])
+    lum = np.ascontiguousarray(scene_arrays["lum_face_ids"], dtype=np.uint32)
+    push = np.ascontiguousarray(push)
+    cfg = np.ascontiguousarray(cfg)
+    lin = np.zeros((th, tw, 3), dtype=np.float32) if want_linear else None
+    rgba = np.zeros((th, tw, 4), dtype=np.uint8)
+    trav = np.zeros(1, dtype=np.uint64)
+    rc = lib().rvcp_oracle_render(_ptr(mats), len(mats), _ptr(verts), len(verts), _ptr(faces),
+                                  len(faces), _ptr(lum), len(lum), _ptr(push), _ptr(cfg),
+                                  W, H, x0, y0, tw, th, _ptr(lin), _ptr(rgba), _ptr(trav),
+                                  int(threads))
+    if rc != 0:
+        raise ValueError(f"rvcp_oracle_render failed: {rc}")
+    return lin, rgba, int(trav[0])

@@ -1,0 +1,521 @@
+/*
+ * rvcp_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, scalar CPU restatement of the path-tracing kernel that the reference's
+ * `src/ray_tracer` dispatches: /root/reference/assets/shaders/ray_tracer_games101_branch.comp
+ * (selected by src/ray_tracer/shader.rs:12).  It exists to check the HIP kernel and to time
+ * the CPU baseline.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load it; the product (librvcp.so) never links, calls or falls back to it.
+ *
+ * It is written independently of the HIP kernel: it follows the GLSL function by function
+ * (each function cites the shader line it restates) and shares with the kernel only the
+ * numeric contract of DESIGN.md §3 (float32 everywhere, no FMA contraction, IEEE
+ * correctly-rounded + - * / sqrt, the software sin below, the gamma threshold table).
+ *
+ * Parity pinning: the reference ships no tests and no golden vectors.  The
+ * only reference-produced output is the README screenshot (1024^2, SPP=30); this oracle is
+ * pinned against its block means by tests/test_oracle_reference.py (fixture made by
+ * tests/golden/make_readme_fixture.py).  Per-pixel parity with the NVIDIA/Vulkan original is
+ * impossible because its sin() is driver-defined; the oracle therefore
+ * pins the algorithm statistically and the HIP kernel bit-exactly against this file.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fno-fast-math).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/rvcp.h"
+
+#if defined(__FP_FAST_FMA) || defined(__FAST_MATH__)
+#if defined(__FAST_MATH__)
+#error "the oracle must not be built with -ffast-math"
+#endif
+#endif
+
+/* ------------------------------------------------------------------------------------- */
+/* Constants: ray_tracer_games101_branch.comp:5-25                                         */
+/* ------------------------------------------------------------------------------------- */
+#define PI_F 3.1415926f          /* :6 (not M_PI) */
+#define MATERIAL_LIGHT 3u        /* :25 */
+
+typedef struct {
+    uint32_t spp, max_bounces;
+    float att_stop, t_min, t_max, rr, eps;
+    int quirk;
+} params_t;
+
+/* ------------------------------------------------------------------------------------- */
+/* vec3 algebra with GLSL semantics, evaluated left to right, no contraction              */
+/* ------------------------------------------------------------------------------------- */
+typedef struct { float x, y, z; } v3;
+
+static inline v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 mulv(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 muls(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline v3 divs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+static inline v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 cross(v3 a, v3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline float length(v3 a) { return sqrtf(dot(a, a)); }
+/* GLSL normalize(v) restated as v * (1 / sqrt(dot(v, v))). */
+static inline v3 normalize(v3 a) { return muls(a, 1.0f / sqrtf(dot(a, a))); }
+static inline float fractf(float x) { return x - floorf(x); }     /* GLSL fract */
+static inline v3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
+
+/* ------------------------------------------------------------------------------------- */
+/* Software sin: Cody-Waite reduction by pi/2 with fma, Cephes minimax    */
+/* polynomials on [-pi/4, pi/4].  Bit-identical wherever fmaf/rintf/floorf are IEEE.       */
+/* ------------------------------------------------------------------------------------- */
+float rvcp_oracle_sinf(float x)
+{
+    if (!(fabsf(x) < 1.0e30f)) return x - x;            /* NaN for inf/NaN */
+    const float q = rintf(x * 0.636619772367581343f);   /* nearest quadrant */
+    float r = fmaf(q, -1.57079637050628662109375f, x);  /* x - q*float(pi/2) */
+    r = fmaf(q, 4.37113900018624283e-8f, r);            /* - q*(pi/2 - float(pi/2)) */
+    const float z = r * r;
+    const float ps = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    const float s = fmaf(ps, z * r, r);
+    const float pc = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                          4.166664568298827e-2f);
+    const float c = fmaf(pc, z * z, fmaf(-0.5f, z, 1.0f));
+    const float qm = q - 4.0f * floorf(q * 0.25f);     /* q mod 4, exact */
+    const int j = (int)qm;
+    return j == 0 ? s : (j == 1 ? c : (j == 2 ? -s : -c));
+}
+
+/* ------------------------------------------------------------------------------------- */
+/* RNG: ray_tracer_games101_branch.comp:151-168                                            */
+/* ------------------------------------------------------------------------------------- */
+typedef struct { float seed, index; } rng_t;
+
+/* srand, :153-155 */
+static inline void srand_glsl(rng_t *g, float time, float u, float v)
+{
+    float a = fractf(rvcp_oracle_sinf(time) * 43758.5453f);
+    float b = fractf(rvcp_oracle_sinf(u) * 22578.5453f);
+    float c = fractf(rvcp_oracle_sinf(v) * 114514.1919f);
+    g->seed = fractf(a + b + c);
+    g->index = 0.0f;     /* :152 global initialiser; one invocation per pixel */
+}
+/* _rand, :156-158 */
+static inline float rand_of(float x) { return fractf(rvcp_oracle_sinf(x) * 43758.5453f); }
+/* rand, :159-162 */
+static inline float rand_next(rng_t *g)
+{
+    g->index = g->index + 1.0f;
+    return rand_of(g->seed + g->index);
+}
+
+/* random_in_unit_sphere, :195-201 (rand3 evaluates x, y, z in order, :166-168) */
+static v3 random_in_unit_sphere(rng_t *g)
+{
+    v3 p;
+    do {
+        float rx = rand_next(g), ry = rand_next(g), rz = rand_next(g);
+        p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
+    } while (dot(p, p) >= 1.0f);
+    return p;
+}
+/* random_in_unit_hemisphere(_surface), :207-214 */
+static v3 random_in_unit_hemisphere_surface(rng_t *g, v3 n)
+{
+    v3 p = random_in_unit_sphere(g);
+    v3 h = dot(p, n) > 0.0f ? p : neg(p);
+    return normalize(h);
+}
+
+/* ------------------------------------------------------------------------------------- */
+/* Scene view                                                                              */
+/* ------------------------------------------------------------------------------------- */
+typedef struct {
+    const rvcp_material_t *mat; uint32_t n_mat;
+    const rvcp_vertex_t *vtx; uint32_t n_vtx;
+    const rvcp_face_t *face; uint32_t n_face;
+    const uint32_t *lum; uint32_t n_lum;   /* packed u32 ids as uploaded */
+} scene_t;
+
+typedef struct { v3 o, d; float t_min, t_max; } ray_t;        /* :116-121 */
+typedef struct {                                                /* :123-133 */
+    float time; v3 pos, normal; uint32_t material_id; int outward;
+} hit_t;
+
+/* Luminous face id i as the shader reads it (:109-111). */
+static inline uint32_t lum_face_id(const scene_t *s, uint32_t i, int quirk)
+{
+    if (!quirk) return s->lum[i];
+    return (4u * i < s->n_lum) ? s->lum[4u * i] : 0u;
+}
+
+/* is_intersect_with_face, :238-280 */
+static int is_intersect_with_face(const scene_t *sc, const ray_t *ray, const rvcp_face_t *f,
+                                  hit_t *out)
+{
+    v3 v0 = ld3(sc->vtx[f->vertices[0]].position);
+    v3 v1 = ld3(sc->vtx[f->vertices[1]].position);
+    v3 v2 = ld3(sc->vtx[f->vertices[2]].position);
+    v3 e1 = sub(v1, v0), e2 = sub(v2, v0), s = sub(ray->o, v0);
+    v3 s1 = cross(ray->d, e2), s2 = cross(s, e1);
+    float f_ = 1.0f / dot(s1, e1);
+    float t = f_ * dot(s2, e2);
+    float b1 = f_ * dot(s1, s);
+    float b2 = f_ * dot(s2, ray->d);
+    if (b1 < 0 || 1 < b1 || b2 < 0 || 1 < b2 || 1 < b1 + b2) return 0;
+    if (t < ray->t_min || ray->t_max < t) return 0;
+    v3 n0 = ld3(sc->vtx[f->vertices[0]].normal);
+    v3 n1 = ld3(sc->vtx[f->vertices[1]].normal);
+    v3 n2 = ld3(sc->vtx[f->vertices[2]].normal);
+    v3 n = normalize(add(add(muls(n0, 1.0f - b1 - b2), muls(n1, b1)), muls(n2, b2)));
+    out->time = t;
+    out->pos = add(ray->o, muls(ray->d, t));
+    out->normal = n;
+    out->material_id = f->material_id;
+    out->outward = 1;
+    if (dot(n, ray->d) > 0.0f) { out->normal = neg(n); out->outward = 0; }
+    return 1;
+}
+
+/* get_intersection_with_scene, :283-298.  A miss leaves every field but `time`
+ * uninitialised in the shader; DESIGN.md §3.4 defines them (position = +inf, material 0). */
+static hit_t get_intersection_with_scene(const scene_t *sc, ray_t ray, uint64_t *trav)
+{
+    hit_t inter;
+    inter.time = ray.t_max + 1.0f;
+    inter.pos = mk(INFINITY, INFINITY, INFINITY);
+    inter.normal = mk(0, 0, 0);
+    inter.material_id = 0;
+    inter.outward = 1;
+    for (uint32_t i = 0; i < sc->n_face; i++) {
+        hit_t h;
+        if (is_intersect_with_face(sc, &ray, &sc->face[i], &h)) {
+            if (h.time <= ray.t_max) { ray.t_max = h.time; inter = h; }
+        }
+    }
+    (*trav)++;
+    return inter;
+}
+
+/* get_face_area, :302-307 */
+static float get_face_area(const scene_t *sc, const rvcp_face_t *f)
+{
+    v3 v0 = ld3(sc->vtx[f->vertices[0]].position);
+    v3 v1 = ld3(sc->vtx[f->vertices[1]].position);
+    v3 v2 = ld3(sc->vtx[f->vertices[2]].position);
+    return 0.5f * length(cross(sub(v1, v0), sub(v2, v0)));
+}
+
+/* sample_in_face, :311-329 */
+static void sample_in_face(const scene_t *sc, const rvcp_face_t *f, rng_t *g, hit_t *inter)
+{
+    v3 v0 = ld3(sc->vtx[f->vertices[0]].position);
+    v3 v1 = ld3(sc->vtx[f->vertices[1]].position);
+    v3 v2 = ld3(sc->vtx[f->vertices[2]].position);
+    float x = sqrtf(rand_next(g));
+    float y = rand_next(g);
+    inter->time = 0.0f;
+    inter->pos = add(add(muls(v0, 1.0f - x), muls(v1, x * (1.0f - y))), muls(v2, x * y));
+    inter->normal = normalize(ld3(sc->vtx[f->vertices[0]].normal));
+    inter->material_id = f->material_id;
+    inter->outward = 1;
+}
+
+/* sample_light_games101, :384-404.  Returns 0 when no light face exists (then `inter` is
+ * uninitialised in the shader; DESIGN.md §3.4: the NEE term is skipped). */
+static int sample_light_games101(const scene_t *sc, rng_t *g, int quirk, uint32_t n_lum_len,
+                                 hit_t *inter, float *pdf_light)
+{
+    float emit_area_sum = 0;
+    for (uint32_t i = 0; i < n_lum_len; i++)
+        emit_area_sum += get_face_area(sc, &sc->face[lum_face_id(sc, i, quirk)]);
+    float p = rand_next(g) * emit_area_sum;
+    *pdf_light = 1.0f / emit_area_sum;
+    emit_area_sum = 0.0f;
+    for (uint32_t i = 0; i < n_lum_len; i++) {
+        const rvcp_face_t *f = &sc->face[lum_face_id(sc, i, quirk)];
+        emit_area_sum += get_face_area(sc, f);
+        if (p <= emit_area_sum) { sample_in_face(sc, f, g, inter); return 1; }
+    }
+    return 0;
+}
+
+/* lambertian_brdf_eval, :338-350 */
+static inline v3 lambertian_brdf_eval(const rvcp_material_t *m, v3 wi, v3 normal)
+{
+    float cos_theta = dot(normal, wi);
+    if (cos_theta > 0.0f) return divs(ld3(m->albedo), PI_F);
+    return mk(0, 0, 0);
+}
+/* lambertian_brdf_pdf, :358-365 */
+static inline float lambertian_brdf_pdf(v3 wi, v3 normal)
+{
+    return dot(wi, normal) > 0.0f ? 0.5f / PI_F : 0.0f;
+}
+
+/* ray_trace_games101, :406-482 */
+static v3 ray_trace_games101(const scene_t *sc, const params_t *P, rng_t *g, ray_t ray,
+                             uint64_t *trav)
+{
+    v3 color = mk(0, 0, 0);
+    v3 attenuation = mk(1, 1, 1);
+    for (uint32_t depth = 0; depth < P->max_bounces; depth++) {
+        if (attenuation.x < P->att_stop && attenuation.y < P->att_stop &&
+            attenuation.z < P->att_stop) break;                                   /* :415 */
+
+        hit_t inter_p = get_intersection_with_scene(sc, ray, trav);               /* :421 */
+        if (inter_p.time > ray.t_max) { color = add(color, mk(0.1f, 0.1f, 0.1f)); break; }
+        const rvcp_material_t *material_p = &sc->mat[inter_p.material_id];        /* :422 */
+        if (material_p->ty == MATERIAL_LIGHT) {                                   /* :425 */
+            if (depth == 0) color = add(color, mulv(attenuation, ld3(material_p->albedo)));
+            break;
+        }
+        v3 p = inter_p.pos;
+
+        hit_t inter_x;                                                            /* :434 */
+        float pdf_light;
+        if (sample_light_games101(sc, g, P->quirk, sc->n_lum, &inter_x, &pdf_light)) {
+            const rvcp_material_t *material_x = &sc->mat[inter_x.material_id];
+            float dist = length(sub(inter_x.pos, p));
+            v3 ws = divs(sub(inter_x.pos, p), dist);
+            ray_t shadow = { add(p, muls(ws, P->eps)), ws, P->t_min, P->t_max };  /* :441 */
+            hit_t blocked = get_intersection_with_scene(sc, shadow, trav);
+            float dist_blocked = length(sub(blocked.pos, p));
+            if (fabsf(dist - dist_blocked) < P->eps) {                           /* :449 */
+                v3 f = lambertian_brdf_eval(material_p, ws, inter_p.normal);
+                v3 c = mulv(mulv(attenuation, ld3(material_x->albedo)), f);
+                c = muls(c, dot(inter_p.normal, ws));
+                c = muls(c, dot(inter_x.normal, neg(ws)));
+                c = divs(c, dist * dist * pdf_light);   /* pow(dist, 2.0) := dist*dist */
+                color = add(color, c);
+            }
+        }
+
+        if (rand_next(g) > P->rr) break;                                          /* :462 */
+
+        v3 wi = random_in_unit_hemisphere_surface(g, inter_p.normal);             /* :464 */
+        v3 f = lambertian_brdf_eval(material_p, wi, inter_p.normal);
+        float pdf = lambertian_brdf_pdf(wi, inter_p.normal);
+        float denom = fmaxf(0.1f, pdf) * P->rr;
+        v3 a = divs(muls(muls(f, 1.0f), dot(inter_p.normal, wi)), denom);
+        attenuation = mulv(attenuation, a);                                       /* :465 */
+
+        ray.o = add(inter_p.pos, muls(wi, P->eps));                               /* :473 */
+        ray.d = wi;
+        ray.t_min = P->t_min;
+        ray.t_max = P->t_max;
+    }
+    return color;
+}
+
+/* ------------------------------------------------------------------------------------- */
+/* Camera: sample_ray, :217-235                                                            */
+/* ------------------------------------------------------------------------------------- */
+typedef struct { v3 pos, fwd, up; float t_near, t_far, vfov; } cam_t;
+
+static cam_t cam_of(const rvcp_push_constant_t *pc)
+{
+    cam_t c;
+    c.pos = ld3(pc->camera.position);
+    c.up = ld3(pc->camera.up);
+    c.fwd = ld3(pc->camera.forward);
+    c.t_near = pc->camera.t_near;
+    c.t_far = pc->camera.t_far;
+    c.vfov = pc->camera.vertical_fov;
+    return c;
+}
+
+static ray_t sample_ray(const cam_t *c, float u_, float v_, float W, float H)
+{
+    float rad = c->vfov / 2.0f * PI_F / 180.0f;                 /* degree_to_radian :141 */
+    float h = 2.0f * c->t_near * tanf(rad);
+    float w = h * W / H;
+    v3 u = muls(normalize(cross(c->fwd, c->up)), w);
+    v3 v = muls(normalize(cross(c->fwd, u)), h);
+    v3 pos = add(c->pos, muls(c->fwd, c->t_near));
+    v3 uv_pos = add(add(pos, muls(u, u_ - 0.5f)), muls(v, v_ - 0.5f));
+    float t_coef = length(sub(uv_pos, c->pos)) / length(sub(pos, c->pos));
+    ray_t r = { c->pos, normalize(sub(uv_pos, c->pos)), c->t_near * t_coef, c->t_far * t_coef };
+    return r;
+}
+
+/* ------------------------------------------------------------------------------------- */
+/* Tone map: pow(clamp(c, 0, 1), 0.6) (:498) then UNORM8 store (:500).                     */
+/* u8 = #{k in 1..255 : c >= T[k]}, T[k] = float(((k-0.5)/255)^(1/0.6)).   */
+/* ------------------------------------------------------------------------------------- */
+static float g_gamma_T[256];
+static pthread_once_t g_gamma_once = PTHREAD_ONCE_INIT;
+static void gamma_init(void)
+{
+    g_gamma_T[0] = 0.0f;
+    for (int k = 1; k < 256; k++) g_gamma_T[k] = (float)pow((k - 0.5) / 255.0, 1.0 / 0.6);
+}
+uint8_t rvcp_oracle_gamma_u8(float c)
+{
+    pthread_once(&g_gamma_once, gamma_init);
+    float x = (c > 0.0f) ? ((c < 1.0f) ? c : 1.0f) : 0.0f;     /* clamp, NaN -> 0 */
+    int n = 0;
+    for (int k = 1; k < 256; k++) n += (x >= g_gamma_T[k]);
+    return (uint8_t)n;
+}
+float rvcp_oracle_gamma_threshold(int k)
+{
+    pthread_once(&g_gamma_once, gamma_init);
+    return (k >= 0 && k < 256) ? g_gamma_T[k] : 0.0f;
+}
+
+/* ------------------------------------------------------------------------------------- */
+/* main, :486-501, over a sub-rectangle of a W x H frame, multi-threaded by rows           */
+/* ------------------------------------------------------------------------------------- */
+typedef struct {
+    const scene_t *sc; const params_t *P; cam_t cam; float time;
+    uint32_t W, H, x0, y0, tw, th, tid, nthreads;
+    float *lin; uint8_t *rgba; uint64_t trav;
+} job_t;
+
+static void render_pixel(job_t *J, uint32_t x, uint32_t y, uint32_t out_idx)
+{
+    const float Wf = (float)J->W, Hf = (float)J->H;
+    float u_ = ((float)x + 0.5f) / Wf, v_ = ((float)y + 0.5f) / Hf;     /* :488 */
+    rng_t g;
+    srand_glsl(&g, J->time, u_, v_);                                    /* :489 */
+    ray_t ray = sample_ray(&J->cam, u_, v_, Wf, Hf);                    /* :491 */
+    v3 color = mk(0, 0, 0);
+    const float sppf = (float)J->P->spp;
+    for (uint32_t i = 0; i < J->P->spp; i++)                           /* :494-496 */
+        color = add(color, divs(ray_trace_games101(J->sc, J->P, &g, ray, &J->trav), sppf));
+    if (J->lin) {
+        J->lin[3 * (size_t)out_idx + 0] = color.x;
+        J->lin[3 * (size_t)out_idx + 1] = color.y;
+        J->lin[3 * (size_t)out_idx + 2] = color.z;
+    }
+    if (J->rgba) {
+        J->rgba[4 * (size_t)out_idx + 0] = rvcp_oracle_gamma_u8(color.x);
+        J->rgba[4 * (size_t)out_idx + 1] = rvcp_oracle_gamma_u8(color.y);
+        J->rgba[4 * (size_t)out_idx + 2] = rvcp_oracle_gamma_u8(color.z);
+        J->rgba[4 * (size_t)out_idx + 3] = 255;
+    }
+}
+
+/* Threads take 16-pixel chunks of the rectangle round-robin (balanced even for 1-row rects). */
+static void *render_rows(void *arg)
+{
+    job_t *J = (job_t *)arg;
+    const uint64_t n = (uint64_t)J->tw * J->th;
+    for (uint64_t c = (uint64_t)J->tid * 16u; c < n; c += (uint64_t)J->nthreads * 16u)
+        for (uint64_t i = c; i < c + 16u && i < n; i++) {
+            const uint32_t ty = (uint32_t)(i / J->tw), tx = (uint32_t)(i % J->tw);
+            render_pixel(J, J->x0 + tx, J->y0 + ty, (uint32_t)i);
+        }
+    return NULL;
+}
+
+/* Render the tw x th sub-rectangle at (x0, y0) of a W x H frame.  Output arrays are
+ * tw*th*3 floats / tw*th*4 bytes (either may be NULL).  Returns 0 or a negative error. */
+int rvcp_oracle_render(const rvcp_material_t *materials, uint32_t n_materials,
+                       const rvcp_vertex_t *vertices, uint32_t n_vertices,
+                       const rvcp_face_t *faces, uint32_t n_faces,
+                       const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
+                       const rvcp_push_constant_t *push, const rvcp_config_t *cfg,
+                       uint32_t W, uint32_t H, uint32_t x0, uint32_t y0, uint32_t tw,
+                       uint32_t th, float *out_linear, uint8_t *out_rgba8,
+                       uint64_t *out_traversals, int nthreads)
+{
+    if (!push || !cfg || !W || !H || x0 + tw > W || y0 + th > H) return RVCP_E_INVALID;
+    if (n_materials == 0 || !materials) return RVCP_E_INVALID;
+    for (uint32_t i = 0; i < n_faces; i++) {
+        for (int k = 0; k < 3; k++) if (faces[i].vertices[k] >= n_vertices) return RVCP_E_INVALID;
+        if (faces[i].material_id >= n_materials) return RVCP_E_INVALID;
+    }
+    for (uint32_t i = 0; i < n_lum_face_ids; i++)
+        if (lum_face_ids[i] >= n_faces) return RVCP_E_INVALID;
+    pthread_once(&g_gamma_once, gamma_init);
+
+    scene_t sc = { materials, n_materials, vertices, n_vertices, faces, n_faces,
+                   lum_face_ids, n_lum_face_ids };
+    params_t P = { cfg->spp, cfg->max_bounces, cfg->attenuation_stop_eps, cfg->ray_t_min,
+                   cfg->ray_t_max, cfg->rr_probability, cfg->eps, cfg->lum_id_std140_quirk };
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    job_t *jobs = (job_t *)calloc((size_t)nthreads, sizeof(job_t));
+    pthread_t *th_ids = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    if (!jobs || !th_ids) { free(jobs); free(th_ids); return RVCP_E_NOMEM; }
+    cam_t cam = cam_of(push);
+    for (int t = 0; t < nthreads; t++) {
+        job_t j = { &sc, &P, cam, push->time, W, H, x0, y0, tw, th, (uint32_t)t,
+                    (uint32_t)nthreads, out_linear, out_rgba8, 0 };
+        jobs[t] = j;
+    }
+    int started = 0;
+    for (int t = 1; t < nthreads; t++) {
+        if (pthread_create(&th_ids[t], NULL, render_rows, &jobs[t]) != 0) break;
+        started = t;
+    }
+    if (started < nthreads - 1) {        /* could not spawn: run the rest inline */
+        for (int t = started + 1; t < nthreads; t++) render_rows(&jobs[t]);
+    }
+    render_rows(&jobs[0]);
+    uint64_t trav = jobs[0].trav;
+    for (int t = 1; t <= started; t++) pthread_join(th_ids[t], NULL);
+    for (int t = 1; t < nthreads; t++) trav += jobs[t].trav;
+    if (out_traversals) *out_traversals = trav;
+    free(jobs);
+    free(th_ids);
+    return RVCP_OK;
+}
+
+/* ------------------------------------------------------------------------------------- */
+/* Known-answer-test helpers (tests/test_oracle_kat.py)                                    */
+/* ------------------------------------------------------------------------------------- */
+
+/* out[0] = seed after srand(time, (u, v)); out[1..n] = the first n rand() values. */
+void rvcp_oracle_rand_sequence(float time, float u, float v, int n, float *out)
+{
+    rng_t g;
+    srand_glsl(&g, time, u, v);
+    out[0] = g.seed;
+    for (int i = 0; i < n; i++) out[1 + i] = rand_next(&g);
+}
+
+/* Single ray-triangle test (is_intersect_with_face).  ray = {ox,oy,oz,dx,dy,dz,tmin,tmax},
+ * tri = 3 positions; out = {t, b1, b2} on hit.  Returns 1 on hit. */
+int rvcp_oracle_intersect(const float *ray, const float *tri, float *out)
+{
+    rvcp_vertex_t v[3];
+    memset(v, 0, sizeof v);
+    for (int k = 0; k < 3; k++) {
+        v[k].position[0] = tri[3 * k]; v[k].position[1] = tri[3 * k + 1];
+        v[k].position[2] = tri[3 * k + 2]; v[k].normal[1] = 1.0f;
+    }
+    rvcp_face_t f = { {0, 1, 2}, 0 };
+    scene_t sc = { NULL, 0, v, 3, &f, 1, NULL, 0 };
+    ray_t r = { mk(ray[0], ray[1], ray[2]), mk(ray[3], ray[4], ray[5]), ray[6], ray[7] };
+    hit_t h;
+    if (!is_intersect_with_face(&sc, &r, &f, &h)) return 0;
+    /* recover b1, b2 exactly as the shader computed them */
+    v3 e1 = sub(ld3(v[1].position), ld3(v[0].position));
+    v3 e2 = sub(ld3(v[2].position), ld3(v[0].position));
+    v3 s = sub(r.o, ld3(v[0].position));
+    v3 s1 = cross(r.d, e2), s2 = cross(s, e1);
+    float f_ = 1.0f / dot(s1, e1);
+    out[0] = h.time;
+    out[1] = f_ * dot(s1, s);
+    out[2] = f_ * dot(s2, r.d);
+    return 1;
+}
+
+/* Primary ray of pixel (x, y): out = {ox,oy,oz,dx,dy,dz,tmin,tmax}. */
+void rvcp_oracle_sample_ray(const rvcp_push_constant_t *push, uint32_t W, uint32_t H,
+                            uint32_t x, uint32_t y, float *out)
+{
+    cam_t cam = cam_of(push);
+    float u_ = ((float)x + 0.5f) / (float)W, v_ = ((float)y + 0.5f) / (float)H;
+    ray_t r = sample_ray(&cam, u_, v_, (float)W, (float)H);
+    out[0] = r.o.x; out[1] = r.o.y; out[2] = r.o.z;
+    out[3] = r.d.x; out[4] = r.d.y; out[5] = r.d.z;
+    out[6] = r.t_min; out[7] = r.t_max;
+}

@@ -1,0 +1,94 @@
+"""ctypes binding of librvcp (include/rvcp.h) -- the product's C-ABI.
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950)
+into ``csrc/build/librvcp.so``.  There is no fallback: if the library is missing,
+``load()`` raises, so nothing can silently run a CPU path in its place.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "csrc", "build", "librvcp.so")
+
+# rvcp_config_t (include/rvcp.h)
+CONFIG_DTYPE = np.dtype([("device", "<i4"), ("integrator", "<i4"), ("spp", "<u4"),
+                         ("max_bounces", "<u4"), ("attenuation_stop_eps", "<f4"),
+                         ("ray_t_min", "<f4"), ("ray_t_max", "<f4"), ("rr_probability", "<f4"),
+                         ("eps", "<f4"), ("lum_id_std140_quirk", "<i4"), ("_reserved", "<u4", 6)])
+STATS_DTYPE = np.dtype([("kernel_ms", "<f8"), ("traversals", "<u8"),
+                        ("traversals_executed", "<u8"), ("samples", "<u8"), ("faces", "<u4"),
+                        ("_reserved", "<u4", 3)])
+assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 48
+
+# Defaults == the shader's #defines (ray_tracer_games101_branch.comp:5-13).
+DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop_eps=0.05,
+                ray_t_min=0.01, ray_t_max=10000.0, rr_probability=0.8, eps=0.001,
+                lum_id_std140_quirk=1)
+
+# Error codes
+RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E_NOMEM = \
+    0, -1, -2, -3, -4, -5
+
+EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_create", "rvcp_destroy",
+            "rvcp_last_error", "rvcp_upload_scene", "rvcp_render", "rvcp_render_shard_async",
+            "rvcp_sync_stats", "rvcp_shard_rows", "rvcp_assemble_frame_async"]
+
+
+def make_config(**kw) -> np.ndarray:
+    cfg = np.zeros((), dtype=CONFIG_DTYPE)
+    vals = dict(DEFAULTS)
+    vals.update(kw)
+    for k, v in vals.items():
+        cfg[k] = v
+    return cfg
+
+
+class RvcpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rvcp error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load librvcp.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"librvcp.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    P, u32 = ctypes.c_void_p, ctypes.c_uint32
+    L.rvcp_version.restype = ctypes.c_char_p
+    L.rvcp_config_default.argtypes = [P]
+    L.rvcp_create.argtypes = [P, ctypes.POINTER(ctypes.c_void_p)]
+    L.rvcp_destroy.argtypes = [P]
+    L.rvcp_last_error.argtypes = [P]
+    L.rvcp_last_error.restype = ctypes.c_char_p
+    L.rvcp_upload_scene.argtypes = [P, P, u32, P, u32, P, u32, P, u32, P, u32, P, u32]
+    L.rvcp_render.argtypes = [P, P, u32, u32, P, P, P]
+    L.rvcp_render_shard_async.argtypes = [P, P, u32, u32, u32, u32, P, P, P]
+    L.rvcp_sync_stats.argtypes = [P, P]
+    L.rvcp_shard_rows.argtypes = [u32, u32, u32]
+    L.rvcp_shard_rows.restype = u32
+    L.rvcp_assemble_frame_async.argtypes = [P, P, u32, u32, u32, u32, P, P]
+    for name in ("rvcp_config_default", "rvcp_create", "rvcp_destroy", "rvcp_upload_scene",
+                 "rvcp_render", "rvcp_render_shard_async", "rvcp_sync_stats",
+                 "rvcp_assemble_frame_async"):
+        getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    return a.ctypes.data_as(ctypes.c_void_p)

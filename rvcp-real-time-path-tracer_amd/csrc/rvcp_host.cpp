@@ -1,0 +1,463 @@
+// rvcp_host.cpp -- C-ABI host runtime of librvcp (include/rvcp.h).
+//
+// Replaces the Vulkano runtime of the reference (src/ray_tracer/vulkan.rs): pipeline
+// creation (:576-603) -> rvcp_create, descriptor-set upload (:454-574) -> rvcp_upload_scene,
+// push constants + dispatch (:406-452) -> rvcp_render / rvcp_render_shard_async.
+//
+// Compiled with hipcc -ffp-contract=off: the frame constants it derives (camera basis,
+// light-area prefix sums, gamma thresholds) use the same float operations as the shader, so
+// the kernel's results stay bit-identical to the CPU oracle.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rvcp.h"
+#include "rvcp_internal.h"
+
+using namespace rvcp;
+
+struct rvcp_ctx {
+    rvcp_config_t cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int grid_capacity = 0;           // resident workgroups of the persistent kernel
+
+    // scene (device)
+    TriRecord *d_tri = nullptr;
+    rvcp_face_t *d_faces = nullptr;
+    rvcp_vertex_t *d_verts = nullptr;
+    MatRecord *d_mats = nullptr;
+    LightRecord *d_lights = nullptr;
+    float *d_gamma = nullptr;
+    unsigned long long *d_counters = nullptr;
+    uint32_t n_faces = 0, n_lights = 0, n_mats = 0, n_verts = 0;
+    float light_total = 0.0f, light_pdf = 0.0f;
+    bool has_scene = false;
+
+    // staging for the synchronous host API
+    uint32_t *d_rgba = nullptr;
+    float *d_lin = nullptr;
+    size_t cap_rgba = 0, cap_lin = 0;
+
+    // last launch
+    bool pending = false;
+    bool last_trivial = false;
+    uint64_t last_pixels = 0;
+    uint32_t last_spp = 0;
+
+    std::string err;
+};
+
+namespace {
+
+thread_local std::string g_create_error;
+
+int fail(rvcp_ctx *ctx, int code, const std::string &msg)
+{
+    if (ctx) ctx->err = msg;
+    else g_create_error = msg;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                  \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail((ctx), RVCP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- host-side vec3 with the shader's evaluation order ----
+struct h3 { float x, y, z; };
+inline h3 mk(float x, float y, float z) { return h3{x, y, z}; }
+inline h3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
+inline h3 add(h3 a, h3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline h3 sub(h3 a, h3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline h3 muls(h3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+inline float dot(h3 a, h3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline h3 cross(h3 a, h3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+inline float length(h3 a) { return std::sqrt(dot(a, a)); }
+inline h3 normalize(h3 a) { return muls(a, 1.0f / std::sqrt(dot(a, a))); }
+inline void st3(float *d, h3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; }
+
+// get_face_area, ray_tracer_games101_branch.comp:302-307
+float face_area(const rvcp_vertex_t *v, const rvcp_face_t &f)
+{
+    h3 v0 = ld3(v[f.vertices[0]].position), v1 = ld3(v[f.vertices[1]].position);
+    h3 v2 = ld3(v[f.vertices[2]].position);
+    return 0.5f * length(cross(sub(v1, v0), sub(v2, v0)));
+}
+
+// sample_ray's frame constants, :217-227
+void camera_constants(const rvcp_push_constant_t &pc, uint32_t W, uint32_t H, FrameArgs &A)
+{
+    const float PI = 3.1415926f;
+    h3 cpos = ld3(pc.camera.position), up = ld3(pc.camera.up), fwd = ld3(pc.camera.forward);
+    const float rad = pc.camera.vertical_fov / 2.0f * PI / 180.0f;   // degree_to_radian :141
+    const float h = 2.0f * pc.camera.t_near * std::tan(rad);
+    const float w = h * (float)W / (float)H;
+    h3 u = muls(normalize(cross(fwd, up)), w);
+    h3 v = muls(normalize(cross(fwd, u)), h);
+    h3 pos = add(cpos, muls(fwd, pc.camera.t_near));
+    st3(A.cam_pos, cpos);
+    st3(A.u, u);
+    st3(A.v, v);
+    st3(A.pos, pos);
+    A.base_len = length(sub(pos, cpos));
+    A.t_near = pc.camera.t_near;
+    A.t_far = pc.camera.t_far;
+    A.time = pc.time;
+}
+
+template <typename T>
+int dev_upload(rvcp_ctx *ctx, T **dst, const void *src, size_t n)
+{
+    if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
+    const size_t bytes = n ? n * sizeof(T) : sizeof(T);
+    HIP_TRY(ctx, hipMalloc((void **)dst, bytes));
+    if (n) HIP_TRY(ctx, hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return RVCP_OK;
+}
+
+void free_scene(rvcp_ctx *ctx)
+{
+    (void)hipFree(ctx->d_tri); ctx->d_tri = nullptr;
+    (void)hipFree(ctx->d_faces); ctx->d_faces = nullptr;
+    (void)hipFree(ctx->d_verts); ctx->d_verts = nullptr;
+    (void)hipFree(ctx->d_mats); ctx->d_mats = nullptr;
+    (void)hipFree(ctx->d_lights); ctx->d_lights = nullptr;
+    ctx->has_scene = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *rvcp_version(void) { return "rvcp-mi355x 0.1.0 (gfx950)"; }
+
+int rvcp_config_default(rvcp_config_t *cfg)
+{
+    if (!cfg) return RVCP_E_INVALID;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->device = 0;
+    cfg->integrator = RVCP_INTEGRATOR_GAMES101;
+    cfg->spp = 20;                      // ray_tracer_games101_branch.comp:8
+    cfg->max_bounces = 15;              // :9
+    cfg->attenuation_stop_eps = 0.05f;  // :10
+    cfg->ray_t_min = 0.01f;             // :11
+    cfg->ray_t_max = 10000.0f;          // :12
+    cfg->rr_probability = 0.8f;         // :13
+    cfg->eps = 0.001f;                  // :5
+    cfg->lum_id_std140_quirk = 1;
+    return RVCP_OK;
+}
+
+const char *rvcp_last_error(const rvcp_ctx_t *ctx)
+{
+    return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
+{
+    if (!cfg || !out_ctx) return fail(nullptr, RVCP_E_INVALID, "null argument");
+    *out_ctx = nullptr;
+    if (cfg->integrator != RVCP_INTEGRATOR_GAMES101)
+        return fail(nullptr, RVCP_E_UNSUPPORTED, "unsupported integrator");
+    if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
+    if (!(cfg->ray_t_max < 16777216.0f))
+        return fail(nullptr, RVCP_E_INVALID, "ray_t_max must be < 2^24 (miss test t_max + 1)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(nullptr, RVCP_E_HIP, "no HIP device");
+    if (cfg->device < 0 || cfg->device >= ndev)
+        return fail(nullptr, RVCP_E_INVALID, "device ordinal out of range");
+
+    rvcp_ctx *ctx = new (std::nothrow) rvcp_ctx();
+    if (!ctx) return fail(nullptr, RVCP_E_NOMEM, "out of memory");
+    ctx->cfg = *cfg;
+    ctx->device = cfg->device;
+    auto bail = [&](int rc) {
+        g_create_error = ctx->err;
+        rvcp_destroy(ctx);
+        return rc;
+    };
+    int rc;
+    if (hipSetDevice(ctx->device) != hipSuccess) return bail(fail(ctx, RVCP_E_HIP, "hipSetDevice"));
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess)
+        return bail(fail(ctx, RVCP_E_HIP, "stream/event creation failed"));
+
+    // Gamma thresholds T[k] = float(((k - 0.5) / 255)^(1/0.6)), DESIGN.md §3.3
+    float T[257];
+    T[0] = 0.0f;
+    for (int k = 1; k < 256; k++) T[k] = (float)std::pow((k - 0.5) / 255.0, 1.0 / 0.6);
+    T[256] = INFINITY;
+    if ((rc = dev_upload<float>(ctx, &ctx->d_gamma, T, 257)) != RVCP_OK) return bail(rc);
+    if (hipMalloc((void **)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess)
+        return bail(fail(ctx, RVCP_E_HIP, "hipMalloc counters"));
+
+    int per_cu = 0, cus = 0;
+    if (rvcp_games101_occupancy(&per_cu) != 0 || per_cu <= 0) per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+        cus = 256;
+    ctx->grid_capacity = per_cu * cus;
+    *out_ctx = ctx;
+    return RVCP_OK;
+}
+
+int rvcp_destroy(rvcp_ctx_t *ctx)
+{
+    if (!ctx) return RVCP_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_scene(ctx);
+    (void)hipFree(ctx->d_gamma);
+    (void)hipFree(ctx->d_counters);
+    (void)hipFree(ctx->d_rgba);
+    (void)hipFree(ctx->d_lin);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return RVCP_OK;
+}
+
+int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_t n_materials,
+                      const rvcp_vertex_t *vertices, uint32_t n_vertices,
+                      const rvcp_face_t *faces, uint32_t n_faces,
+                      const rvcp_sphere_t *spheres, uint32_t n_spheres,
+                      const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
+                      const uint32_t *lum_sphere_ids, uint32_t n_lum_sphere_ids)
+{
+    (void)spheres; (void)n_spheres; (void)lum_sphere_ids; (void)n_lum_sphere_ids;
+    if (!ctx) return RVCP_E_INVALID;
+    if (!materials || n_materials == 0) return fail(ctx, RVCP_E_INVALID, "need >= 1 material");
+    if ((n_vertices && !vertices) || (n_faces && !faces) || (n_lum_face_ids && !lum_face_ids))
+        return fail(ctx, RVCP_E_INVALID, "null array with nonzero length");
+    for (uint32_t i = 0; i < n_faces; i++) {
+        for (int k = 0; k < 3; k++)
+            if (faces[i].vertices[k] >= n_vertices)
+                return fail(ctx, RVCP_E_INVALID, "face " + std::to_string(i) + " vertex index out of range");
+        if (faces[i].material_id >= n_materials)
+            return fail(ctx, RVCP_E_INVALID, "face " + std::to_string(i) + " material out of range");
+    }
+    for (uint32_t i = 0; i < n_lum_face_ids; i++)
+        if (lum_face_ids[i] >= n_faces)
+            return fail(ctx, RVCP_E_INVALID, "luminous face id out of range");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+
+    // triangles: v0, e1 = v1 - v0, e2 = v2 - v0 (:243-248)
+    std::vector<TriRecord> tri(n_faces);
+    for (uint32_t i = 0; i < n_faces; i++) {
+        h3 v0 = ld3(vertices[faces[i].vertices[0]].position);
+        h3 v1 = ld3(vertices[faces[i].vertices[1]].position);
+        h3 v2 = ld3(vertices[faces[i].vertices[2]].position);
+        std::memset(&tri[i], 0, sizeof(TriRecord));
+        st3(tri[i].v0, v0);
+        st3(tri[i].e1, sub(v1, v0));
+        st3(tri[i].e2, sub(v2, v0));
+    }
+    std::vector<MatRecord> mats(n_materials);
+    for (uint32_t i = 0; i < n_materials; i++) {
+        std::memcpy(mats[i].albedo, materials[i].albedo, sizeof(float) * 3);
+        mats[i].ty = materials[i].ty;
+    }
+    // light table (sample_light_games101, :384-404) with the std140 id quirk (:109-111)
+    const bool quirk = ctx->cfg.lum_id_std140_quirk != 0;
+    std::vector<LightRecord> lights(n_lum_face_ids ? n_lum_face_ids : 1);
+    float total = 0.0f;
+    for (uint32_t i = 0; i < n_lum_face_ids; i++) {
+        const uint32_t id = quirk ? ((4u * i < n_lum_face_ids) ? lum_face_ids[4u * i] : 0u)
+                                  : lum_face_ids[i];
+        total += face_area(vertices, faces[id]);
+    }
+    float run = 0.0f;
+    for (uint32_t i = 0; i < n_lum_face_ids; i++) {
+        const uint32_t id = quirk ? ((4u * i < n_lum_face_ids) ? lum_face_ids[4u * i] : 0u)
+                                  : lum_face_ids[i];
+        const rvcp_face_t &f = faces[id];
+        run += face_area(vertices, f);
+        LightRecord &L = lights[i];
+        std::memset(&L, 0, sizeof(L));
+        L.cum = run;
+        L.face = id;
+        std::memcpy(L.v0, vertices[f.vertices[0]].position, 12);
+        std::memcpy(L.v1, vertices[f.vertices[1]].position, 12);
+        std::memcpy(L.v2, vertices[f.vertices[2]].position, 12);
+        st3(L.n, normalize(ld3(vertices[f.vertices[0]].normal)));
+        std::memcpy(L.le, materials[f.material_id].albedo, 12);
+    }
+
+    free_scene(ctx);
+    int rc;
+    if ((rc = dev_upload<TriRecord>(ctx, &ctx->d_tri, tri.data(), n_faces)) ||
+        (rc = dev_upload<rvcp_face_t>(ctx, &ctx->d_faces, faces, n_faces)) ||
+        (rc = dev_upload<rvcp_vertex_t>(ctx, &ctx->d_verts, vertices, n_vertices)) ||
+        (rc = dev_upload<MatRecord>(ctx, &ctx->d_mats, mats.data(), n_materials)) ||
+        (rc = dev_upload<LightRecord>(ctx, &ctx->d_lights, lights.data(), n_lum_face_ids)))
+        return rc;
+    ctx->n_faces = n_faces;
+    ctx->n_verts = n_vertices;
+    ctx->n_mats = n_materials;
+    ctx->n_lights = n_lum_face_ids;
+    ctx->light_total = total;
+    ctx->light_pdf = 1.0f / total;
+    ctx->has_scene = true;
+    return RVCP_OK;
+}
+
+uint32_t rvcp_shard_rows(uint32_t height, uint32_t shard_index, uint32_t shard_count)
+{
+    if (shard_count == 0 || shard_index >= shard_count) return 0;
+    const uint32_t stripes = (height + 7) / 8;
+    uint32_t rows = 0;
+    for (uint32_t s = shard_index; s < stripes; s += shard_count)
+        rows += (s + 1) * 8 <= height ? 8 : height - s * 8;
+    return rows;
+}
+
+int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+                            uint32_t height, uint32_t shard_index, uint32_t shard_count,
+                            void *d_rgba8, void *d_linear_rgb, void *stream)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!push || !d_rgba8 || width == 0 || height == 0 || shard_count == 0 ||
+        shard_index >= shard_count)
+        return fail(ctx, RVCP_E_INVALID, "invalid render arguments");
+    if ((uint64_t)width * height >= (1ull << 31))
+        return fail(ctx, RVCP_E_INVALID, "frame too large (W*H must be < 2^31)");
+    if (!ctx->has_scene) return fail(ctx, RVCP_E_NO_SCENE, "render before rvcp_upload_scene");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+
+    const uint32_t rows = rvcp_shard_rows(height, shard_index, shard_count);
+    FrameArgs A;
+    std::memset(&A, 0, sizeof(A));
+    camera_constants(*push, width, height, A);
+    A.width = width;
+    A.height = height;
+    A.shard_index = shard_index;
+    A.shard_count = shard_count;
+    A.n_pixels = rows * width;
+    A.spp = ctx->cfg.spp;
+    A.max_bounces = ctx->cfg.max_bounces;
+    A.att_stop = ctx->cfg.attenuation_stop_eps;
+    A.t_min = ctx->cfg.ray_t_min;
+    A.t_max = ctx->cfg.ray_t_max;
+    A.rr = ctx->cfg.rr_probability;
+    A.eps = ctx->cfg.eps;
+    A.n_faces = ctx->n_faces;
+    A.n_lights = ctx->n_lights;
+    A.light_total = ctx->light_total;
+    A.light_pdf = ctx->light_pdf;
+    A.want_linear = d_linear_rgb ? 1u : 0u;
+
+    // With MAX_BOUNCES == 0 or ATTENUATION_STOP_EPS > 1 every sample returns 0 before its
+    // first traversal (:413-419): the frame is black.
+    const bool trivial = A.max_bounces == 0 || 1.0f < A.att_stop;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(unsigned long long), s));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
+    if (A.n_pixels > 0) {
+        int rc;
+        if (trivial) {
+            rc = rvcp_launch_fill((uint32_t *)d_rgba8, (float *)d_linear_rgb, A.n_pixels,
+                                  0xFF000000u, s);
+        } else {
+            const uint32_t waves_needed = (A.n_pixels + kChunk - 1) / kChunk;
+            uint32_t blocks = (waves_needed + (kBlock / kWave) - 1) / (kBlock / kWave);
+            if (blocks > (uint32_t)ctx->grid_capacity) blocks = (uint32_t)ctx->grid_capacity;
+            if (blocks == 0) blocks = 1;
+            A.static_chunks = blocks * (kBlock / kWave) * kChunk;
+            rc = rvcp_launch_games101(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts, ctx->d_mats,
+                                      ctx->d_lights, ctx->d_gamma, (uint32_t *)d_rgba8,
+                                      (float *)d_linear_rgb, ctx->d_counters, blocks, s);
+        }
+        if (rc != 0) return fail(ctx, RVCP_E_HIP, std::string("kernel launch failed: ") +
+                                                      hipGetErrorString(hipGetLastError()));
+    }
+    HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
+    ctx->pending = true;
+    ctx->last_trivial = trivial;
+    ctx->last_pixels = A.n_pixels;
+    ctx->last_spp = A.spp;
+    return RVCP_OK;
+}
+
+int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!ctx->pending) return fail(ctx, RVCP_E_INVALID, "no render in flight");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ev1));
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        float ms = 0.0f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        unsigned long long c[4] = {0, 0, 0, 0};
+        HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+        stats->kernel_ms = ms;
+        stats->traversals_executed = c[0];
+        // the reference re-traces the (RNG-independent) primary ray in every sample
+        stats->traversals = ctx->last_trivial ? 0 : c[0] + ctx->last_pixels * (ctx->last_spp - 1);
+        stats->samples = ctx->last_pixels * ctx->last_spp;
+        stats->faces = ctx->n_faces;
+    }
+    return RVCP_OK;
+}
+
+int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+                uint32_t height, uint8_t *out_rgba8, float *out_linear_rgb, rvcp_stats_t *stats)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!out_rgba8) return fail(ctx, RVCP_E_INVALID, "out_rgba8 is required");
+    if (width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 31))
+        return fail(ctx, RVCP_E_INVALID, "invalid frame size");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t npx = (size_t)width * height;
+    if (ctx->cap_rgba < npx) {
+        (void)hipFree(ctx->d_rgba);
+        ctx->d_rgba = nullptr;
+        ctx->cap_rgba = 0;
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_rgba, npx * 4));
+        ctx->cap_rgba = npx;
+    }
+    if (out_linear_rgb && ctx->cap_lin < npx) {
+        (void)hipFree(ctx->d_lin);
+        ctx->d_lin = nullptr;
+        ctx->cap_lin = 0;
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_lin, npx * 12));
+        ctx->cap_lin = npx;
+    }
+    int rc = rvcp_render_shard_async(ctx, push, width, height, 0, 1, ctx->d_rgba,
+                                     out_linear_rgb ? ctx->d_lin : nullptr, ctx->stream);
+    if (rc != RVCP_OK) return rc;
+    if ((rc = rvcp_sync_stats(ctx, stats)) != RVCP_OK) return rc;
+    HIP_TRY(ctx, hipMemcpy(out_rgba8, ctx->d_rgba, npx * 4, hipMemcpyDeviceToHost));
+    if (out_linear_rgb) HIP_TRY(ctx, hipMemcpy(out_linear_rgb, ctx->d_lin, npx * 12, hipMemcpyDeviceToHost));
+    return RVCP_OK;
+}
+
+int rvcp_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t slot_rows,
+                              uint32_t width, uint32_t height, uint32_t shard_count,
+                              void *d_frame, void *stream)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!d_gathered || !d_frame || width == 0 || height == 0 || shard_count == 0)
+        return fail(ctx, RVCP_E_INVALID, "invalid assemble arguments");
+    for (uint32_t k = 0; k < shard_count; k++)
+        if (rvcp_shard_rows(height, k, shard_count) > slot_rows)
+            return fail(ctx, RVCP_E_INVALID, "slot_rows smaller than a shard");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    if (rvcp_launch_assemble((const uint32_t *)d_gathered, slot_rows, width, height, shard_count,
+                             (uint32_t *)d_frame, s) != 0)
+        return fail(ctx, RVCP_E_HIP, "assemble launch failed");
+    return RVCP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// rvcp_internal.h -- device-side data layout shared by the host runtime (rvcp_host.cpp) and
+// the gfx950 kernels (rvcp_kernels.hip).  Not part of the C-ABI.
+#pragma once
+
+#include <stdint.h>
+
+namespace rvcp {
+
+// Wave width on CDNA4.
+constexpr int kWave = 64;
+// Threads per workgroup of the path-tracing kernel (4 independent waves).
+constexpr int kBlock = 256;
+// Pixels a wave takes from the frame queue per atomic.
+constexpr uint32_t kChunk = 64;
+
+// One triangle as the brute-force scan reads it: v0, e1 = v1 - v0, e2 = v2 - v0, computed on
+// the host with the same float subtractions the shader performs per test
+// (ray_tracer_games101_branch.comp:247-248), so the scan is bit-identical while reading
+// 36 algorithmic bytes per test.  Padded to 48 B (three 16-B rows).
+struct alignas(16) TriRecord {
+    float v0[3];
+    float e1[3];
+    float e2[3];
+    float pad[3];
+};
+static_assert(sizeof(TriRecord) == 48, "TriRecord is 48 B");
+
+// One entry of the light table: a luminous face as sample_light_games101 sees it
+// (ray_tracer_games101_branch.comp:384-404), with the std140 id quirk already applied.
+struct alignas(16) LightRecord {
+    float cum;          // running emit_area_sum after this entry (second loop, :396-399)
+    uint32_t face;      // face index
+    float pad0[2];
+    float v0[4];        // positions of the face's three vertices (sample_in_face :315-317)
+    float v1[4];
+    float v2[4];
+    float n[4];         // normalize(vertices[face.x].normal)  (:325)
+    float le[4];        // materials[face.material_id].albedo  (:437)
+};
+static_assert(sizeof(LightRecord) == 96, "LightRecord is 96 B");
+
+// Per-material record: albedo + type (MaterialBuffer, :74-83).
+struct alignas(16) MatRecord {
+    float albedo[3];
+    uint32_t ty;
+};
+
+// Frame-constant parameters of one render launch.
+struct FrameArgs {
+    // camera, precomputed on the host exactly as sample_ray (:217-235) computes it
+    float cam_pos[3];
+    float u[3];          // normalize(cross(fwd, up)) * w
+    float v[3];          // normalize(cross(fwd, u)) * h
+    float pos[3];        // cam_pos + fwd * t_near
+    float base_len;      // length(pos - cam_pos)
+    float t_near, t_far;
+    float time;          // push-constant time (RNG seed input)
+    uint32_t width, height;
+    uint32_t shard_index, shard_count;
+    uint32_t n_pixels;   // pixels owned by this shard (rows * width)
+    uint32_t spp, max_bounces;
+    float att_stop, t_min, t_max, rr, eps;
+    uint32_t n_faces, n_lights;
+    float light_total, light_pdf;
+    uint32_t static_chunks;  // pixels handed out statically (one chunk per wave)
+    uint32_t want_linear;
+};
+
+}  // namespace rvcp
+
+// Launchers (defined in rvcp_kernels.hip), called by rvcp_host.cpp.
+extern "C" {
+int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
+                         const void *faces, const void *verts, const rvcp::MatRecord *mats,
+                         const rvcp::LightRecord *lights, const float *gamma_t,
+                         uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
+                         uint32_t grid_blocks, void *stream);
+int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows, uint32_t width,
+                         uint32_t height, uint32_t shard_count, uint32_t *frame, void *stream);
+int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n_pixels, uint32_t rgba,
+                     void *stream);
+int rvcp_games101_occupancy(int *blocks_per_cu);
+}

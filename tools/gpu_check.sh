@@ -1,0 +1,42 @@
+#!/usr/bin/env bash
+# GPU-box check: build, smoke, gpu tests, bench, rocprofv3 kernel trace.
+# Each GPU step has its own time limit; a fault/abort/timeout stops the script.
+# Usage: tools/gpu_check.sh [tag] [steps...]   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-"smoke tests bench prof"}
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # run <name> <timeout> cmd...
+    local name=$1 lim=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"
+    tail -n 25 "$OUT/$name.log"
+    case $rc in
+        0|1) return 0 ;;            # 1 = test failures / python error: keep going
+        *) echo "STOP: $name exited $rc"; exit $rc ;;
+    esac
+}
+
+echo "=== build"
+python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { tail -30 "$OUT/build.log"; exit 3; }
+rocm-smi --showproductname > "$OUT/rocm-smi.txt" 2>&1 || true
+lscpu > "$OUT/lscpu.txt" 2>&1 || true
+
+for s in $STEPS; do
+    case $s in
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
+        bench2) run bench_c2 300 python bench.py --workload c2 --steps 50 --warmup 5 --no-cpu-baseline ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+        pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    esac
+done
+echo "=== done"
