@@ -106,9 +106,17 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    # Rehearsal (RVCP_BENCH_REHEARSAL=1): every rank on device 0 and a gloo gather through host
+    # memory, to exercise the N>1 code path on a 1-GPU box.  Never used for reported numbers.
+    rehearsal = os.environ.get("RVCP_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     wl = workload(args.workload, world)
     W, H, spp = wl["W"], wl["H"], wl["spp"]
@@ -125,8 +133,6 @@ def main():
     slot = max(rvcp_amd.shard_rows(H, k, world) for k in range(world))
     dev = torch.device("cuda", local_rank)
     shard_buf = torch.zeros((slot, W), dtype=torch.int32, device=dev)
-    gathered = [torch.zeros((slot, W), dtype=torch.int32, device=dev) for _ in range(world)] \
-        if (world > 1 and rank == 0) else None
     frame = torch.zeros((H, W), dtype=torch.int32, device=dev) if rank == 0 else None
     gat_flat = torch.zeros((world, slot, W), dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream().cuda_stream
@@ -138,10 +144,13 @@ def main():
             return st
         rt.render_shard_async(push, W, H, rank, world, shard_buf.data_ptr(), stream=stream)
         st = rt.sync_stats()
-        dist.gather(shard_buf, gathered if rank == 0 else None, dst=0)
+        if rehearsal:
+            got = rvcp_amd.frame.gather_shards(shard_buf.cpu(), rank, world, dst=0)
+            if rank == 0:
+                gat_flat.copy_(torch.stack(got))
+        else:
+            rvcp_amd.frame.gather_shards(shard_buf, rank, world, dst=0, out=gat_flat)   # RCCL
         if rank == 0:
-            for k in range(world):
-                gat_flat[k].copy_(gathered[k])
             rt.assemble_frame_async(gat_flat.data_ptr(), slot, W, H, world, frame.data_ptr(),
                                     stream=stream)
         return st
@@ -165,7 +174,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -179,6 +188,15 @@ def main():
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
     tests_per_s = trav / args.steps * n_faces / avg_kernel_s
     exec_tests_per_s = trav_exec / args.steps * n_faces / avg_kernel_s
+
+    frame_check = None
+    if world > 1 and rank == 0:
+        # the assembled N-rank frame must be bit-identical to a 1-rank render (outside timing)
+        single = torch.zeros((H, W), dtype=torch.int32, device=dev)
+        rt.render_shard_async(push, W, H, 0, 1, single.data_ptr(), stream=stream)
+        rt.sync_stats()
+        torch.cuda.synchronize()
+        frame_check = bool(torch.equal(single, frame))
 
     if args.save_frame and rank == 0:
         np.save(args.save_frame, frame.cpu().numpy().view(np.uint8).reshape(H, W, 4))
@@ -200,7 +218,7 @@ def main():
             "data": "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)",
             "config": {"workload": wl["workload"], "width": W, "height": H, "spp": spp,
                        "faces": n_faces, "parallelism": f"pixel-stripes x{world}",
-                       "gather": "rccl" if world > 1 else "none"},
+                       "gather": ("gloo-rehearsal" if rehearsal else "rccl") if world > 1 else "none"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
@@ -215,6 +233,8 @@ def main():
                          "executed_tests_per_s": round(exec_tests_per_s, 1)},
             "cpu_baseline": None,
         }
+        if frame_check is not None:
+            out["config"]["assembled_frame_bitexact_vs_1gpu"] = frame_check
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(sc, cfg_kw, W, H, threads)

@@ -27,7 +27,7 @@ extern "C" {
 #endif
 
 /* ---------------------------------------------------------------------------------------
- * Upload structs (byte-identical to the reference; static_asserts in rvcp_layout_check.c)
+ * Upload structs (byte-identical to the reference; RVCP_STATIC_ASSERTs below)
  * ------------------------------------------------------------------------------------- */
 
 /* == AlignedCamera, src/ray_tracer/scene/camera.rs:27-37 (64 B).
@@ -125,7 +125,9 @@ typedef struct rvcp_stats {
                                          are reused across a pixel's samples) */
     uint64_t samples;                 /* pixels * spp */
     uint32_t faces;                   /* F, triangles tested per traversal */
-    uint32_t _reserved[3];
+    uint32_t _reserved;
+    uint64_t wave_iterations;         /* wave-level trace iterations; lane utilisation of the
+                                         scan = traversals_executed / (64 * wave_iterations) */
 } rvcp_stats_t;
 
 /* Layout checks: sizes/offsets the reference's Rust structs and std140/std430 blocks imply. */

@@ -21,7 +21,7 @@ CONFIG_DTYPE = np.dtype([("device", "<i4"), ("integrator", "<i4"), ("spp", "<u4"
                          ("eps", "<f4"), ("lum_id_std140_quirk", "<i4"), ("_reserved", "<u4", 6)])
 STATS_DTYPE = np.dtype([("kernel_ms", "<f8"), ("traversals", "<u8"),
                         ("traversals_executed", "<u8"), ("samples", "<u8"), ("faces", "<u4"),
-                        ("_reserved", "<u4", 3)])
+                        ("_reserved", "<u4"), ("wave_iterations", "<u8")])
 assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 48
 
 # Defaults == the shader's #defines (ray_tracer_games101_branch.comp:5-13).
@@ -56,6 +56,25 @@ class RvcpError(RuntimeError):
 _lib = None
 
 
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm bundles its own libamdhip64.so and NEEDs it by the unversioned name, while
+    librvcp NEEDs libamdhip64.so.7.  If librvcp loaded first, a later `import torch` would
+    load a SECOND HIP runtime that sees no GPU.  Preloading torch's copy (soname
+    libamdhip64.so.7) makes both resolve to one runtime whatever the import order, so device
+    pointers and streams from torch are valid in librvcp.  RVCP_HIP_RUNTIME=system skips it."""
+    if os.environ.get("RVCP_HIP_RUNTIME") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+            f = os.path.join(d, "lib", name)
+            if os.path.exists(f):
+                ctypes.CDLL(f, mode=ctypes.RTLD_GLOBAL)
+
+
 def load():
     """Load librvcp.so (raises if it has not been built)."""
     global _lib
@@ -63,6 +82,7 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"librvcp.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    _share_torch_hip_runtime()
     L = ctypes.CDLL(LIB_PATH)
     P, u32 = ctypes.c_void_p, ctypes.c_uint32
     L.rvcp_version.restype = ctypes.c_char_p

@@ -406,6 +406,7 @@ int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         stats->traversals = ctx->last_trivial ? 0 : c[0] + ctx->last_pixels * (ctx->last_spp - 1);
         stats->samples = ctx->last_pixels * ctx->last_spp;
         stats->faces = ctx->n_faces;
+        stats->wave_iterations = c[2];
     }
     return RVCP_OK;
 }

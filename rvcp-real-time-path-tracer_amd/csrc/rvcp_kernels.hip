@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
 
     // ---- lane state ----
     int action = A_NEED, kind = K_PRIMARY;
-    uint32_t pix = 0, k = 0, depth = 0, trav = 0;
+    uint32_t pix = 0, k = 0, depth = 0, trav = 0, waves_iter = 0;
     float seed = 0.0f, ridx = 0.0f;
     f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
     f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0);   // cached primary hit (surface)
@@ -286,6 +286,7 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
             if (!__any(action == A_RR || action == A_END || action == A_SURF)) break;
         }
         if (!__any(action == A_TRACE)) break;
+        waves_iter += 1;
 
         // ============ trace: brute-force nearest hit (:283-298, :238-260) ============
         int best = -1;
@@ -386,7 +387,10 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
     // executed traversals: one atomic per wave
     unsigned long long t64 = trav;
     for (int off = 32; off >= 1; off >>= 1) t64 += __shfl_xor(t64, off);
-    if (lane == 0) atomicAdd(&counters[0], t64);
+    if (lane == 0) {
+        atomicAdd(&counters[0], t64);
+        atomicAdd(&counters[2], (unsigned long long)waves_iter);
+    }
 }
 
 // Frame assembly after the RCCL gather: slot k holds shard k's stripes packed.

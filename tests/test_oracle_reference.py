@@ -1,0 +1,98 @@
+"""Pinning the CPU oracle (no GPU).
+
+1. Against the reference's only rendered output: the README screenshot (1024^2, SPP=30,
+   rendered by ray_tracer_games101_branch.comp on an RTX 3060).  Its driver sin() differs
+   from ours, so only statistics can match: 32x32-pixel block means of the 8-bit image
+   (fixture tests/golden/readme_blockmeans.npz, made by tests/golden/make_readme_fixture.py).
+2. Against tests/pyref.py, an independent pure-Python restatement, bit for bit, per pixel.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import pyref
+import rvcp_amd
+from conftest import block_means, readme_blocks, scene_arrays
+
+TIME = 123.0
+
+
+def _rms_vs_readme(rgba):
+    b32, _ = readme_blocks()
+    ours = block_means(rgba, 32)
+    ok = np.isfinite(b32)
+    return float(np.sqrt(np.mean((ours[ok] - b32[ok]) ** 2))), (ours[ok] - b32[ok]).reshape(-1, 3).mean(0)
+
+
+@pytest.fixture(scope="module")
+def oracle_256(cornell_arrays, cornell):
+    out = {}
+    for quirk in (1, 0):
+        cfg = rvcp_amd.abi.make_config(spp=30, lum_id_std140_quirk=quirk)
+        out[quirk] = O.render(cornell_arrays, cornell.push_constant(TIME), cfg, 256, 256)
+    return out
+
+
+def test_readme_blocks_quirk_on(oracle_256):
+    rms, mean = _rms_vs_readme(oracle_256[1][1])
+    assert rms < 0.012, rms                  # measured 0.0084 (resolution-limited at 256^2)
+    assert np.all(np.abs(mean) < 0.004), mean
+
+
+def test_readme_blocks_discriminate_quirk(oracle_256):
+    """The std140 luminous-id quirk is visible in the reference's output:
+    emulating the intended packed ids lands ~3x further from the screenshot."""
+    on, _ = _rms_vs_readme(oracle_256[1][1])
+    off, _ = _rms_vs_readme(oracle_256[0][1])
+    assert off > 0.02 and off > 2.5 * on, (on, off)
+
+
+def test_readme_blocks_full_resolution(cornell_arrays, cornell):
+    cfg = rvcp_amd.abi.make_config(spp=30)
+    _, rgba, trav = O.render(cornell_arrays, cornell.push_constant(TIME), cfg, 1024, 1024,
+                             want_linear=False)
+    rms, mean = _rms_vs_readme(rgba)
+    assert rms < 0.006, rms                  # measured 0.0031
+    # miss pixels outside the open box are exactly 64 in the screenshot and here
+    assert (rgba[0, 0, :3] == 64).all() and (rgba[1023, 1023, :3] == 64).all()
+    assert 4.85 < trav / (1024 * 1024 * 30) < 5.0
+
+
+def _pyref_check(sc, cfg, W, H, pixels, time=TIME):
+    arrays = scene_arrays(sc)
+    lin, _, _ = O.render(arrays, sc.push_constant(time), cfg, W, H)
+    ps = pyref.Scene(arrays["materials"], arrays["vertices"], arrays["faces"],
+                     arrays["lum_face_ids"], quirk=bool(cfg["lum_id_std140_quirk"]))
+    P = pyref.params(cfg)
+    for (x, y) in pixels:
+        c, _ = pyref.render_pixel(ps, P, sc.push_constant(time), W, H, x, y)
+        assert np.array_equal(np.array(c, dtype=np.float32).view(np.uint32),
+                              lin[y, x].view(np.uint32)), (x, y, c, lin[y, x])
+
+
+def _pixels(W, H, n, seed):
+    rng = np.random.default_rng(seed)
+    return list(zip(rng.integers(0, W, n).tolist(), rng.integers(0, H, n).tolist()))
+
+
+def test_pyref_default(cornell):
+    _pyref_check(cornell, rvcp_amd.abi.make_config(spp=2), 24, 24, _pixels(24, 24, 24, 1))
+
+
+def test_pyref_quirk_off(cornell):
+    _pyref_check(cornell, rvcp_amd.abi.make_config(spp=2, lum_id_std140_quirk=0), 24, 24,
+                 _pixels(24, 24, 16, 2))
+
+
+def test_pyref_params(cornell):
+    cfg = rvcp_amd.abi.make_config(spp=2, max_bounces=3, rr_probability=1.0,
+                                   attenuation_stop_eps=0.01, ray_t_max=1000.0)
+    _pyref_check(cornell, cfg, 20, 20, _pixels(20, 20, 12, 3), time=7.5)
+
+
+def test_pyref_moved_camera_random_mesh(cornell):
+    base = rvcp_amd.Scene(rvcp_amd.Camera.new([120.0, 400.0, -700.0], [-50.0, 150.0, 100.0],
+                                              0.1, 10000.0, 55.0, 150.0, 5.0),
+                          cornell.materials, [], cornell.mesh)
+    sc = rvcp_amd.scene.with_random_triangles(base, 40)
+    _pyref_check(sc, rvcp_amd.abi.make_config(spp=1), 16, 12, _pixels(16, 12, 8, 4))
