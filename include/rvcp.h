@@ -113,7 +113,11 @@ typedef struct rvcp_config {
      * (ray_tracer_games101_branch.comp:109-111 vs vulkan.rs:473-478): element i is
      * ids[4*i] when 4*i < n_ids, else 0.  0 = the intended packed semantics. */
     int32_t lum_id_std140_quirk;
-    uint32_t _reserved[6];
+    /* Kernel schedule, for A/B measurement only: 0 = the default (fastest), 1 = one ray per
+     * lane per iteration, 2 = shadow + continuation ray per lane per iteration.  Every
+     * schedule produces bit-identical frames. */
+    int32_t kernel_variant;
+    uint32_t _reserved[5];
 } rvcp_config_t;
 
 /* Per-render statistics (all optional). */

@@ -12,13 +12,14 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "csrc", "build", "librvcp.so")
+LIB_PATH = os.environ.get("RVCP_LIB") or os.path.join(_HERE, "csrc", "build", "librvcp.so")
 
 # rvcp_config_t (include/rvcp.h)
 CONFIG_DTYPE = np.dtype([("device", "<i4"), ("integrator", "<i4"), ("spp", "<u4"),
                          ("max_bounces", "<u4"), ("attenuation_stop_eps", "<f4"),
                          ("ray_t_min", "<f4"), ("ray_t_max", "<f4"), ("rr_probability", "<f4"),
-                         ("eps", "<f4"), ("lum_id_std140_quirk", "<i4"), ("_reserved", "<u4", 6)])
+                         ("eps", "<f4"), ("lum_id_std140_quirk", "<i4"), ("kernel_variant", "<i4"),
+                         ("_reserved", "<u4", 5)])
 STATS_DTYPE = np.dtype([("kernel_ms", "<f8"), ("traversals", "<u8"),
                         ("traversals_executed", "<u8"), ("samples", "<u8"), ("faces", "<u4"),
                         ("_reserved", "<u4"), ("wave_iterations", "<u8")])
@@ -27,7 +28,7 @@ assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 48
 # Defaults == the shader's #defines (ray_tracer_games101_branch.comp:5-13).
 DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop_eps=0.05,
                 ray_t_min=0.01, ray_t_max=10000.0, rr_probability=0.8, eps=0.001,
-                lum_id_std140_quirk=1)
+                lum_id_std140_quirk=1, kernel_variant=0)
 
 # Error codes
 RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E_NOMEM = \

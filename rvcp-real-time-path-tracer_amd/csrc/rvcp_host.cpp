@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -26,7 +27,7 @@ struct rvcp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    int grid_capacity = 0;           // resident workgroups of the persistent kernel
+    int grid_capacity[kMaxVariant + 1] = {};   // resident workgroups per kernel variant
 
     // scene (device)
     TriRecord *d_tri = nullptr;
@@ -39,6 +40,10 @@ struct rvcp_ctx {
     uint32_t n_faces = 0, n_lights = 0, n_mats = 0, n_verts = 0;
     float light_total = 0.0f, light_pdf = 0.0f;
     bool has_scene = false;
+
+    // primary pre-pass output (variant 3): compact list of surface pixels
+    SurfRecord *d_surf = nullptr;
+    size_t cap_surf = 0;
 
     // staging for the synchronous host API
     uint32_t *d_rgba = nullptr;
@@ -169,6 +174,8 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     if (cfg->integrator != RVCP_INTEGRATOR_GAMES101)
         return fail(nullptr, RVCP_E_UNSUPPORTED, "unsupported integrator");
     if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
+    if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant)
+        return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
     if (!(cfg->ray_t_max < 16777216.0f))
         return fail(nullptr, RVCP_E_INVALID, "ray_t_max must be < 2^24 (miss test t_max + 1)");
     int ndev = 0;
@@ -201,11 +208,18 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     if (hipMalloc((void **)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "hipMalloc counters"));
 
-    int per_cu = 0, cus = 0;
-    if (rvcp_games101_occupancy(&per_cu) != 0 || per_cu <= 0) per_cu = 1;
+    int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
         cus = 256;
-    ctx->grid_capacity = per_cu * cus;
+    // RVCP_DEBUG_BLOCKS_PER_CU caps the persistent grid (occupancy experiments only)
+    const char *cap_env = std::getenv("RVCP_DEBUG_BLOCKS_PER_CU");
+    const int cap = cap_env ? std::atoi(cap_env) : 0;
+    for (int v = 1; v <= kMaxVariant; v++) {
+        int per_cu = 0;
+        if (rvcp_games101_occupancy(v, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
+        if (cap > 0 && cap < per_cu) per_cu = cap;
+        ctx->grid_capacity[v] = per_cu * cus;
+    }
     *out_ctx = ctx;
     return RVCP_OK;
 }
@@ -220,6 +234,7 @@ int rvcp_destroy(rvcp_ctx_t *ctx)
     (void)hipFree(ctx->d_counters);
     (void)hipFree(ctx->d_rgba);
     (void)hipFree(ctx->d_lin);
+    (void)hipFree(ctx->d_surf);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -266,6 +281,8 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     for (uint32_t i = 0; i < n_materials; i++) {
         std::memcpy(mats[i].albedo, materials[i].albedo, sizeof(float) * 3);
         mats[i].ty = materials[i].ty;
+        for (int c = 0; c < 3; c++) mats[i].alb_pi[c] = materials[i].albedo[c] / 3.1415926f;
+        mats[i].pad = 0;
     }
     // light table (sample_light_games101, :384-404) with the std140 id quirk (:109-111)
     const bool quirk = ctx->cfg.lum_id_std140_quirk != 0;
@@ -356,6 +373,7 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     A.light_total = ctx->light_total;
     A.light_pdf = ctx->light_pdf;
     A.want_linear = d_linear_rgb ? 1u : 0u;
+    A.variant = ctx->cfg.kernel_variant == 0 ? kDefaultVariant : ctx->cfg.kernel_variant;
 
     // With MAX_BOUNCES == 0 or ATTENUATION_STOP_EPS > 1 every sample returns 0 before its
     // first traversal (:413-419): the frame is black.
@@ -370,12 +388,27 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
         } else {
             const uint32_t waves_needed = (A.n_pixels + kChunk - 1) / kChunk;
             uint32_t blocks = (waves_needed + (kBlock / kWave) - 1) / (kBlock / kWave);
-            if (blocks > (uint32_t)ctx->grid_capacity) blocks = (uint32_t)ctx->grid_capacity;
+            if (blocks > (uint32_t)ctx->grid_capacity[A.variant])
+                blocks = (uint32_t)ctx->grid_capacity[A.variant];
             if (blocks == 0) blocks = 1;
             A.static_chunks = blocks * (kBlock / kWave) * kChunk;
-            rc = rvcp_launch_games101(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts, ctx->d_mats,
-                                      ctx->d_lights, ctx->d_gamma, (uint32_t *)d_rgba8,
-                                      (float *)d_linear_rgb, ctx->d_counters, blocks, s);
+            if (A.variant == 3) {
+                if (ctx->cap_surf < A.n_pixels) {
+                    (void)hipFree(ctx->d_surf);
+                    ctx->d_surf = nullptr;
+                    ctx->cap_surf = 0;
+                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)A.n_pixels * sizeof(SurfRecord)));
+                    ctx->cap_surf = A.n_pixels;
+                }
+                rc = rvcp_launch_games101_v3(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
+                                             ctx->d_mats, ctx->d_lights, ctx->d_gamma,
+                                             (uint32_t *)d_rgba8, (float *)d_linear_rgb,
+                                             ctx->d_counters, ctx->d_surf, blocks, s);
+            } else {
+                rc = rvcp_launch_games101(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts, ctx->d_mats,
+                                          ctx->d_lights, ctx->d_gamma, (uint32_t *)d_rgba8,
+                                          (float *)d_linear_rgb, ctx->d_counters, blocks, s);
+            }
         }
         if (rc != 0) return fail(ctx, RVCP_E_HIP, std::string("kernel launch failed: ") +
                                                       hipGetErrorString(hipGetLastError()));

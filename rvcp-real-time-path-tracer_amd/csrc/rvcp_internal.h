@@ -10,8 +10,13 @@ namespace rvcp {
 constexpr int kWave = 64;
 // Threads per workgroup of the path-tracing kernel (4 independent waves).
 constexpr int kBlock = 256;
-// Pixels a wave takes from the frame queue per atomic (see DESIGN.md §4.3).
+// Pixels a wave takes from the frame queue per atomic (see DESIGN.md §4.1).
 constexpr uint32_t kChunk = 64;
+// Kernel schedules (rvcp_config_t::kernel_variant): 1 = one ray per lane per iteration,
+// 2 = shadow + continuation ray per lane per iteration, 3 = primary pre-pass kernel + the
+// variant-2 loop over surface pixels only.
+constexpr int kDefaultVariant = 3;
+constexpr int kMaxVariant = 3;
 
 // One triangle as the brute-force scan reads it: v0, e1 = v1 - v0, e2 = v2 - v0, computed on
 // the host with the same float subtractions the shader performs per test
@@ -39,11 +44,25 @@ struct alignas(16) LightRecord {
 };
 static_assert(sizeof(LightRecord) == 96, "LightRecord is 96 B");
 
-// Per-material record: albedo + type (MaterialBuffer, :74-83).
+// A pixel whose primary ray hit a non-emissive surface, as the primary pre-pass hands it to
+// the path kernel (variant 3): the cached primary hit record (:421-431 at depth 0).
+struct alignas(16) SurfRecord {
+    float pos[3];
+    uint32_t mat;
+    float nrm[3];
+    uint32_t pix;
+};
+static_assert(sizeof(SurfRecord) == 32, "SurfRecord is 32 B");
+
+// Per-material record: albedo + type (MaterialBuffer, :74-83) and albedo / PI, the value
+// lambertian_brdf_eval returns (:346), divided once on the host with the same float division.
 struct alignas(16) MatRecord {
     float albedo[3];
     uint32_t ty;
+    float alb_pi[3];
+    uint32_t pad;
 };
+static_assert(sizeof(MatRecord) == 32, "MatRecord is 32 B");
 
 // Frame-constant parameters of one render launch.
 struct FrameArgs {
@@ -64,6 +83,7 @@ struct FrameArgs {
     float light_total, light_pdf;
     uint32_t static_chunks;  // pixels handed out statically (one chunk per wave)
     uint32_t want_linear;
+    int32_t variant;         // kernel schedule (rvcp_config_t::kernel_variant, resolved)
 };
 
 }  // namespace rvcp
@@ -75,9 +95,14 @@ int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri
                          const rvcp::LightRecord *lights, const float *gamma_t,
                          uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
                          uint32_t grid_blocks, void *stream);
+int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
+                            const void *faces, const void *verts, const rvcp::MatRecord *mats,
+                            const rvcp::LightRecord *lights, const float *gamma_t,
+                            uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
+                            rvcp::SurfRecord *surf, uint32_t grid_blocks, void *stream);
 int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows, uint32_t width,
                          uint32_t height, uint32_t shard_count, uint32_t *frame, void *stream);
 int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n_pixels, uint32_t rgba,
                      void *stream);
-int rvcp_games101_occupancy(int *blocks_per_cu);
+int rvcp_games101_occupancy(int variant, int *blocks_per_cu);
 }

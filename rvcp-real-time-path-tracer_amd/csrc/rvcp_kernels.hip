@@ -1,26 +1,28 @@
-// rvcp_kernels.hip -- gfx950 (CDNA4) path-tracing kernel for the hot path of
+// rvcp_kernels.hip -- gfx950 (CDNA4) path-tracing kernels for the hot path of
 // YXHXianYu/RVCP-Real-Time-Path-Tracer: assets/shaders/ray_tracer_games101_branch.comp,
 // dispatched from src/ray_tracer/vulkan.rs:446.
 //
 // Design:
-//  * Persistent wave64 "ray machine".  Every lane owns one pixel at a time and advances it
-//    through an explicit state machine; each loop iteration the whole wave traces exactly one
-//    ray per lane (a primary, path or shadow ray) through the brute-force triangle scan, then
-//    every lane runs the small shading step that produces its next ray.  A lane whose pixel
-//    finishes takes the next pixel from a per-wave chunk of the frame queue (one atomic per
-//    64 pixels), so lanes never idle while the frame has work.  This replaces the
-//    reference's lockstep SPP x bounce loops (:494, :413), which leave ~70 % of an 8x8 wave
-//    idle waiting for the longest path.
-//  * The scan reads the triangles with wave-uniform addresses, so they arrive as scalar
-//    loads into SGPRs (s_load_dwordx*), broadcast to all 64 lanes; the scan is VALU-bound.
-//  * The primary ray does not depend on the RNG (:491 is outside the SPP loop), so its hit
-//    record is computed once per pixel and reused by every sample.
-//  * The hit record (interpolated normal, material) is resolved once per traversal for the
-//    nearest face only, instead of once per accepted face.
+//  * Persistent wave64 "ray machines".  Every lane owns one pixel at a time and advances it
+//    through an explicit state machine that keeps the shader's RNG order, accumulation order
+//    and termination rules; each loop iteration the wave traces rays through the brute-force
+//    triangle scan, then every lane runs the shading step that produces its next ray(s).  A
+//    lane whose pixel finishes takes the next pixel from a per-wave chunk of the frame queue
+//    (one atomic per 64 pixels), so lanes never idle while the frame has work.  This replaces
+//    the reference's lockstep SPP x bounce loops (:494, :413).
+//      variant 1: one ray per lane per iteration (primary, path or shadow);
+//      variant 2: a surface event emits its shadow ray AND its continuation ray (the RNG
+//                 stream does not depend on the visibility result), both traced in one scan.
+//  * The scan reads the triangles with wave-uniform addresses, so they arrive as scalar loads
+//    into SGPRs (s_load_dwordx*), broadcast to all 64 lanes; the scan is VALU-bound.
+//  * The primary ray does not depend on the RNG (:491 is outside the SPP loop): its hit record
+//    is computed once per pixel and reused by every sample.
+//  * The hit record (interpolated normal, material) is resolved once per traversal, for the
+//    nearest face only.
 //
 // Numerics: float32, no contraction (-ffp-contract=off), IEEE correctly
-// rounded division and sqrt, the software sin shared with the CPU oracle by contract, so
-// every pixel is bit-identical to oracle/rvcp_oracle.c.
+// rounded division and sqrt, the software sin of the contract, so every pixel is
+// bit-identical to oracle/rvcp_oracle.c whichever variant runs.
 #include <hip/hip_runtime.h>
 
 #include "rvcp_internal.h"
@@ -49,8 +51,7 @@ __device__ __forceinline__ f3 normalize(f3 a) { return muls(a, 1.0f / __builtin_
 __device__ __forceinline__ float fractf(float x) { return x - __builtin_floorf(x); }
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 
-constexpr float kPi = 3.1415926f;       // ray_tracer_games101_branch.comp:6
-constexpr uint32_t kLight = 3u;         // MATERIAL_LIGHT :25
+constexpr uint32_t kLight = 3u;         // MATERIAL_LIGHT, ray_tracer_games101_branch.comp:25
 
 // Software sin: the DESIGN.md §3.2 contract (same algorithm as the oracle).
 __device__ __forceinline__ float pt_sinf(float x) {
@@ -77,6 +78,19 @@ __device__ __forceinline__ float rnd(float seed, float &idx) {
     return fractf(pt_sinf(seed + idx) * 43758.5453f);
 }
 
+// 1 / den, IEEE round-to-nearest (the shader's `1.0 / dot(s1, e1)`, :254).
+// Fast path: v_rcp_f32 plus one FMA Newton step.  tools/rcp_check.hip compares it with the
+// IEEE division for every normal |den| in [2^-126, 2^126) (all 2^23 mantissas, both signs):
+// 0 mismatches.  Outside that range (zero, denormal, huge, inf, NaN) -- a degenerate or
+// grazing triangle -- the lanes concerned take the full IEEE division.
+__device__ __forceinline__ float rcp_ieee(float den) {
+    const float r = __builtin_amdgcn_rcpf(den);
+    float f = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    const float a = __builtin_fabsf(den);
+    if (__builtin_expect(!(a >= 0x1p-126f && a < 0x1p126f), 0)) f = 1.0f / den;
+    return f;
+}
+
 // Tone map + UNORM8 (:498-500) by the threshold table of DESIGN.md §3.3.
 __device__ __forceinline__ uint32_t gamma_u8(float c, const float *__restrict__ T) {
     const float x = (c > 0.0f) ? ((c < 1.0f) ? c : 1.0f) : 0.0f;
@@ -87,10 +101,155 @@ __device__ __forceinline__ uint32_t gamma_u8(float c, const float *__restrict__ 
     return lo;
 }
 
-// Lane actions of the ray machine.
-enum : int { A_TRACE = 0, A_RR = 1, A_END = 2, A_SURF = 3, A_NEED = 4, A_DONE = 5 };
-// Kinds of the ray a lane is tracing.
-enum : int { K_PRIMARY = 0, K_PATH = 1, K_SHADOW = 2 };
+__device__ __forceinline__ uint32_t pack_rgba(f3 c, const float *__restrict__ T) {
+    return gamma_u8(c.x, T) | (gamma_u8(c.y, T) << 8) | (gamma_u8(c.z, T) << 16) | 0xFF000000u;
+}
+
+__device__ __forceinline__ void store_pixel(uint32_t pix, f3 acc, const FrameArgs &A,
+                                            const float *__restrict__ gamma_t,
+                                            uint32_t *__restrict__ out_rgba,
+                                            float *__restrict__ out_lin) {
+    out_rgba[pix] = pack_rgba(acc, gamma_t);
+    if (A.want_linear) {
+        out_lin[3 * (size_t)pix + 0] = acc.x;
+        out_lin[3 * (size_t)pix + 1] = acc.y;
+        out_lin[3 * (size_t)pix + 2] = acc.z;
+    }
+}
+
+// One exact ray-triangle test (is_intersect_with_face, :238-260) with the nearest-hit rule
+// of get_intersection_with_scene (:291): accept iff the shader would replace the current
+// nearest hit whose time is `bt`.  5-compare form, DESIGN.md §3.5.
+__device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float tmin, float bt,
+                                           float &t_out) {
+    const f3 s = mk(o.x - T.v0[0], o.y - T.v0[1], o.z - T.v0[2]);
+    const f3 e1 = ld3(T.e1), e2 = ld3(T.e2);
+    const f3 s1 = cross(d, e2);
+    const f3 s2 = cross(s, e1);
+    const float f = rcp_ieee(dot(s1, e1));
+    const float t = f * dot(s2, e2);
+    const float b1 = f * dot(s1, s);
+    const float b2 = f * dot(s2, d);
+    t_out = t;
+    return (b1 >= 0.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f) & (t >= tmin) & (t <= bt);
+}
+
+// Hit record of face `best` for ray (o, d) hit at time t (:262-278).
+__device__ __forceinline__ void hit_record(const TriRecord *__restrict__ tri,
+                                           const rvcp_face_t *__restrict__ faces,
+                                           const rvcp_vertex_t *__restrict__ verts, int best,
+                                           f3 o, f3 d, float t, f3 &pos, f3 &n, uint32_t &mat) {
+    const rvcp_face_t F = faces[best];
+    const TriRecord T = tri[best];
+    const f3 s = mk(o.x - T.v0[0], o.y - T.v0[1], o.z - T.v0[2]);
+    const f3 e1 = ld3(T.e1), e2 = ld3(T.e2);
+    const f3 s1 = cross(d, e2);
+    const f3 s2 = cross(s, e1);
+    const float f = rcp_ieee(dot(s1, e1));
+    const float b1 = f * dot(s1, s);
+    const float b2 = f * dot(s2, d);
+    const f3 n0 = ld3(verts[F.vertices[0]].normal);
+    const f3 n1 = ld3(verts[F.vertices[1]].normal);
+    const f3 n2 = ld3(verts[F.vertices[2]].normal);
+    n = normalize(add(add(muls(n0, 1.0f - b1 - b2), muls(n1, b1)), muls(n2, b2)));
+    if (dot(n, d) > 0.0f) n = neg(n);
+    pos = add(o, muls(d, t));
+    mat = F.material_id;
+}
+
+// uv of shard-local pixel `pix` (main :487-488); stripes of 8 rows are dealt round-robin.
+__device__ __forceinline__ void pixel_uv(const FrameArgs &A, uint32_t pix, float &u_, float &v_) {
+    const uint32_t lr = pix / A.width;
+    const uint32_t x = pix - lr * A.width;
+    const uint32_t gy = ((lr >> 3) * A.shard_count + A.shard_index) * 8u + (lr & 7u);
+    u_ = ((float)x + 0.5f) / (float)A.width;
+    v_ = ((float)gy + 0.5f) / (float)A.height;
+}
+
+// srand, :153-155
+__device__ __forceinline__ float pixel_seed(const FrameArgs &A, float u_, float v_) {
+    const float sa = fractf(pt_sinf(A.time) * 43758.5453f);
+    const float sb = fractf(pt_sinf(u_) * 22578.5453f);
+    const float sc = fractf(pt_sinf(v_) * 114514.1919f);
+    return fractf(sa + sb + sc);
+}
+
+// sample_ray, :217-235 (frame constants from the host)
+__device__ __forceinline__ void primary_ray(const FrameArgs &A, float u_, float v_, f3 &o, f3 &d,
+                                            float &tmin, float &tmax) {
+    const f3 uv_pos = add(add(ld3(A.pos), muls(ld3(A.u), u_ - 0.5f)), muls(ld3(A.v), v_ - 0.5f));
+    const f3 dv = sub(uv_pos, ld3(A.cam_pos));
+    const float t_coef = len(dv) / A.base_len;
+    o = ld3(A.cam_pos);
+    d = normalize(dv);
+    tmin = A.t_near * t_coef;
+    tmax = A.t_far * t_coef;
+}
+
+// Primary ray of pixel `pix` (main :486-491): srand + sample_ray.
+__device__ __forceinline__ void start_pixel(const FrameArgs &A, uint32_t pix, float &seed,
+                                            float &ridx, f3 &o, f3 &d, float &tmin, float &tmax) {
+    float u_, v_;
+    pixel_uv(A, pix, u_, v_);
+    seed = pixel_seed(A, u_, v_);
+    ridx = 0.0f;
+    primary_ray(A, u_, v_, o, d, tmin, tmax);
+}
+
+// NEE half of a surface event (:431-440 + sample_light_games101 :384-404): the light sample,
+// the contribution C the shadow ray will add if it sees the sample (:450-458), and the
+// shadow ray direction.  Returns false when there is no luminous face.
+__device__ __forceinline__ bool nee_sample(const FrameArgs &A, const LightRecord *__restrict__ lights,
+                                           const MatRecord &m, f3 S_pos, f3 S_nrm, f3 att,
+                                           float seed, float &ridx, f3 &C, float &dist, f3 &ws) {
+    const float pl = rnd(seed, ridx) * A.light_total;
+    uint32_t li = A.n_lights;
+    for (uint32_t i = 0; i < A.n_lights; ++i) {
+        if (pl <= lights[i].cum) { li = i; break; }
+    }
+    if (li >= A.n_lights) return false;
+    const LightRecord &L = lights[li];
+    const float x = __builtin_sqrtf(rnd(seed, ridx));                              // :319
+    const float y = rnd(seed, ridx);                                               // :320
+    const f3 Xp = add(add(muls(ld3(L.v0), 1.0f - x), muls(ld3(L.v1), x * (1.0f - y))),
+                      muls(ld3(L.v2), x * y));                                     // :324
+    const f3 dv = sub(Xp, S_pos);
+    dist = len(dv);                                                                // :438
+    ws = divs(dv, dist);                                                           // :439
+    const float cosp = dot(S_nrm, ws);
+    const f3 f = cosp > 0.0f ? ld3(m.alb_pi) : mk(0, 0, 0);                        // :344-349
+    C = mulv(mulv(att, ld3(L.le)), f);                                             // :450-458
+    C = muls(C, cosp);
+    C = muls(C, dot(ld3(L.n), neg(ws)));
+    C = divs(C, dist * dist * A.light_pdf);
+    return true;
+}
+
+// Continuation half of a surface event (:461-471): Russian roulette, the uniform hemisphere
+// direction and the attenuation update.  Returns false when the path ends at RR.
+__device__ __forceinline__ bool brdf_continue(const FrameArgs &A, const MatRecord &m, f3 S_nrm,
+                                              float seed, float &ridx, f3 &att, f3 &wi) {
+    if (rnd(seed, ridx) > A.rr) return false;                                      // :462
+    f3 p;
+    do {                                                                           // :195-201
+        const float rx = rnd(seed, ridx);
+        const float ry = rnd(seed, ridx);
+        const float rz = rnd(seed, ridx);
+        p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
+    } while (dot(p, p) >= 1.0f);
+    const f3 h = dot(p, S_nrm) > 0.0f ? p : neg(p);                                // :207-210
+    wi = normalize(h);                                                             // :212-214
+    const float cosw = dot(S_nrm, wi);
+    const f3 f = cosw > 0.0f ? ld3(m.alb_pi) : mk(0, 0, 0);
+    const float pdf = dot(wi, S_nrm) > 0.0f ? 0.5f / 3.1415926f : 0.0f;            // :358-365
+    const float denom = __builtin_fmaxf(0.1f, pdf) * A.rr;
+    att = mulv(att, divs(muls(f, cosw), denom));                                   // :465-471
+    return true;
+}
+
+__device__ __forceinline__ bool att_stop(const FrameArgs &A, f3 att) {          // :415-419
+    return att.x < A.att_stop && att.y < A.att_stop && att.z < A.att_stop;
+}
 
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -100,11 +259,72 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Wave-uniform frame-queue state: [next, end) pixels owned by this wave.
+struct Queue {
+    uint32_t next, end;
+    bool exhausted;
+};
+
+__device__ __forceinline__ Queue queue_init(const FrameArgs &A) {
+    const uint32_t wave_global =
+        __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) / kWave);
+    Queue q;
+    q.next = wave_global * kChunk;
+    q.end = q.next + kChunk;
+    if (q.next > A.n_pixels) q.next = A.n_pixels;
+    if (q.end > A.n_pixels) q.end = A.n_pixels;
+    q.exhausted = false;
+    return q;
+}
+
+// Hand pixels to the lanes in `need` (must be called in wave-uniform control flow).  Lanes
+// that receive one get got=true and their pixel index.
+__device__ __forceinline__ void queue_take(Queue &q, uint64_t need, uint32_t lane,
+                                           const FrameArgs &A,
+                                           unsigned long long *__restrict__ counters,
+                                           bool &got, uint32_t &pix) {
+    got = false;
+    while (need != 0ull) {
+        if (q.next >= q.end) {
+            if (q.exhausted) break;
+            const int leader = (int)__builtin_ctzll(need);
+            uint32_t base = 0;
+            if (lane == (uint32_t)leader) base = atomicAdd((unsigned int *)&counters[1], kChunk);
+            base = __builtin_amdgcn_readfirstlane(__shfl(base, leader)) + A.static_chunks;
+            if (base >= A.n_pixels) { q.exhausted = true; break; }
+            q.next = base;
+            q.end = base + kChunk < A.n_pixels ? base + kChunk : A.n_pixels;
+        }
+        const uint32_t avail = q.end - q.next;
+        const uint32_t r = rank_in(need);
+        const bool mine = ((need >> lane) & 1ull) && r < avail;
+        const uint64_t given = __ballot(mine);
+        if (mine) { pix = q.next + r; got = true; }
+        q.next += __builtin_popcountll(given);
+        need &= ~given;
+    }
+}
+
+__device__ __forceinline__ void flush_counters(unsigned long long *__restrict__ counters,
+                                               uint32_t lane, uint32_t trav, uint32_t iters) {
+    unsigned long long t64 = trav;
+    for (int off = 32; off >= 1; off >>= 1) t64 += __shfl_xor(t64, off);
+    if (lane == 0) {
+        atomicAdd(&counters[0], t64);
+        atomicAdd(&counters[2], (unsigned long long)iters);
+    }
+}
+
+// Lane actions of the single-ray machine.
+enum : int { A_TRACE = 0, A_RR = 1, A_END = 2, A_SURF = 3, A_NEED = 4, A_DONE = 5 };
+// Kinds of a traced ray.
+enum : int { K_NONE = -1, K_PRIMARY = 0, K_PATH = 1, K_SHADOW = 2 };
+
 }  // namespace
 
-// ------------------------------------------------------------------------------------
-// The persistent path-tracing kernel
-// ------------------------------------------------------------------------------------
+// ======================================================================================
+// Variant 1: one ray per lane per iteration
+// ======================================================================================
 __global__ __launch_bounds__(kBlock) void games101_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
     const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
@@ -113,22 +333,11 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
     unsigned long long *__restrict__ counters)
 {
     const uint32_t lane = lane_id();
-    const uint32_t wave_global =
-        __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) / kWave);
-
-    // wave-uniform queue state: [chunk_next, chunk_end) of pixels owned by this wave
-    uint32_t chunk_next = wave_global * kChunk;
-    uint32_t chunk_end = chunk_next + kChunk;
-    if (chunk_next > A.n_pixels) chunk_next = A.n_pixels;
-    if (chunk_end > A.n_pixels) chunk_end = A.n_pixels;
-    bool exhausted = false;
-
+    Queue q = queue_init(A);
     const float sppf = (float)A.spp;
-    const float Wf = (float)A.width, Hf = (float)A.height;
 
-    // ---- lane state ----
     int action = A_NEED, kind = K_PRIMARY;
-    uint32_t pix = 0, k = 0, depth = 0, trav = 0, waves_iter = 0;
+    uint32_t pix = 0, k = 0, depth = 0, trav = 0, iters = 0;
     float seed = 0.0f, ridx = 0.0f;
     f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
     f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0);   // cached primary hit (surface)
@@ -143,50 +352,25 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
     for (;;) {
         // ============ settle: advance every lane until it has a ray or is done ============
         for (;;) {
-            // --- Russian roulette + BRDF sample (:461-478) ---
-            if (action == A_RR) {
-                if (rnd(seed, ridx) > A.rr) {
+            if (action == A_RR) {                                   // :461-478
+                f3 wi;
+                if (!brdf_continue(A, mats[S_mat], S_nrm, seed, ridx, att, wi)) {
                     action = A_END;
                 } else {
-                    f3 p;
-                    do {                                              // :195-201
-                        const float rx = rnd(seed, ridx);
-                        const float ry = rnd(seed, ridx);
-                        const float rz = rnd(seed, ridx);
-                        p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
-                    } while (dot(p, p) >= 1.0f);
-                    const f3 h = dot(p, S_nrm) > 0.0f ? p : neg(p);   // :207-210
-                    const f3 wi = normalize(h);                       // :212-214
-                    const float cosw = dot(S_nrm, wi);
-                    const MatRecord m = mats[S_mat];
-                    const f3 f = cosw > 0.0f ? divs(ld3(m.albedo), kPi) : mk(0, 0, 0);
-                    const float pdf = dot(wi, S_nrm) > 0.0f ? 0.5f / kPi : 0.0f;
-                    const float denom = __builtin_fmaxf(0.1f, pdf) * A.rr;
-                    att = mulv(att, divs(muls(f, cosw), denom));       // :465-471
                     depth += 1;
-                    ro = add(S_pos, muls(wi, A.eps));                  // :473-478
+                    ro = add(S_pos, muls(wi, A.eps));
                     rd = wi;
                     rtmin = A.t_min;
                     rtmax = A.t_max;
                     kind = K_PATH;
-                    const bool stop = att.x < A.att_stop && att.y < A.att_stop &&
-                                      att.z < A.att_stop;             // :415-419
-                    action = (depth >= A.max_bounces || stop) ? A_END : A_TRACE;
+                    action = (depth >= A.max_bounces || att_stop(A, att)) ? A_END : A_TRACE;
                 }
             }
-            // --- end of one sample: color += L / SPP (:495) ---
-            if (action == A_END) {
+            if (action == A_END) {                                  // color += L / SPP (:495)
                 acc = add(acc, divs(col, sppf));
                 k += 1;
                 if (k >= A.spp) {
-                    const uint32_t rgba = gamma_u8(acc.x, gamma_t) | (gamma_u8(acc.y, gamma_t) << 8) |
-                                          (gamma_u8(acc.z, gamma_t) << 16) | 0xFF000000u;
-                    out_rgba[pix] = rgba;
-                    if (A.want_linear) {
-                        out_lin[3 * (size_t)pix + 0] = acc.x;
-                        out_lin[3 * (size_t)pix + 1] = acc.y;
-                        out_lin[3 * (size_t)pix + 2] = acc.z;
-                    }
+                    store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
                     action = A_NEED;
                 } else {
                     depth = 0;
@@ -198,34 +382,13 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
                     action = A_SURF;
                 }
             }
-            // --- surface event: light sample (:384-404) and the shadow ray (:434-447) ---
-            if (action == A_SURF) {
-                const float pl = rnd(seed, ridx) * A.light_total;
-                uint32_t li = A.n_lights;
-                for (uint32_t i = 0; i < A.n_lights; ++i) {
-                    if (pl <= lights[i].cum) { li = i; break; }
-                }
-                if (li >= A.n_lights) {
-                    action = A_RR;      // no luminous face: no NEE term
+            if (action == A_SURF) {                                 // :431-447
+                f3 ws;
+                if (!nee_sample(A, lights, mats[S_mat], S_pos, S_nrm, att, seed, ridx, nee_C,
+                                nee_dist, ws)) {
+                    action = A_RR;
                 } else {
-                    const LightRecord &L = lights[li];
-                    const float x = __builtin_sqrtf(rnd(seed, ridx));
-                    const float y = rnd(seed, ridx);
-                    const f3 Xp = add(add(muls(ld3(L.v0), 1.0f - x), muls(ld3(L.v1), x * (1.0f - y))),
-                                      muls(ld3(L.v2), x * y));                     // :324
-                    const f3 dv = sub(Xp, S_pos);
-                    const float dist = len(dv);                                    // :438
-                    const f3 ws = divs(dv, dist);                                  // :439
-                    const float cosp = dot(S_nrm, ws);
-                    const MatRecord m = mats[S_mat];
-                    const f3 f = cosp > 0.0f ? divs(ld3(m.albedo), kPi) : mk(0, 0, 0);
-                    f3 C = mulv(mulv(att, ld3(L.le)), f);                          // :450-458
-                    C = muls(C, cosp);
-                    C = muls(C, dot(ld3(L.n), neg(ws)));
-                    C = divs(C, dist * dist * A.light_pdf);
-                    nee_C = C;
-                    nee_dist = dist;
-                    ro = add(S_pos, muls(ws, A.eps));                              // :441-446
+                    ro = add(S_pos, muls(ws, A.eps));
                     rd = ws;
                     rtmin = A.t_min;
                     rtmax = A.t_max;
@@ -233,133 +396,58 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
                     action = A_TRACE;
                 }
             }
-            // --- take new pixels from the frame queue (wave-uniform control flow) ---
-            uint64_t need = __ballot(action == A_NEED);
-            while (need != 0ull) {
-                if (chunk_next >= chunk_end) {
-                    if (exhausted) break;
-                    uint32_t base = 0;
-                    if (lane == (uint32_t)__builtin_ctzll(need))
-                        base = atomicAdd((unsigned int *)&counters[1], kChunk);
-                    base = __builtin_amdgcn_readfirstlane(
-                               __shfl(base, (int)__builtin_ctzll(need))) + A.static_chunks;
-                    if (base >= A.n_pixels) { exhausted = true; break; }
-                    chunk_next = base;
-                    chunk_end = base + kChunk < A.n_pixels ? base + kChunk : A.n_pixels;
-                }
-                const uint32_t avail = chunk_end - chunk_next;
-                const uint32_t r = rank_in(need);
-                const bool mine = ((need >> lane) & 1ull) && r < avail;
-                const uint64_t got = __ballot(mine);
-                if (mine) {
-                    // ---- start a pixel: main(), :486-491 ----
-                    pix = chunk_next + r;
-                    const uint32_t lr = pix / A.width;
-                    const uint32_t x = pix - lr * A.width;
-                    const uint32_t gy = ((lr >> 3) * A.shard_count + A.shard_index) * 8u + (lr & 7u);
-                    const float u_ = ((float)x + 0.5f) / Wf;
-                    const float v_ = ((float)gy + 0.5f) / Hf;
-                    // srand, :153-155
-                    const float sa = fractf(pt_sinf(A.time) * 43758.5453f);
-                    const float sb = fractf(pt_sinf(u_) * 22578.5453f);
-                    const float sc = fractf(pt_sinf(v_) * 114514.1919f);
-                    seed = fractf(sa + sb + sc);
-                    ridx = 0.0f;
-                    // sample_ray, :217-235
-                    const f3 uv_pos = add(add(ld3(A.pos), muls(ld3(A.u), u_ - 0.5f)),
-                                          muls(ld3(A.v), v_ - 0.5f));
-                    const f3 dv = sub(uv_pos, ld3(A.cam_pos));
-                    const float t_coef = len(dv) / A.base_len;
-                    ro = ld3(A.cam_pos);
-                    rd = normalize(dv);
-                    rtmin = A.t_near * t_coef;
-                    rtmax = A.t_far * t_coef;
+            {   // take new pixels from the frame queue (wave-uniform control flow)
+                bool got;
+                uint32_t np = pix;
+                queue_take(q, __ballot(action == A_NEED), lane, A, counters, got, np);
+                if (got) {
+                    pix = np;
+                    start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
                     kind = K_PRIMARY;
                     k = 0;
                     acc = mk(0, 0, 0);
                     action = A_TRACE;
                 }
-                chunk_next += __builtin_popcountll(got);
-                need &= ~got;
             }
-            if (exhausted && action == A_NEED) action = A_DONE;
+            if (q.exhausted && action == A_NEED) action = A_DONE;
             if (!__any(action == A_RR || action == A_END || action == A_SURF)) break;
         }
         if (!__any(action == A_TRACE)) break;
-        waves_iter += 1;
+        iters += 1;
 
-        // ============ trace: brute-force nearest hit (:283-298, :238-260) ============
+        // ============ trace: brute-force nearest hit (:283-298) ============
         int best = -1;
         float bt = rtmax;
         if (action == A_TRACE) {
             trav += 1;
             for (uint32_t i = 0; i < A.n_faces; ++i) {
-                const TriRecord T = tri[i];
-                const f3 s = mk(ro.x - T.v0[0], ro.y - T.v0[1], ro.z - T.v0[2]);
-                const f3 e1 = ld3(T.e1), e2 = ld3(T.e2);
-                const f3 s1 = cross(rd, e2);
-                const f3 s2 = cross(s, e1);
-                const float f = 1.0f / dot(s1, e1);
-                const float t = f * dot(s2, e2);
-                const float b1 = f * dot(s1, s);
-                const float b2 = f * dot(s2, rd);
-                // == !(b1<0 || 1<b1 || b2<0 || 1<b2 || 1<b1+b2 || t<t_min || t_max<t)
-                //    && t <= t_max  (DESIGN.md §3.5 proves the equivalence, NaN included)
-                const bool ok = (b1 >= 0.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f) &
-                                (t >= rtmin) & (t <= bt);
-                if (ok) { bt = t; best = (int)i; }
+                float t;
+                if (tri_accept(tri[i], ro, rd, rtmin, bt, t)) { bt = t; best = (int)i; }
             }
         }
 
         // ============ post-trace shading ============
         if (action == A_TRACE) {
-            if (kind == K_SHADOW) {
-                // :447-459 -- visibility of the light sample
+            if (kind == K_SHADOW) {                                 // :447-459
                 const f3 hp = best >= 0 ? add(ro, muls(rd, bt))
                                         : mk(__builtin_inff(), __builtin_inff(), __builtin_inff());
                 const float dist_blocked = len(sub(hp, S_pos));
                 if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) col = add(col, nee_C);
                 action = A_RR;
             } else {
-                // resolve the nearest hit's record (:262-278) for face `best`
                 f3 hpos = mk(0, 0, 0), hn = mk(0, 0, 0);
                 uint32_t hmat = 0;
-                if (best >= 0) {
-                    const rvcp_face_t F = faces[best];
-                    const TriRecord T = tri[best];
-                    const f3 s = mk(ro.x - T.v0[0], ro.y - T.v0[1], ro.z - T.v0[2]);
-                    const f3 e1 = ld3(T.e1), e2 = ld3(T.e2);
-                    const f3 s1 = cross(rd, e2);
-                    const f3 s2 = cross(s, e1);
-                    const float f = 1.0f / dot(s1, e1);
-                    const float b1 = f * dot(s1, s);
-                    const float b2 = f * dot(s2, rd);
-                    const f3 n0 = ld3(verts[F.vertices[0]].normal);
-                    const f3 n1 = ld3(verts[F.vertices[1]].normal);
-                    const f3 n2 = ld3(verts[F.vertices[2]].normal);
-                    f3 n = normalize(add(add(muls(n0, 1.0f - b1 - b2), muls(n1, b1)), muls(n2, b2)));
-                    if (dot(n, rd) > 0.0f) n = neg(n);
-                    hn = n;
-                    hpos = add(ro, muls(rd, bt));
-                    hmat = F.material_id;
-                }
+                if (best >= 0) hit_record(tri, faces, verts, best, ro, rd, bt, hpos, hn, hmat);
                 const bool miss = best < 0;
                 const bool is_light = !miss && mats[hmat].ty == kLight;
                 if (kind == K_PRIMARY) {
                     if (miss || is_light) {
-                        // every sample of this pixel returns the same L without using the RNG:
+                        // every sample returns the same L without touching the RNG:
                         // miss -> 0.1 (:424), light at depth 0 -> Le (:425-427)
                         const f3 L = miss ? mk(0.1f, 0.1f, 0.1f) : ld3(mats[hmat].albedo);
                         const f3 Ls = divs(L, sppf);
                         for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, Ls);
-                        const uint32_t rgba = gamma_u8(acc.x, gamma_t) | (gamma_u8(acc.y, gamma_t) << 8) |
-                                              (gamma_u8(acc.z, gamma_t) << 16) | 0xFF000000u;
-                        out_rgba[pix] = rgba;
-                        if (A.want_linear) {
-                            out_lin[3 * (size_t)pix + 0] = acc.x;
-                            out_lin[3 * (size_t)pix + 1] = acc.y;
-                            out_lin[3 * (size_t)pix + 2] = acc.z;
-                        }
+                        store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
                         action = A_NEED;
                     } else {
                         P_pos = hpos; P_nrm = hn; P_mat = hmat;
@@ -369,12 +457,12 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
                         col = mk(0, 0, 0);
                         action = A_SURF;
                     }
-                } else {  // K_PATH
+                } else {                                            // K_PATH
                     if (miss) {
                         col = add(col, mk(0.1f, 0.1f, 0.1f));
                         action = A_END;
                     } else if (is_light) {
-                        action = A_END;        // depth >= 1: no emission term (:426)
+                        action = A_END;     // depth >= 1: no emission term (:426)
                     } else {
                         S_pos = hpos; S_nrm = hn; S_mat = hmat;
                         action = A_SURF;
@@ -383,14 +471,431 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
             }
         }
     }
+    flush_counters(counters, lane, trav, iters);
+}
 
-    // executed traversals: one atomic per wave
-    unsigned long long t64 = trav;
-    for (int off = 32; off >= 1; off >>= 1) t64 += __shfl_xor(t64, off);
-    if (lane == 0) {
-        atomicAdd(&counters[0], t64);
-        atomicAdd(&counters[2], (unsigned long long)waves_iter);
+// ======================================================================================
+// Variant 2: a surface event emits its shadow ray (A) and its continuation ray (B); both are
+// traced by one scan.  The RNG stream of a path does not depend on the shadow result, so
+// sampling the continuation before the shadow ray is resolved keeps every rand() in order;
+// the NEE term of bounce d is added before the miss/emission term of bounce d+1, as in the
+// shader.
+// ======================================================================================
+__global__ __launch_bounds__(kBlock) void games101_dual_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
+    const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters)
+{
+    const uint32_t lane = lane_id();
+    Queue q = queue_init(A);
+    const float sppf = (float)A.spp;
+
+    bool need_pixel = true, done = false;
+    uint32_t pix = 0, k = 0, depth = 0, trav = 0, iters = 0;
+    float seed = 0.0f, ridx = 0.0f;
+    f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
+    f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0);
+    uint32_t P_mat = 0;
+    // ray A: pending shadow ray of the last surface event
+    bool hasA = false;
+    f3 a_o = mk(0, 0, 0), a_d = mk(0, 0, 1), a_p = mk(0, 0, 0), nee_C = mk(0, 0, 0);
+    float nee_dist = 0.0f;
+    // ray B: primary or continuation ray
+    int kindB = K_NONE;
+    f3 b_o = mk(0, 0, 0), b_d = mk(0, 0, 1);
+    float b_tmin = 0.0f, b_tmax = 0.0f;
+
+    for (;;) {
+        // ---- new pixels (wave-uniform) ----
+        {
+            bool got;
+            uint32_t np = pix;
+            queue_take(q, __ballot(need_pixel && !done), lane, A, counters, got, np);
+            if (got) {
+                pix = np;
+                start_pixel(A, pix, seed, ridx, b_o, b_d, b_tmin, b_tmax);
+                kindB = K_PRIMARY;
+                hasA = false;
+                k = 0;
+                acc = mk(0, 0, 0);
+                need_pixel = false;
+            } else if (need_pixel && q.exhausted) {
+                done = true;
+            }
+        }
+        if (!__any(hasA || kindB != K_NONE)) break;
+        iters += 1;
+
+        // ---- scan: both rays against every triangle ----
+        int bestA = -1, bestB = -1;
+        float btA = A.t_max, btB = b_tmax;
+        trav += (hasA ? 1u : 0u) + (kindB != K_NONE ? 1u : 0u);
+#pragma unroll 2
+        for (uint32_t i = 0; i < A.n_faces; ++i) {
+            const TriRecord T = tri[i];
+            float tA, tB;
+            if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
+            if (tri_accept(T, b_o, b_d, b_tmin, btB, tB)) { btB = tB; bestB = (int)i; }
+        }
+
+        // ---- resolve A: visibility of the light sample (:447-459) ----
+        if (hasA) {
+            const f3 hp = bestA >= 0 ? add(a_o, muls(a_d, btA))
+                                     : mk(__builtin_inff(), __builtin_inff(), __builtin_inff());
+            const float dist_blocked = len(sub(hp, a_p));
+            if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) col = add(col, nee_C);
+        }
+
+        // ---- resolve B ----
+        bool surf = false, ended = false;
+        f3 S_pos = P_pos, S_nrm = P_nrm;
+        uint32_t S_mat = P_mat;
+        if (kindB != K_NONE) {
+            f3 hpos = mk(0, 0, 0), hn = mk(0, 0, 0);
+            uint32_t hmat = 0;
+            if (bestB >= 0) hit_record(tri, faces, verts, bestB, b_o, b_d, btB, hpos, hn, hmat);
+            const bool miss = bestB < 0;
+            const bool is_light = !miss && mats[hmat].ty == kLight;
+            if (kindB == K_PRIMARY) {
+                if (miss || is_light) {
+                    const f3 L = miss ? mk(0.1f, 0.1f, 0.1f) : ld3(mats[hmat].albedo);
+                    const f3 Ls = divs(L, sppf);
+                    for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, Ls);
+                    store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
+                    need_pixel = true;
+                } else {
+                    P_pos = hpos; P_nrm = hn; P_mat = hmat;
+                    S_pos = hpos; S_nrm = hn; S_mat = hmat;
+                    depth = 0;
+                    att = mk(1, 1, 1);
+                    col = mk(0, 0, 0);
+                    surf = true;
+                }
+            } else {                                                    // K_PATH
+                if (miss) {
+                    col = add(col, mk(0.1f, 0.1f, 0.1f));
+                    ended = true;
+                } else if (is_light) {
+                    ended = true;
+                } else {
+                    S_pos = hpos; S_nrm = hn; S_mat = hmat;
+                    surf = true;
+                }
+            }
+        } else if (hasA) {
+            ended = true;       // the path ended at its last surface event (RR / depth / att)
+        }
+        hasA = false;
+        kindB = K_NONE;
+
+        // ---- end samples and emit the next surface event (loops only without lights) ----
+        for (;;) {
+            if (ended) {
+                ended = false;
+                acc = add(acc, divs(col, sppf));
+                k += 1;
+                if (k >= A.spp) {
+                    store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
+                    need_pixel = true;
+                } else {
+                    depth = 0;
+                    att = mk(1, 1, 1);
+                    col = mk(0, 0, 0);
+                    S_pos = P_pos; S_nrm = P_nrm; S_mat = P_mat;
+                    surf = true;
+                }
+            }
+            if (surf) {
+                surf = false;
+                const MatRecord m = mats[S_mat];
+                f3 ws;
+                if (nee_sample(A, lights, m, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist, ws)) {
+                    a_o = add(S_pos, muls(ws, A.eps));
+                    a_d = ws;
+                    a_p = S_pos;
+                    hasA = true;
+                }
+                f3 wi;
+                if (brdf_continue(A, m, S_nrm, seed, ridx, att, wi)) {
+                    depth += 1;
+                    if (!(depth >= A.max_bounces || att_stop(A, att))) {
+                        b_o = add(S_pos, muls(wi, A.eps));
+                        b_d = wi;
+                        b_tmin = A.t_min;
+                        b_tmax = A.t_max;
+                        kindB = K_PATH;
+                    }
+                }
+                if (!hasA && kindB == K_NONE) ended = true;
+            }
+            if (!__any(ended)) break;
+        }
     }
+    flush_counters(counters, lane, trav, iters);
+}
+
+// ======================================================================================
+// Variant 3, kernel 1: primary pre-pass, one pixel per lane.  Traces every primary ray once
+// (all lanes busy, no divergence), finishes miss / light pixels in closed form (their samples
+// never touch the RNG, :424-428), and appends every other pixel with its primary hit record to
+// a compact list for the path kernel (one atomic per wave).
+// ======================================================================================
+__global__ __launch_bounds__(kBlock) void games101_primary_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
+    const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
+    const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
+    SurfRecord *__restrict__ surf)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t pix = blockIdx.x * kBlock + threadIdx.x;
+    const bool live = pix < A.n_pixels;
+    bool is_surf = false;
+    f3 hpos = mk(0, 0, 0), hn = mk(0, 0, 0);
+    uint32_t hmat = 0;
+    if (live) {
+        float u_, v_, tmin, tmax;
+        f3 o, d;
+        pixel_uv(A, pix, u_, v_);
+        primary_ray(A, u_, v_, o, d, tmin, tmax);
+        int best = -1;
+        float bt = tmax;
+#pragma unroll 2
+        for (uint32_t i = 0; i < A.n_faces; ++i) {
+            float t;
+            if (tri_accept(tri[i], o, d, tmin, bt, t)) { bt = t; best = (int)i; }
+        }
+        if (best >= 0) hit_record(tri, faces, verts, best, o, d, bt, hpos, hn, hmat);
+        const bool miss = best < 0;
+        const bool is_light = !miss && mats[hmat].ty == kLight;
+        if (miss || is_light) {
+            const f3 L = miss ? mk(0.1f, 0.1f, 0.1f) : ld3(mats[hmat].albedo);
+            const f3 Ls = divs(L, (float)A.spp);
+            f3 acc = mk(0, 0, 0);
+            for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, Ls);
+            store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
+        } else {
+            is_surf = true;
+        }
+    }
+    const uint64_t m = __ballot(is_surf);
+    if (m) {
+        const int leader = (int)__builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == (uint32_t)leader)
+            base = atomicAdd((unsigned int *)&counters[3], (unsigned int)__builtin_popcountll(m));
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+        if (is_surf) {
+            SurfRecord r;
+            r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.mat = hmat;
+            r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.pix = pix;
+            surf[base + rank_in(m)] = r;
+        }
+    }
+    const uint64_t lv = __ballot(live);
+    if (lane == 0 && lv) atomicAdd(&counters[0], (unsigned long long)__builtin_popcountll(lv));
+}
+
+// ======================================================================================
+// Variant 3, kernel 2: the dual-ray machine over the surface pixels of the pre-pass.  Every
+// pixel starts with a surface event at its cached primary hit, so no iteration is spent on
+// primary rays and every lane enters the scan with a shadow and (usually) a path ray.
+// ======================================================================================
+#ifndef RVCP_PATH_MIN_WAVES
+#define RVCP_PATH_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
+    const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];   // tail: ray rank -> owner lane
+    const uint32_t lane = lane_id();
+    // the queue runs over the pre-pass's compact list; its length is in counters[3]
+    FrameArgs Q = A;
+    Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
+    Queue q = queue_init(Q);
+    const float sppf = (float)A.spp;
+
+    bool need_pixel = true, done = false, ended = false, surf_ev = false;
+    uint32_t pix = 0, k = 0, depth = 0, trav = 0, iters = 0;
+    float seed = 0.0f, ridx = 0.0f;
+    f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
+    f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0);
+    uint32_t P_mat = 0;
+    f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0);
+    uint32_t S_mat = 0;
+    bool hasA = false;
+    f3 a_o = mk(0, 0, 0), a_d = mk(0, 0, 1), a_p = mk(0, 0, 0), nee_C = mk(0, 0, 0);
+    float nee_dist = 0.0f;
+    bool hasB = false;
+    f3 b_o = mk(0, 0, 0), b_d = mk(0, 0, 1);
+
+    for (;;) {
+        // ---- settle: end samples, take pixels, emit surface events ----
+        for (;;) {
+            if (ended) {                                            // color += L / SPP (:495)
+                ended = false;
+                acc = add(acc, divs(col, sppf));
+                k += 1;
+                if (k >= A.spp) {
+                    store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
+                    need_pixel = true;
+                } else {
+                    depth = 0;
+                    att = mk(1, 1, 1);
+                    col = mk(0, 0, 0);
+                    S_pos = P_pos; S_nrm = P_nrm; S_mat = P_mat;
+                    surf_ev = true;
+                }
+            }
+            {   // new pixels (wave-uniform control flow)
+                bool got;
+                uint32_t slot = 0;
+                queue_take(q, __ballot(need_pixel && !done), lane, Q, counters, got, slot);
+                if (got) {
+                    const SurfRecord r = surf[slot];
+                    pix = r.pix;
+                    P_pos = ld3(r.pos); P_nrm = ld3(r.nrm); P_mat = r.mat;
+                    float u_, v_;
+                    pixel_uv(A, pix, u_, v_);
+                    seed = pixel_seed(A, u_, v_);
+                    ridx = 0.0f;
+                    k = 0;
+                    acc = mk(0, 0, 0);
+                    depth = 0;
+                    att = mk(1, 1, 1);
+                    col = mk(0, 0, 0);
+                    S_pos = P_pos; S_nrm = P_nrm; S_mat = P_mat;
+                    need_pixel = false;
+                    surf_ev = true;
+                } else if (need_pixel && q.exhausted) {
+                    done = true;
+                }
+            }
+            if (surf_ev) {                                          // :431-478
+                surf_ev = false;
+                const MatRecord m = mats[S_mat];
+                f3 ws;
+                if (nee_sample(A, lights, m, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist, ws)) {
+                    a_o = add(S_pos, muls(ws, A.eps));
+                    a_d = ws;
+                    a_p = S_pos;
+                    hasA = true;
+                }
+                f3 wi;
+                if (brdf_continue(A, m, S_nrm, seed, ridx, att, wi)) {
+                    depth += 1;
+                    if (!(depth >= A.max_bounces || att_stop(A, att))) {
+                        b_o = add(S_pos, muls(wi, A.eps));
+                        b_d = wi;
+                        hasB = true;
+                    }
+                }
+                if (!hasA && !hasB) ended = true;
+            }
+            if (!__any(ended)) break;
+        }
+        const uint64_t mA = __ballot(hasA), mB = __ballot(hasB);
+        if ((mA | mB) == 0ull) break;
+        iters += 1;
+        trav += (hasA ? 1u : 0u) + (hasB ? 1u : 0u);
+
+        int bestA = -1, bestB = -1;
+        float btA = A.t_max, btB = A.t_max;
+        const uint32_t na = (uint32_t)__builtin_popcountll(mA);
+        const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
+        if (q.exhausted && nr <= kWave / 2) {
+            // ---- tail: R lanes per ray, each scanning every R-th triangle ----
+            // The frame queue is empty, so what is left are the serial sample chains of the
+            // last pixels.  The sequential scan keeps (min t, largest index among equal t)
+            // (:288-295), so partial scans over disjoint face subsets combined with that same
+            // order give the identical nearest hit.
+            uint32_t R = 2;
+            while (nr * R * 2 <= (uint32_t)kWave) R *= 2;
+            uint8_t *tab = tail_tab[threadIdx.x / kWave];
+            if (hasA) tab[rank_in(mA)] = (uint8_t)lane;
+            if (hasB) tab[na + rank_in(mB)] = (uint8_t)lane;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t j = lane / R, part = lane % R;
+            const bool worker = j < nr;
+            const int owner = worker ? (int)tab[j] : (int)lane;
+            const bool isA = j < na;
+            f3 o, d;
+            {
+                const f3 oa = mk(__shfl(a_o.x, owner), __shfl(a_o.y, owner), __shfl(a_o.z, owner));
+                const f3 da = mk(__shfl(a_d.x, owner), __shfl(a_d.y, owner), __shfl(a_d.z, owner));
+                const f3 ob = mk(__shfl(b_o.x, owner), __shfl(b_o.y, owner), __shfl(b_o.z, owner));
+                const f3 db = mk(__shfl(b_d.x, owner), __shfl(b_d.y, owner), __shfl(b_d.z, owner));
+                o = isA ? oa : ob;
+                d = isA ? da : db;
+            }
+            float bt = A.t_max;
+            int best = -1;
+            if (worker) {
+                for (uint32_t i = part; i < A.n_faces; i += R) {
+                    float t;
+                    if (tri_accept(tri[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
+                }
+            }
+            for (uint32_t off = R >> 1; off >= 1; off >>= 1) {
+                const float ot = __shfl_xor(bt, (int)off);
+                const int ob = __shfl_xor(best, (int)off);
+                if (ot < bt || (ot == bt && ob > best)) { bt = ot; best = ob; }
+            }
+            const int srcA = hasA ? (int)(rank_in(mA) * R) : (int)lane;
+            const int srcB = hasB ? (int)((na + rank_in(mB)) * R) : (int)lane;
+            const float tA_ = __shfl(bt, srcA), tB_ = __shfl(bt, srcB);
+            const int iA_ = __shfl(best, srcA), iB_ = __shfl(best, srcB);
+            if (hasA) { btA = tA_; bestA = iA_; }
+            if (hasB) { btB = tB_; bestB = iB_; }
+        } else {
+            // ---- scan: both rays against every triangle (wave-uniform face index) ----
+#pragma unroll 2
+            for (uint32_t i = 0; i < A.n_faces; ++i) {
+                const TriRecord T = tri[i];
+                float tA, tB;
+                if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
+                if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
+            }
+        }
+
+        // ---- resolve A: visibility of the light sample (:447-459) ----
+        if (hasA) {
+            const f3 hp = bestA >= 0 ? add(a_o, muls(a_d, btA))
+                                     : mk(__builtin_inff(), __builtin_inff(), __builtin_inff());
+            const float dist_blocked = len(sub(hp, a_p));
+            if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) col = add(col, nee_C);
+        }
+        // ---- resolve B: next bounce (:421-429) ----
+        if (hasB) {
+            if (bestB < 0) {
+                col = add(col, mk(0.1f, 0.1f, 0.1f));
+                ended = true;
+            } else {
+                f3 hpos, hn;
+                uint32_t hmat;
+                hit_record(tri, faces, verts, bestB, b_o, b_d, btB, hpos, hn, hmat);
+                if (mats[hmat].ty == kLight) {
+                    ended = true;       // depth >= 1: no emission term (:426)
+                } else {
+                    S_pos = hpos; S_nrm = hn; S_mat = hmat;
+                    surf_ev = true;
+                }
+            }
+        } else if (hasA) {
+            ended = true;       // the path ended at its last surface event (RR / depth / att)
+        }
+        hasA = false;
+        hasB = false;
+    }
+    flush_counters(counters, lane, trav, iters);
 }
 
 // Frame assembly after the RCCL gather: slot k holds shard k's stripes packed.
@@ -426,10 +931,30 @@ extern "C" int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::Tri
                                     unsigned long long *counters, uint32_t grid_blocks,
                                     void *stream)
 {
-    hipLaunchKernelGGL(rvcp::games101_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+    auto kern = args->variant == 2 ? rvcp::games101_dual_kernel : rvcp::games101_kernel;
+    hipLaunchKernelGGL(kern, dim3(grid_blocks), dim3(rvcp::kBlock), 0, (hipStream_t)stream,
+                       *args, tri, (const rvcp_face_t *)faces, (const rvcp_vertex_t *)verts, mats,
+                       lights, gamma_t, out_rgba, out_lin, counters);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
+                                       const void *faces, const void *verts,
+                                       const rvcp::MatRecord *mats,
+                                       const rvcp::LightRecord *lights, const float *gamma_t,
+                                       uint32_t *out_rgba, float *out_lin,
+                                       unsigned long long *counters, rvcp::SurfRecord *surf,
+                                       uint32_t grid_blocks, void *stream)
+{
+    const uint32_t pre_blocks = (args->n_pixels + rvcp::kBlock - 1) / rvcp::kBlock;
+    hipLaunchKernelGGL(rvcp::games101_primary_kernel, dim3(pre_blocks), dim3(rvcp::kBlock), 0,
+                       (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
+                       (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
+                       surf);
+    hipLaunchKernelGGL(rvcp::games101_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                        (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
                        (const rvcp_vertex_t *)verts, mats, lights, gamma_t, out_rgba, out_lin,
-                       counters);
+                       counters, surf);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -446,18 +971,21 @@ extern "C" int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows
 extern "C" int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n, uint32_t rgba,
                                 void *stream)
 {
-    const uint32_t blocks = n ? (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096 : 1;
+    const uint32_t blocks = n ? ((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096) : 1;
     hipLaunchKernelGGL(rvcp::fill_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        out_rgba, out_lin, n, rgba);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-extern "C" int rvcp_games101_occupancy(int *blocks_per_cu)
+extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
 {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_kernel, rvcp::kBlock, 0) !=
-        hipSuccess)
-        return -2;
+    const hipError_t e = variant == 3
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel, rvcp::kBlock, 0)
+        : variant == 2
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_dual_kernel, rvcp::kBlock, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_kernel, rvcp::kBlock, 0);
+    if (e != hipSuccess) return -2;
     *blocks_per_cu = b;
     return 0;
 }

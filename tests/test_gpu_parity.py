@@ -39,11 +39,35 @@ def _assert_same(gpu, orc):
     assert int(stats["traversals"]) == o_trav
 
 
+VARIANTS = [1, 2, 3]       # kernel schedules (rvcp_config_t::kernel_variant); 0 = default
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("W,H,spp", [(64, 64, 4), (128, 128, 1), (37, 23, 3), (8, 8, 30),
                                      (1, 1, 7), (130, 3, 2)])
-def test_bitexact_cornell(cornell, W, H, spp):
-    cfg = rvcp_amd.abi.make_config(spp=spp)
+def test_bitexact_cornell(cornell, W, H, spp, variant):
+    cfg = rvcp_amd.abi.make_config(spp=spp, kernel_variant=variant)
     _assert_same(_gpu(cornell, cfg, W, H), _oracle(cornell, cfg, W, H))
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("case", ["quirk_off", "params", "no_lights", "random_mesh", "rr1"])
+def test_variants_bitexact(cornell, variant, case):
+    sc, kw = cornell, dict(spp=3)
+    if case == "quirk_off":
+        kw["lum_id_std140_quirk"] = 0
+    elif case == "params":
+        kw.update(max_bounces=2, attenuation_stop_eps=0.2, eps=0.01)
+    elif case == "rr1":
+        kw.update(rr_probability=1.0, max_bounces=4)
+    elif case == "no_lights":
+        mats = list(cornell.materials)
+        mats[3] = rvcp_amd.Material.new_lambertian([0.5, 0.5, 0.5])
+        sc = rvcp_amd.Scene(cornell.camera, mats, [], cornell.mesh)
+    elif case == "random_mesh":
+        sc = rvcp_amd.scene.with_random_triangles(cornell, 200)
+    cfg = rvcp_amd.abi.make_config(kernel_variant=variant, **kw)
+    _assert_same(_gpu(sc, cfg, 40, 36), _oracle(sc, cfg, 40, 36))
 
 
 def test_bitexact_quirk_off(cornell):
@@ -129,6 +153,18 @@ def c3_render(cornell):
         stats = rt.last_stats.copy()
         b = rt.render(1024, 1024, TIME)
     return cfg, a, lin, b, stats
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_c3_variants_identical(cornell, c3_render, variant):
+    """Every kernel schedule renders the identical full-size frame."""
+    cfg = rvcp_amd.abi.make_config(spp=30, kernel_variant=variant)
+    with rvcp_amd.RayTracer(cfg) as rt:
+        rt.upload_scene(cornell)
+        img = rt.render(1024, 1024, TIME)
+        trav = int(rt.last_stats["traversals"])
+    assert np.array_equal(img, c3_render[1])
+    assert trav == int(c3_render[4]["traversals"])
 
 
 def test_c3_deterministic(c3_render):

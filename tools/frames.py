@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Render N frames of a workload with one kernel variant (profiling driver for rocprofv3).
+
+  python tools/frames.py [--variant V] [--frames N] [--size S] [--spp P] [--tris T]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import rvcp_amd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--spp", type=int, default=30)
+    ap.add_argument("--tris", type=int, default=0)
+    a = ap.parse_args()
+    sc = rvcp_amd.Scene.default()
+    if a.tris:
+        sc = rvcp_amd.scene.with_random_triangles(sc, a.tris)
+    with rvcp_amd.RayTracer(spp=a.spp, kernel_variant=a.variant) as rt:
+        rt.upload_scene(sc)
+        for _ in range(a.frames):
+            rt.render(a.size, a.size, 123.0)
+            st = rt.last_stats
+            print(json.dumps({"variant": a.variant, "kernel_ms": round(float(st["kernel_ms"]), 3),
+                              "executed": int(st["traversals_executed"]),
+                              "wave_iterations": int(st["wave_iterations"])}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -37,7 +37,15 @@ for s in $STEPS; do
         bench2) run bench_c2 300 python bench.py --workload c2 --steps 50 --warmup 5 --no-cpu-baseline ;;
         rehearse2) run rehearse2 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
         rehearse4) run rehearse4 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 4 --steps 3 --warmup 1 ;;
+        rcp) run rcp_check 120 tools/build/rcp_check ;;
+        split) run split 300 python tools/exp_split.py ;;
+        split2) run split2 300 env RVCP_KERNEL_VARIANT=2 python tools/exp_split.py ;;
+        occ) run occ 400 bash tools/exp_occ.sh ;;
+        split3) run split3 300 env RVCP_KERNEL_VARIANT=3 python tools/exp_split.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+        sqpmc) run sqpmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 tools/frames.py --variant 2 --frames 2 ;;
+        sqpmc2) run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 tools/frames.py --variant 2 --frames 2 ;;
+        listpmc) run listpmc 120 rocprofv3 -L ;;
         pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     esac
 done
