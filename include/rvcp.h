@@ -113,9 +113,11 @@ typedef struct rvcp_config {
      * (ray_tracer_games101_branch.comp:109-111 vs vulkan.rs:473-478): element i is
      * ids[4*i] when 4*i < n_ids, else 0.  0 = the intended packed semantics. */
     int32_t lum_id_std140_quirk;
-    /* Kernel schedule, for A/B measurement only: 0 = the default (fastest), 1 = one ray per
-     * lane per iteration, 2 = shadow + continuation ray per lane per iteration.  Every
-     * schedule produces bit-identical frames. */
+    /* Kernel schedule, for A/B measurement only: 0 = automatic (3, or 4 for meshes of 4096+
+     * faces), 1 = one ray per lane per iteration, 2 = shadow + continuation ray per lane per
+     * iteration, 3 = primary pre-pass + 2 over surface pixels (scalar-cache scan), 4 = 3 with
+     * the scan staged through LDS tiles shared by the workgroup.  Every schedule produces
+     * bit-identical frames. */
     int32_t kernel_variant;
     uint32_t _reserved[5];
 } rvcp_config_t;

@@ -34,6 +34,7 @@ struct rvcp_ctx {
     rvcp_face_t *d_faces = nullptr;
     rvcp_vertex_t *d_verts = nullptr;
     MatRecord *d_mats = nullptr;
+    FaceShade *d_shade = nullptr;
     LightRecord *d_lights = nullptr;
     float *d_gamma = nullptr;
     unsigned long long *d_counters = nullptr;
@@ -135,6 +136,7 @@ void free_scene(rvcp_ctx *ctx)
     (void)hipFree(ctx->d_faces); ctx->d_faces = nullptr;
     (void)hipFree(ctx->d_verts); ctx->d_verts = nullptr;
     (void)hipFree(ctx->d_mats); ctx->d_mats = nullptr;
+    (void)hipFree(ctx->d_shade); ctx->d_shade = nullptr;
     (void)hipFree(ctx->d_lights); ctx->d_lights = nullptr;
     ctx->has_scene = false;
 }
@@ -284,6 +286,17 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         for (int c = 0; c < 3; c++) mats[i].alb_pi[c] = materials[i].albedo[c] / 3.1415926f;
         mats[i].pad = 0;
     }
+    std::vector<FaceShade> shade(n_faces);
+    for (uint32_t i = 0; i < n_faces; i++) {
+        FaceShade &fs = shade[i];
+        std::memset(&fs, 0, sizeof(fs));
+        std::memcpy(fs.n0, vertices[faces[i].vertices[0]].normal, 12);
+        std::memcpy(fs.n1, vertices[faces[i].vertices[1]].normal, 12);
+        std::memcpy(fs.n2, vertices[faces[i].vertices[2]].normal, 12);
+        fs.mat = faces[i].material_id;
+        fs.ty = mats[fs.mat].ty;
+        std::memcpy(fs.alb_pi, mats[fs.mat].alb_pi, 12);
+    }
     // light table (sample_light_games101, :384-404) with the std140 id quirk (:109-111)
     const bool quirk = ctx->cfg.lum_id_std140_quirk != 0;
     std::vector<LightRecord> lights(n_lum_face_ids ? n_lum_face_ids : 1);
@@ -316,6 +329,7 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         (rc = dev_upload<rvcp_face_t>(ctx, &ctx->d_faces, faces, n_faces)) ||
         (rc = dev_upload<rvcp_vertex_t>(ctx, &ctx->d_verts, vertices, n_vertices)) ||
         (rc = dev_upload<MatRecord>(ctx, &ctx->d_mats, mats.data(), n_materials)) ||
+        (rc = dev_upload<FaceShade>(ctx, &ctx->d_shade, shade.data(), n_faces)) ||
         (rc = dev_upload<LightRecord>(ctx, &ctx->d_lights, lights.data(), n_lum_face_ids)))
         return rc;
     ctx->n_faces = n_faces;
@@ -373,7 +387,8 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     A.light_total = ctx->light_total;
     A.light_pdf = ctx->light_pdf;
     A.want_linear = d_linear_rgb ? 1u : 0u;
-    A.variant = ctx->cfg.kernel_variant == 0 ? kDefaultVariant : ctx->cfg.kernel_variant;
+    A.variant = ctx->cfg.kernel_variant != 0 ? ctx->cfg.kernel_variant
+              : (ctx->n_faces >= kTiledMinFaces ? 4 : kDefaultVariant);
 
     // With MAX_BOUNCES == 0 or ATTENUATION_STOP_EPS > 1 every sample returns 0 before its
     // first traversal (:413-419): the frame is black.
@@ -392,7 +407,7 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
                 blocks = (uint32_t)ctx->grid_capacity[A.variant];
             if (blocks == 0) blocks = 1;
             A.static_chunks = blocks * (kBlock / kWave) * kChunk;
-            if (A.variant == 3) {
+            if (A.variant >= 3) {
                 if (ctx->cap_surf < A.n_pixels) {
                     (void)hipFree(ctx->d_surf);
                     ctx->d_surf = nullptr;
@@ -403,7 +418,8 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
                 rc = rvcp_launch_games101_v3(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
                                              ctx->d_mats, ctx->d_lights, ctx->d_gamma,
                                              (uint32_t *)d_rgba8, (float *)d_linear_rgb,
-                                             ctx->d_counters, ctx->d_surf, blocks, s);
+                                             ctx->d_counters, ctx->d_surf, ctx->d_shade,
+                                             blocks, s);
             } else {
                 rc = rvcp_launch_games101(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts, ctx->d_mats,
                                           ctx->d_lights, ctx->d_gamma, (uint32_t *)d_rgba8,

@@ -15,8 +15,12 @@ constexpr uint32_t kChunk = 64;
 // Kernel schedules (rvcp_config_t::kernel_variant): 1 = one ray per lane per iteration,
 // 2 = shadow + continuation ray per lane per iteration, 3 = primary pre-pass kernel + the
 // variant-2 loop over surface pixels only.
+// 4 = variant 3 with the triangle scan staged through LDS tiles shared by the workgroup
+// (selected automatically for meshes of kTiledMinFaces faces or more).
 constexpr int kDefaultVariant = 3;
-constexpr int kMaxVariant = 3;
+constexpr int kMaxVariant = 4;
+constexpr uint32_t kTile = 256;             // triangles per LDS tile (12 KiB)
+constexpr uint32_t kTiledMinFaces = 4096;
 
 // One triangle as the brute-force scan reads it: v0, e1 = v1 - v0, e2 = v2 - v0, computed on
 // the host with the same float subtractions the shader performs per test
@@ -53,6 +57,21 @@ struct alignas(16) SurfRecord {
     uint32_t pix;
 };
 static_assert(sizeof(SurfRecord) == 32, "SurfRecord is 32 B");
+
+// Per-face shading data, gathered by index once per traversal for the nearest face only:
+// the three vertex normals (interpolated at :262-266), the face material (:272) with its type
+// and albedo / PI.  One independent 64-B gather instead of face -> vertices -> material.
+struct alignas(16) FaceShade {
+    float n0[3];
+    uint32_t mat;
+    float n1[3];
+    uint32_t ty;
+    float n2[3];
+    uint32_t pad0;
+    float alb_pi[3];
+    uint32_t pad1;
+};
+static_assert(sizeof(FaceShade) == 64, "FaceShade is 64 B");
 
 // Per-material record: albedo + type (MaterialBuffer, :74-83) and albedo / PI, the value
 // lambertian_brdf_eval returns (:346), divided once on the host with the same float division.
@@ -99,7 +118,8 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *
                             const void *faces, const void *verts, const rvcp::MatRecord *mats,
                             const rvcp::LightRecord *lights, const float *gamma_t,
                             uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
-                            rvcp::SurfRecord *surf, uint32_t grid_blocks, void *stream);
+                            rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
+                            uint32_t grid_blocks, void *stream);
 int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows, uint32_t width,
                          uint32_t height, uint32_t shard_count, uint32_t *frame, void *stream);
 int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n_pixels, uint32_t rgba,

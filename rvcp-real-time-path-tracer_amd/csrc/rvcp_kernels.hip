@@ -72,6 +72,14 @@ __device__ __forceinline__ float pt_sinf(float x) {
     return (j & 2) ? -v : v;
 }
 
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
 // rand(), :159-162: index += 1; fract(sin(seed + index) * 43758.5453)
 __device__ __forceinline__ float rnd(float seed, float &idx) {
     idx = idx + 1.0f;
@@ -186,6 +194,25 @@ __device__ __forceinline__ void primary_ray(const FrameArgs &A, float u_, float 
     tmax = A.t_far * t_coef;
 }
 
+// Hit record of face `best` from its FaceShade record (same arithmetic as hit_record).
+__device__ __forceinline__ void hit_shade(const TriRecord *__restrict__ tri,
+                                          const FaceShade *__restrict__ shade, int best, f3 o,
+                                          f3 d, float t, f3 &pos, f3 &n, FaceShade &fs) {
+    const TriRecord T = tri[best];
+    fs = shade[best];
+    const f3 s = mk(o.x - T.v0[0], o.y - T.v0[1], o.z - T.v0[2]);
+    const f3 e1 = ld3(T.e1), e2 = ld3(T.e2);
+    const f3 s1 = cross(d, e2);
+    const f3 s2 = cross(s, e1);
+    const float f = rcp_ieee(dot(s1, e1));
+    const float b1 = f * dot(s1, s);
+    const float b2 = f * dot(s2, d);
+    n = normalize(add(add(muls(ld3(fs.n0), 1.0f - b1 - b2), muls(ld3(fs.n1), b1)),
+                      muls(ld3(fs.n2), b2)));
+    if (dot(n, d) > 0.0f) n = neg(n);
+    pos = add(o, muls(d, t));
+}
+
 // Primary ray of pixel `pix` (main :486-491): srand + sample_ray.
 __device__ __forceinline__ void start_pixel(const FrameArgs &A, uint32_t pix, float &seed,
                                             float &ridx, f3 &o, f3 &d, float &tmin, float &tmax) {
@@ -200,7 +227,7 @@ __device__ __forceinline__ void start_pixel(const FrameArgs &A, uint32_t pix, fl
 // the contribution C the shadow ray will add if it sees the sample (:450-458), and the
 // shadow ray direction.  Returns false when there is no luminous face.
 __device__ __forceinline__ bool nee_sample(const FrameArgs &A, const LightRecord *__restrict__ lights,
-                                           const MatRecord &m, f3 S_pos, f3 S_nrm, f3 att,
+                                           f3 alb_pi, f3 S_pos, f3 S_nrm, f3 att,
                                            float seed, float &ridx, f3 &C, float &dist, f3 &ws) {
     const float pl = rnd(seed, ridx) * A.light_total;
     uint32_t li = A.n_lights;
@@ -217,7 +244,7 @@ __device__ __forceinline__ bool nee_sample(const FrameArgs &A, const LightRecord
     dist = len(dv);                                                                // :438
     ws = divs(dv, dist);                                                           // :439
     const float cosp = dot(S_nrm, ws);
-    const f3 f = cosp > 0.0f ? ld3(m.alb_pi) : mk(0, 0, 0);                        // :344-349
+    const f3 f = cosp > 0.0f ? alb_pi : mk(0, 0, 0);                               // :344-349
     C = mulv(mulv(att, ld3(L.le)), f);                                             // :450-458
     C = muls(C, cosp);
     C = muls(C, dot(ld3(L.n), neg(ws)));
@@ -247,17 +274,70 @@ __device__ __forceinline__ bool brdf_continue(const FrameArgs &A, const MatRecor
     return true;
 }
 
+// Continuation, after the direction: the attenuation update of :465-471 for direction wi
+// (wi = normalize(h), h the hemisphere-flipped unit-ball sample, :207-214).
+__device__ __forceinline__ void brdf_finish(const FrameArgs &A, f3 alb_pi, f3 S_nrm, f3 p,
+                                            f3 &att, f3 &wi) {
+    const f3 h = dot(p, S_nrm) > 0.0f ? p : neg(p);
+    wi = normalize(h);
+    const float cosw = dot(S_nrm, wi);
+    const f3 f = cosw > 0.0f ? alb_pi : mk(0, 0, 0);
+    const float pdf = dot(wi, S_nrm) > 0.0f ? 0.5f / 3.1415926f : 0.0f;
+    const float denom = __builtin_fmaxf(0.1f, pdf) * A.rr;
+    att = mulv(att, divs(muls(f, cosw), denom));
+}
+
+// random_in_unit_sphere (:195-201) for every lane with `need`, cooperatively: each round the
+// n lanes still rejecting get K = 2^floor(log2(64/n)) lanes, which evaluate K consecutive
+// candidates of the OWNER's rand() stream (candidate c uses indices ridx+3c+1..ridx+3c+3, the
+// exact integers the sequential loop would reach by +1.0f steps).  The owner keeps the first
+// accepted candidate in stream order and advances ridx just past it, so the result and the
+// rand() index are bit-identical to the do-while; a wave needs ~3 rounds instead of the ~7
+// its unluckiest lane needs sequentially.  Wave-uniform control flow; `tab` is this wave's
+// 64-byte LDS scratch.
+__device__ __forceinline__ void coop_unit_sphere(bool need, float seed, float &ridx, f3 &p_out,
+                                                 uint32_t lane, uint8_t *tab) {
+    for (;;) {
+        const uint64_t M = __ballot(need);
+        if (M == 0ull) break;
+        const uint32_t n = (uint32_t)__builtin_popcountll(M);
+        const uint32_t lgK = 31u - (uint32_t)__builtin_clz((uint32_t)kWave / n);   // floor(log2(64/n))
+        const uint32_t K = 1u << lgK;
+        const uint32_t r = rank_in(M);
+        if (need) tab[r] = (uint8_t)lane;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t j = lane >> lgK, c = lane & (K - 1u);
+        const bool worker = j < n;
+        const int owner = worker ? (int)tab[j] : (int)lane;
+        const float s_seed = __shfl(seed, owner);
+        const float base = __shfl(ridx, owner) + (float)(3u * c);
+        const float rx = fractf(pt_sinf(s_seed + (base + 1.0f)) * 43758.5453f);
+        const float ry = fractf(pt_sinf(s_seed + (base + 2.0f)) * 43758.5453f);
+        const float rz = fractf(pt_sinf(s_seed + (base + 3.0f)) * 43758.5453f);
+        const f3 p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
+        const uint64_t AM = __ballot(worker && !(dot(p, p) >= 1.0f));
+        const uint64_t segmask = K >= 64u ? ~0ull : ((1ull << K) - 1ull);
+        const uint64_t seg = need ? ((AM >> (r << lgK)) & segmask) : 0ull;
+        const bool got = seg != 0ull;
+        const uint32_t cstar = got ? (uint32_t)__builtin_ctzll(seg) : 0u;
+        const int src = got ? (int)((r << lgK) + cstar) : (int)lane;
+        const f3 pp = mk(__shfl(p.x, src), __shfl(p.y, src), __shfl(p.z, src));
+        if (got) {
+            p_out = pp;
+            ridx = ridx + (float)(3u * (cstar + 1u));
+            need = false;
+        } else if (need) {
+            ridx = ridx + (float)(3u * K);
+        }
+    }
+}
+
 __device__ __forceinline__ bool att_stop(const FrameArgs &A, f3 att) {          // :415-419
     return att.x < A.att_stop && att.y < A.att_stop && att.z < A.att_stop;
 }
 
-__device__ __forceinline__ uint32_t lane_id() {
-    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
-__device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
 
 // Wave-uniform frame-queue state: [next, end) pixels owned by this wave.
 struct Queue {
@@ -384,8 +464,8 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
             }
             if (action == A_SURF) {                                 // :431-447
                 f3 ws;
-                if (!nee_sample(A, lights, mats[S_mat], S_pos, S_nrm, att, seed, ridx, nee_C,
-                                nee_dist, ws)) {
+                if (!nee_sample(A, lights, ld3(mats[S_mat].alb_pi), S_pos, S_nrm, att, seed, ridx,
+                                nee_C, nee_dist, ws)) {
                     action = A_RR;
                 } else {
                     ro = add(S_pos, muls(ws, A.eps));
@@ -611,7 +691,8 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
                 surf = false;
                 const MatRecord m = mats[S_mat];
                 f3 ws;
-                if (nee_sample(A, lights, m, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist, ws)) {
+                if (nee_sample(A, lights, ld3(m.alb_pi), S_pos, S_nrm, att, seed, ridx, nee_C,
+                               nee_dist, ws)) {
                     a_o = add(S_pos, muls(ws, A.eps));
                     a_d = ws;
                     a_p = S_pos;
@@ -647,7 +728,7 @@ __global__ __launch_bounds__(kBlock) void games101_primary_kernel(
     const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
     const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    SurfRecord *__restrict__ surf)
+    SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade)
 {
     const uint32_t lane = lane_id();
     const uint32_t pix = blockIdx.x * kBlock + threadIdx.x;
@@ -667,9 +748,11 @@ __global__ __launch_bounds__(kBlock) void games101_primary_kernel(
             float t;
             if (tri_accept(tri[i], o, d, tmin, bt, t)) { bt = t; best = (int)i; }
         }
-        if (best >= 0) hit_record(tri, faces, verts, best, o, d, bt, hpos, hn, hmat);
+        FaceShade fs;
+        fs.ty = 0;
+        if (best >= 0) { hit_shade(tri, shade, best, o, d, bt, hpos, hn, fs); hmat = fs.mat; }
         const bool miss = best < 0;
-        const bool is_light = !miss && mats[hmat].ty == kLight;
+        const bool is_light = !miss && fs.ty == kLight;
         if (miss || is_light) {
             const f3 L = miss ? mk(0.1f, 0.1f, 0.1f) : ld3(mats[hmat].albedo);
             const f3 Ls = divs(L, (float)A.spp);
@@ -699,21 +782,26 @@ __global__ __launch_bounds__(kBlock) void games101_primary_kernel(
 }
 
 // ======================================================================================
-// Variant 3, kernel 2: the dual-ray machine over the surface pixels of the pre-pass.  Every
+// Variant 3/4, kernel 2: the dual-ray machine over the surface pixels of the pre-pass.  Every
 // pixel starts with a surface event at its cached primary hit, so no iteration is spent on
 // primary rays and every lane enters the scan with a shadow and (usually) a path ray.
+//   TILED = false (variant 3): each wave scans the triangles with wave-uniform scalar loads
+//           (the whole Cornell scene stays in the scalar cache);
+//   TILED = true  (variant 4, large meshes): the workgroup's waves scan in lockstep over
+//           triangle tiles that the workgroup loads once, coalesced, into LDS -- the triangle
+//           stream is read from L2/HBM once per workgroup instead of once per wave.
 // ======================================================================================
 #ifndef RVCP_PATH_MIN_WAVES
 #define RVCP_PATH_MIN_WAVES 1
 #endif
-__global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_kernel(
-    FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
-    const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
+template <bool TILED>
+__device__ __forceinline__ void path_body(
+    const FrameArgs &A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
-    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf)
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile)
 {
-    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];   // tail: ray rank -> owner lane
     const uint32_t lane = lane_id();
     // the queue runs over the pre-pass's compact list; its length is in counters[3]
     FrameArgs Q = A;
@@ -725,10 +813,8 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
     uint32_t pix = 0, k = 0, depth = 0, trav = 0, iters = 0;
     float seed = 0.0f, ridx = 0.0f;
     f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
-    f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0);
-    uint32_t P_mat = 0;
-    f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0);
-    uint32_t S_mat = 0;
+    f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0), P_alb = mk(0, 0, 0);
+    f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0), S_alb = mk(0, 0, 0);
     bool hasA = false;
     f3 a_o = mk(0, 0, 0), a_d = mk(0, 0, 1), a_p = mk(0, 0, 0), nee_C = mk(0, 0, 0);
     float nee_dist = 0.0f;
@@ -749,7 +835,7 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
                     depth = 0;
                     att = mk(1, 1, 1);
                     col = mk(0, 0, 0);
-                    S_pos = P_pos; S_nrm = P_nrm; S_mat = P_mat;
+                    S_pos = P_pos; S_nrm = P_nrm; S_alb = P_alb;
                     surf_ev = true;
                 }
             }
@@ -760,7 +846,7 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
                 if (got) {
                     const SurfRecord r = surf[slot];
                     pix = r.pix;
-                    P_pos = ld3(r.pos); P_nrm = ld3(r.nrm); P_mat = r.mat;
+                    P_pos = ld3(r.pos); P_nrm = ld3(r.nrm); P_alb = ld3(mats[r.mat].alb_pi);
                     float u_, v_;
                     pixel_uv(A, pix, u_, v_);
                     seed = pixel_seed(A, u_, v_);
@@ -770,46 +856,124 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
                     depth = 0;
                     att = mk(1, 1, 1);
                     col = mk(0, 0, 0);
-                    S_pos = P_pos; S_nrm = P_nrm; S_mat = P_mat;
+                    S_pos = P_pos; S_nrm = P_nrm; S_alb = P_alb;
                     need_pixel = false;
                     surf_ev = true;
                 } else if (need_pixel && q.exhausted) {
                     done = true;
                 }
             }
-            if (surf_ev) {                                          // :431-478
+            bool need_dir = false;
+            if (surf_ev) {                                          // :431-462
                 surf_ev = false;
-                const MatRecord m = mats[S_mat];
                 f3 ws;
-                if (nee_sample(A, lights, m, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist, ws)) {
+                if (nee_sample(A, lights, S_alb, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist,
+                               ws)) {
                     a_o = add(S_pos, muls(ws, A.eps));
                     a_d = ws;
                     a_p = S_pos;
                     hasA = true;
                 }
+                need_dir = !(rnd(seed, ridx) > A.rr);               // Russian roulette :462
+                if (!need_dir && !hasA) ended = true;
+            }
+            f3 p = mk(0, 0, 0);
+            coop_unit_sphere(need_dir, seed, ridx, p, lane, tail_tab[threadIdx.x / kWave]);
+            if (need_dir) {                                         // :464-478
                 f3 wi;
-                if (brdf_continue(A, m, S_nrm, seed, ridx, att, wi)) {
-                    depth += 1;
-                    if (!(depth >= A.max_bounces || att_stop(A, att))) {
-                        b_o = add(S_pos, muls(wi, A.eps));
-                        b_d = wi;
-                        hasB = true;
-                    }
+                brdf_finish(A, S_alb, S_nrm, p, att, wi);
+                depth += 1;
+                if (!(depth >= A.max_bounces || att_stop(A, att))) {
+                    b_o = add(S_pos, muls(wi, A.eps));
+                    b_d = wi;
+                    hasB = true;
                 }
                 if (!hasA && !hasB) ended = true;
             }
             if (!__any(ended)) break;
         }
         const uint64_t mA = __ballot(hasA), mB = __ballot(hasB);
-        if ((mA | mB) == 0ull) break;
-        iters += 1;
+        const bool wave_active = (mA | mB) != 0ull;
+        if (TILED) {
+            // every wave of the workgroup keeps loading tiles until the whole group is done
+            if (!__syncthreads_or(wave_active ? 1 : 0)) break;
+        } else if (!wave_active) {
+            break;
+        }
+        if (wave_active) iters += 1;
         trav += (hasA ? 1u : 0u) + (hasB ? 1u : 0u);
 
         int bestA = -1, bestB = -1;
         float btA = A.t_max, btB = A.t_max;
         const uint32_t na = (uint32_t)__builtin_popcountll(mA);
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
-        if (q.exhausted && nr <= kWave / 2) {
+        const bool tail = wave_active && q.exhausted && nr <= kWave / 2;
+        if (TILED) {
+            // ---- LDS-tiled scan (optionally with the tail partition below) ----
+            uint32_t R = 1, part = 0;
+            bool worker = false;
+            f3 o = a_o, d = a_d;
+            if (tail) {
+                R = 2;
+                while (nr * R * 2 <= (uint32_t)kWave) R *= 2;
+                uint8_t *tab = tail_tab[threadIdx.x / kWave];
+                if (hasA) tab[rank_in(mA)] = (uint8_t)lane;
+                if (hasB) tab[na + rank_in(mB)] = (uint8_t)lane;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t j = lane / R;
+                part = lane % R;
+                worker = j < nr;
+                const int owner = worker ? (int)tab[j] : (int)lane;
+                const bool isA = j < na;
+                const f3 oa = mk(__shfl(a_o.x, owner), __shfl(a_o.y, owner), __shfl(a_o.z, owner));
+                const f3 da = mk(__shfl(a_d.x, owner), __shfl(a_d.y, owner), __shfl(a_d.z, owner));
+                const f3 ob = mk(__shfl(b_o.x, owner), __shfl(b_o.y, owner), __shfl(b_o.z, owner));
+                const f3 db = mk(__shfl(b_d.x, owner), __shfl(b_d.y, owner), __shfl(b_d.z, owner));
+                o = isA ? oa : ob;
+                d = isA ? da : db;
+            }
+            float bt = A.t_max;
+            int best = -1;
+            for (uint32_t base = 0; base < A.n_faces; base += kTile) {
+                const uint32_t n = A.n_faces - base < kTile ? A.n_faces - base : kTile;
+                const float4 *src = reinterpret_cast<const float4 *>(tri + base);
+                float4 *dst = reinterpret_cast<float4 *>(tile);
+                for (uint32_t e = threadIdx.x; e < 3 * n; e += kBlock) dst[e] = src[e];
+                __syncthreads();
+                if (tail) {
+                    if (worker) {
+                        for (uint32_t i = part; i < n; i += R) {
+                            float t;
+                            if (tri_accept(tile[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)(base + i); }
+                        }
+                    }
+                } else if (wave_active) {
+#pragma unroll 2
+                    for (uint32_t i = 0; i < n; ++i) {
+                        const TriRecord T = tile[i];
+                        float tA, tB;
+                        if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
+                        if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
+                    }
+                }
+                __syncthreads();
+            }
+            if (tail) {
+                for (uint32_t off = R >> 1; off >= 1; off >>= 1) {
+                    const float ot = __shfl_xor(bt, (int)off);
+                    const int ob = __shfl_xor(best, (int)off);
+                    if (ot < bt || (ot == bt && ob > best)) { bt = ot; best = ob; }
+                }
+                const int srcA = hasA ? (int)(rank_in(mA) * R) : (int)lane;
+                const int srcB = hasB ? (int)((na + rank_in(mB)) * R) : (int)lane;
+                const float tA_ = __shfl(bt, srcA), tB_ = __shfl(bt, srcB);
+                const int iA_ = __shfl(best, srcA), iB_ = __shfl(best, srcB);
+                if (hasA) { btA = tA_; bestA = iA_; }
+                if (hasB) { btB = tB_; bestB = iB_; }
+            }
+        } else if (tail) {
             // ---- tail: R lanes per ray, each scanning every R-th triangle ----
             // The frame queue is empty, so what is left are the serial sample chains of the
             // last pixels.  The sequential scan keeps (min t, largest index among equal t)
@@ -880,12 +1044,12 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
                 ended = true;
             } else {
                 f3 hpos, hn;
-                uint32_t hmat;
-                hit_record(tri, faces, verts, bestB, b_o, b_d, btB, hpos, hn, hmat);
-                if (mats[hmat].ty == kLight) {
+                FaceShade fs;
+                hit_shade(tri, shade, bestB, b_o, b_d, btB, hpos, hn, fs);
+                if (fs.ty == kLight) {
                     ended = true;       // depth >= 1: no emission term (:426)
                 } else {
-                    S_pos = hpos; S_nrm = hn; S_mat = hmat;
+                    S_pos = hpos; S_nrm = hn; S_alb = ld3(fs.alb_pi);
                     surf_ev = true;
                 }
             }
@@ -896,6 +1060,31 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
         hasB = false;
     }
     flush_counters(counters, lane, trav, iters);
+}
+
+__global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];   // tail: ray rank -> owner lane
+    path_body<false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade,
+                     tail_tab, nullptr);
+}
+
+__global__ __launch_bounds__(kBlock) void games101_tiled_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    __shared__ TriRecord tile[kTile];
+    path_body<true>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade,
+                    tail_tab, tile);
 }
 
 // Frame assembly after the RCCL gather: slot k holds shard k's stripes packed.
@@ -944,17 +1133,18 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                                        const rvcp::LightRecord *lights, const float *gamma_t,
                                        uint32_t *out_rgba, float *out_lin,
                                        unsigned long long *counters, rvcp::SurfRecord *surf,
-                                       uint32_t grid_blocks, void *stream)
+                                       const rvcp::FaceShade *shade, uint32_t grid_blocks,
+                                       void *stream)
 {
     const uint32_t pre_blocks = (args->n_pixels + rvcp::kBlock - 1) / rvcp::kBlock;
     hipLaunchKernelGGL(rvcp::games101_primary_kernel, dim3(pre_blocks), dim3(rvcp::kBlock), 0,
                        (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
                        (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
-                       surf);
-    hipLaunchKernelGGL(rvcp::games101_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
-                       (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
-                       (const rvcp_vertex_t *)verts, mats, lights, gamma_t, out_rgba, out_lin,
-                       counters, surf);
+                       surf, shade);
+    auto kern = args->variant == 4 ? rvcp::games101_tiled_kernel : rvcp::games101_path_kernel;
+    hipLaunchKernelGGL(kern, dim3(grid_blocks), dim3(rvcp::kBlock), 0, (hipStream_t)stream,
+                       *args, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
+                       shade);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -980,7 +1170,9 @@ extern "C" int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n, 
 extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
 {
     int b = 0;
-    const hipError_t e = variant == 3
+    const hipError_t e = variant == 4
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_kernel, rvcp::kBlock, 0)
+        : variant == 3
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel, rvcp::kBlock, 0)
         : variant == 2
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_dual_kernel, rvcp::kBlock, 0)
