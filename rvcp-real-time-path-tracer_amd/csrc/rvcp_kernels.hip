@@ -723,16 +723,21 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
 // never touch the RNG, :424-428), and appends every other pixel with its primary hit record to
 // a compact list for the path kernel (one atomic per wave).
 // ======================================================================================
-__global__ __launch_bounds__(kBlock) void games101_primary_kernel(
+constexpr uint32_t kPrimaryBlock = 1024;   // one list append (global atomic) per 1024 pixels
+
+__global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
     const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
     const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
     SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade)
 {
+    __shared__ uint32_t block_count, block_base;
     const uint32_t lane = lane_id();
-    const uint32_t pix = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t pix = blockIdx.x * kPrimaryBlock + threadIdx.x;
     const bool live = pix < A.n_pixels;
+    if (threadIdx.x == 0) block_count = 0;
+    __syncthreads();
     bool is_surf = false;
     f3 hpos = mk(0, 0, 0), hn = mk(0, 0, 0);
     uint32_t hmat = 0;
@@ -763,22 +768,24 @@ __global__ __launch_bounds__(kBlock) void games101_primary_kernel(
             is_surf = true;
         }
     }
+    // append the block's surface pixels to the list: LDS aggregation, one global atomic
     const uint64_t m = __ballot(is_surf);
-    if (m) {
-        const int leader = (int)__builtin_ctzll(m);
-        uint32_t base = 0;
-        if (lane == (uint32_t)leader)
-            base = atomicAdd((unsigned int *)&counters[3], (unsigned int)__builtin_popcountll(m));
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
-        if (is_surf) {
-            SurfRecord r;
-            r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.mat = hmat;
-            r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.pix = pix;
-            surf[base + rank_in(m)] = r;
-        }
+    uint32_t wave_off = 0;
+    if (lane == 0 && m) wave_off = atomicAdd(&block_count, (uint32_t)__builtin_popcountll(m));
+    wave_off = __shfl(wave_off, 0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        block_base = block_count ? atomicAdd((unsigned int *)&counters[3], block_count) : 0u;
+        const uint32_t lim = A.n_pixels - blockIdx.x * kPrimaryBlock;
+        atomicAdd(&counters[0], (unsigned long long)(lim < kPrimaryBlock ? lim : kPrimaryBlock));
     }
-    const uint64_t lv = __ballot(live);
-    if (lane == 0 && lv) atomicAdd(&counters[0], (unsigned long long)__builtin_popcountll(lv));
+    __syncthreads();
+    if (is_surf) {
+        SurfRecord r;
+        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.mat = hmat;
+        r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.pix = pix;
+        surf[block_base + wave_off + rank_in(m)] = r;
+    }
 }
 
 // ======================================================================================
@@ -1136,8 +1143,8 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                                        const rvcp::FaceShade *shade, uint32_t grid_blocks,
                                        void *stream)
 {
-    const uint32_t pre_blocks = (args->n_pixels + rvcp::kBlock - 1) / rvcp::kBlock;
-    hipLaunchKernelGGL(rvcp::games101_primary_kernel, dim3(pre_blocks), dim3(rvcp::kBlock), 0,
+    const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
+    hipLaunchKernelGGL(rvcp::games101_primary_kernel, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
                        (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
                        (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
                        surf, shade);
