@@ -71,8 +71,9 @@ typedef struct rvcp_face {
     uint32_t material_id;
 } rvcp_face_t;
 
-/* == AlignedSphere, src/ray_tracer/scene/sphere.rs:10-17 (32 B).  Accepted for ABI
- *    completeness; the dispatched games101 kernel never reads spheres. */
+/* == AlignedSphere, src/ray_tracer/scene/sphere.rs:10-17 (32 B).  Traced by integrator
+ *    RVCP_INTEGRATOR_LEGACY (ray_tracer.comp:300-321); the games101 shader never reads
+ *    spheres. */
 typedef struct rvcp_sphere {
     float center[3];
     float radius;
@@ -95,7 +96,15 @@ typedef struct rvcp_lengths {
  * same defaults (ray_tracer_games101_branch.comp:5-13).
  * ------------------------------------------------------------------------------------- */
 enum {
-    RVCP_INTEGRATOR_GAMES101 = 0,     /* ray_trace_games101, the dispatched shader */
+    /* ray_trace_games101 of ray_tracer_games101_branch.comp: the shader src/ray_tracer
+     * dispatches (shader.rs:12).  Triangles only; area-light NEE; gamma 0.6 on store. */
+    RVCP_INTEGRATOR_GAMES101 = 0,
+    /* ray_trace of ray_tracer.comp (compiled by src/ray_tracer_deprecated/shader.rs:12):
+     * spheres then triangles, Lambertian / metal / dielectric scattering, no NEE, no gamma
+     * (ray_tracer.comp:618-694, :802-822).  Its #define defaults (ray_tracer.comp:5-13) come
+     * from rvcp_config_default_for(RVCP_INTEGRATOR_LEGACY, ...); attenuation_stop_eps and
+     * lum_id_std140_quirk are unused (the black-path test uses eps, :672). */
+    RVCP_INTEGRATOR_LEGACY = 1,
 };
 
 typedef struct rvcp_config {
@@ -178,6 +187,11 @@ const char *rvcp_version(void);
  * them into the SPIR-V at `vulkano_shaders::shader!`, src/ray_tracer/shader.rs:9-14). */
 int rvcp_config_default(rvcp_config_t *cfg);
 
+/* Same, for integrator `integrator` (RVCP_INTEGRATOR_*): the #defines of the shader that
+ * integrator restates (ray_tracer_games101_branch.comp:5-13 or ray_tracer.comp:5-13).
+ * RVCP_E_UNSUPPORTED for an unknown integrator. */
+int rvcp_config_default_for(int32_t integrator, rvcp_config_t *cfg);
+
 /* Create a context on cfg->device.  Replaces pipeline creation:
  * `Vk::create_compute_pipeline(device, ray_tracer_shader::load(device))`,
  * src/ray_tracer/vulkan.rs:576-603 (called at :239-242). */
@@ -192,9 +206,11 @@ const char *rvcp_last_error(const rvcp_ctx_t *ctx);
 /* Upload a scene.  Replaces `Vk::create_descriptor_set_0s`, src/ray_tracer/vulkan.rs:454-574
  * (bindings 1 LengthBuffer, 2 MaterialBuffer, 4 VertexBuffer, 5 FaceBuffer,
  * 7 LuminousFaceIdBuffer).  `lum_face_ids` are the packed u32 ids the host computes at
- * vulkan.rs:473-478; the std140 quirk is applied inside.  Spheres / luminous sphere ids
- * (bindings 3 / 6 of ray_tracer.comp) may be NULL/0.  Face vertex indices and material
- * ids are validated (the reference does not bound-check; out-of-range ids are an error). */
+ * vulkan.rs:473-478; the std140 quirk is applied inside.  Spheres (binding 3) are traced by
+ * RVCP_INTEGRATOR_LEGACY and ignored by games101; luminous sphere ids (binding 6) are read
+ * by neither integrator's dispatched path and may be NULL/0.  Face vertex indices and
+ * material ids are validated (the reference does not bound-check; out-of-range ids are an
+ * error). */
 int rvcp_upload_scene(rvcp_ctx_t *ctx,
                       const rvcp_material_t *materials, uint32_t n_materials,
                       const rvcp_vertex_t *vertices, uint32_t n_vertices,
@@ -207,7 +223,8 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx,
  * `push_constants(...)` + `dispatch([W/8, H/8, 1])` + present of vulkan.rs:406-452 and
  * :298-404.  out_rgba8: W*H*4 bytes, row-major, logical RGBA (the reference's swapchain was
  * B8G8R8A8_UNORM, records/swapchain_image.txt:8), alpha 255.  out_linear_rgb (optional):
- * W*H*3 floats, the pre-clamp, pre-gamma `color` of ray_tracer_games101_branch.comp:497.
+ * W*H*3 floats, the pre-clamp, pre-gamma `color` of ray_tracer_games101_branch.comp:497
+ * (ray_tracer.comp:819 for RVCP_INTEGRATOR_LEGACY, whose RGBA8 store has no gamma).
  * Unlike the reference, W and H need not be multiples of 8 (every pixel is rendered). */
 int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
                 uint32_t width, uint32_t height,

@@ -45,8 +45,10 @@ def lib():
                                              ctypes.c_uint32, P]
         L.rvcp_oracle_sample_ray.restype = None
         u32 = ctypes.c_uint32
-        L.rvcp_oracle_render.argtypes = [P, u32, P, u32, P, u32, P, u32, P, P,
+        L.rvcp_oracle_render.argtypes = [P, u32, P, u32, P, u32, P, u32, P, u32, P, P,
                                          u32, u32, u32, u32, u32, u32, P, P, P, ctypes.c_int]
+        L.rvcp_oracle_unorm_u8.argtypes = [ctypes.c_float]
+        L.rvcp_oracle_unorm_u8.restype = ctypes.c_uint8
         L.rvcp_oracle_render.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -62,6 +64,10 @@ def sinf(x: float) -> float:
 
 def gamma_u8(c: float) -> int:
     return int(lib().rvcp_oracle_gamma_u8(ctypes.c_float(c)))
+
+
+def unorm_u8(c: float) -> int:
+    return int(lib().rvcp_oracle_unorm_u8(ctypes.c_float(c)))
 
 
 def rand_sequence(time: float, u: float, v: float, n: int) -> np.ndarray:
@@ -97,13 +103,16 @@ def render(scene_arrays: dict, push, cfg, W, H, rect=None, threads=None, want_li
     verts = np.ascontiguousarray(scene_arrays["vertices"])
     faces = np.ascontiguousarray(scene_arrays["faces"])
     lum = np.ascontiguousarray(scene_arrays["lum_face_ids"], dtype=np.uint32)
+    sph = scene_arrays.get("spheres")
+    sph = np.ascontiguousarray(sph) if sph is not None and len(sph) else None
     push = np.ascontiguousarray(push)
     cfg = np.ascontiguousarray(cfg)
     lin = np.zeros((th, tw, 3), dtype=np.float32) if want_linear else None
     rgba = np.zeros((th, tw, 4), dtype=np.uint8)
     trav = np.zeros(1, dtype=np.uint64)
     rc = lib().rvcp_oracle_render(_ptr(mats), len(mats), _ptr(verts), len(verts), _ptr(faces),
-                                  len(faces), _ptr(lum), len(lum), _ptr(push), _ptr(cfg),
+                                  len(faces), _ptr(sph), 0 if sph is None else len(sph),
+                                  _ptr(lum), len(lum), _ptr(push), _ptr(cfg),
                                   W, H, x0, y0, tw, th, _ptr(lin), _ptr(rgba), _ptr(trav),
                                   int(threads))
     if rc != 0:

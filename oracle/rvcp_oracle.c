@@ -45,6 +45,7 @@ typedef struct {
     uint32_t spp, max_bounces;
     float att_stop, t_min, t_max, rr, eps;
     int quirk;
+    int integrator;          /* 0 = games101 (dispatched), 1 = ray_tracer.comp ray_trace */
 } params_t;
 
 /* ------------------------------------------------------------------------------------- */
@@ -139,6 +140,7 @@ typedef struct {
     const rvcp_vertex_t *vtx; uint32_t n_vtx;
     const rvcp_face_t *face; uint32_t n_face;
     const uint32_t *lum; uint32_t n_lum;   /* packed u32 ids as uploaded */
+    const rvcp_sphere_t *sph; uint32_t n_sph;   /* integrator mode 2 only */
 } scene_t;
 
 typedef struct { v3 o, d; float t_min, t_max; } ray_t;        /* :116-121 */
@@ -313,6 +315,173 @@ static v3 ray_trace_games101(const scene_t *sc, const params_t *P, rng_t *g, ray
 }
 
 /* ------------------------------------------------------------------------------------- */
+/* Integrator mode 2: ray_tracer.comp (the file north_star names; compiled only by the     */
+/* deprecated host, src/ray_tracer_deprecated/shader.rs:12).  RNG, sample_ray and          */
+/* is_intersect_with_face are identical to the games101 shader (ray_tracer.comp:151-258,   */
+/* :324-366).                                                                              */
+/* ------------------------------------------------------------------------------------- */
+
+/* is_intersect_with_quadratic_equation, ray_tracer.comp:260-297 */
+static int quad_hit(float a, float b, float c, const ray_t *ray, hit_t *out)
+{
+    float delta = b * b - 4.0f * a * c;
+    if (delta < 0.0f) return 0;                       /* sign(delta) < 0.0 */
+    float sq = sqrtf(delta);
+    float t0 = (-b + sq) / (2.0f * a);
+    float t1 = (-b - sq) / (2.0f * a);
+    if (t0 > t1) { float tmp = t0; t0 = t1; t1 = tmp; }
+    float t;
+    if (ray->t_min <= t0 && t0 <= ray->t_max) t = t0;
+    else if (ray->t_min <= t1 && t1 <= ray->t_max) t = t1;
+    else return 0;
+    out->time = t;
+    out->pos = add(ray->o, muls(ray->d, t));
+    out->normal = mk(0, 0, 0);
+    out->material_id = 0;
+    out->outward = 1;
+    return 1;
+}
+
+/* is_intersect_with_sphere, ray_tracer.comp:300-321 */
+static int sphere_hit(const ray_t *ray, const rvcp_sphere_t *sp, hit_t *out)
+{
+    v3 ce = ld3(sp->center);
+    v3 co = sub(ray->o, ce);
+    float a = dot(ray->d, ray->d);
+    float b = 2.0f * dot(ray->d, co);
+    float c = dot(co, co) - sp->radius * sp->radius;
+    if (!quad_hit(a, b, c, ray, out)) return 0;
+    out->normal = normalize(sub(out->pos, ce));
+    out->material_id = sp->material_id;
+    v3 oc = sub(ray->o, ce);
+    if (dot(oc, oc) < sp->radius * sp->radius) { out->normal = neg(out->normal); out->outward = 0; }
+    return 1;
+}
+
+/* get_intersection_with_scene, ray_tracer.comp:369-393: spheres first, then faces */
+static hit_t scene_hit_legacy(const scene_t *sc, ray_t ray, uint64_t *trav)
+{
+    hit_t inter;
+    inter.time = ray.t_max + 1.0f;
+    inter.pos = mk(INFINITY, INFINITY, INFINITY);
+    inter.normal = mk(0, 0, 0);
+    inter.material_id = 0;
+    inter.outward = 1;
+    for (uint32_t i = 0; i < sc->n_sph; i++) {
+        hit_t h;
+        if (sphere_hit(&ray, &sc->sph[i], &h) && h.time <= ray.t_max) { ray.t_max = h.time; inter = h; }
+    }
+    for (uint32_t i = 0; i < sc->n_face; i++) {
+        hit_t h;
+        if (is_intersect_with_face(sc, &ray, &sc->face[i], &h) && h.time <= ray.t_max) {
+            ray.t_max = h.time;
+            inter = h;
+        }
+    }
+    (*trav)++;
+    return inter;
+}
+
+/* GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N */
+static inline v3 reflect_glsl(v3 I, v3 N) { return sub(I, muls(N, 2.0f * dot(N, I))); }
+/* GLSL refract(I, N, eta) */
+static inline v3 refract_glsl(v3 I, v3 N, float eta)
+{
+    float d = dot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return mk(0, 0, 0);
+    return sub(muls(I, eta), muls(N, eta * d + sqrtf(k)));
+}
+/* fresnel_schlick, ray_tracer.comp:544-551; pow(x, 5.0) := ((x*x)*(x*x))*x */
+static inline float fresnel_schlick(float cosine, float ratio)
+{
+    float r0 = (1.0f - ratio) / (1.0f + ratio);
+    r0 = r0 * r0;
+    float x = 1.0f - cosine;
+    return r0 + (1.0f - r0) * (x * x * (x * x) * x);
+}
+
+/* material_scatter, ray_tracer.comp:491-602.  Unknown types leave attenuation 0 (:655). */
+static void material_scatter(const rvcp_material_t *m, const ray_t *ray, const hit_t *h,
+                             rng_t *g, const params_t *P, v3 *att, ray_t *nr)
+{
+    nr->o = h->pos; nr->t_min = P->t_min; nr->t_max = P->t_max; nr->d = mk(0, 0, 0);
+    *att = mk(0, 0, 0);
+    if (m->ty == 0) {                                   /* lambertian_scatter :491-513 */
+        v3 u = normalize(random_in_unit_sphere(g));
+        v3 dir = normalize(add(h->normal, u));
+        if (fabsf(dir.x) < P->eps && fabsf(dir.y) < P->eps && fabsf(dir.z) < P->eps) dir = h->normal;
+        *att = ld3(m->albedo);
+        nr->d = dir;
+    } else if (m->ty == 1) {                            /* metal_scatter :517-540 */
+        v3 refl = reflect_glsl(ray->d, h->normal);
+        if (dot(refl, h->normal) < 0.0f) refl = neg(refl);
+        v3 dir;
+        do {
+            v3 u = normalize(random_in_unit_sphere(g));
+            dir = normalize(add(refl, muls(u, m->fuzz)));
+        } while (dot(dir, h->normal) < 0.0f);
+        *att = ld3(m->albedo);
+        nr->d = dir;
+    } else if (m->ty == 2) {                            /* dielectric_scatter :553-581 */
+        float ratio = h->outward ? (1.0f / m->refraction_ratio) : m->refraction_ratio;
+        float cos_t = dot(neg(ray->d), h->normal);
+        float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        int refracted = ratio * sin_t <= 1.0f;
+        if (refracted && (rand_next(g) >= fresnel_schlick(cos_t, ratio)))
+            nr->d = refract_glsl(ray->d, h->normal, ratio);
+        else
+            nr->d = reflect_glsl(ray->d, h->normal);
+        *att = mk(1, 1, 1);
+    }
+}
+
+/* ray_trace, ray_tracer.comp:618-694 (path_reuse_count is 0 or 1: its division is exact) */
+static v3 ray_trace_legacy(const scene_t *sc, const params_t *P, rng_t *g, ray_t ray, uint64_t *trav)
+{
+    v3 color = mk(0, 0, 0);
+    v3 attenuation = mk(1, 1, 1);
+    for (uint32_t left = P->max_bounces; left > 0;) {
+        left -= 1;
+        hit_t inter = scene_hit_legacy(sc, ray, trav);
+        if (inter.time > ray.t_max) {                   /* miss: sample_infinite_light = 0 */
+            color = add(color, mulv(attenuation, mk(0, 0, 0)));
+            break;
+        }
+        const rvcp_material_t *m = &sc->mat[inter.material_id];
+        if (m->ty == MATERIAL_LIGHT) { color = add(color, mulv(attenuation, ld3(m->albedo))); break; }
+        v3 new_att;
+        ray_t new_ray;
+        material_scatter(m, &ray, &inter, g, P, &new_att, &new_ray);
+        attenuation = mulv(attenuation, new_att);
+        ray = new_ray;
+        ray.o = add(ray.o, muls(ray.d, P->t_min));     /* :670 RAY_T_MIN */
+        if (attenuation.x < P->eps && attenuation.y < P->eps && attenuation.z < P->eps) break;
+        if (rand_next(g) >= P->rr) break;
+        attenuation = divs(attenuation, P->rr);
+    }
+    return color;
+}
+
+/* UNORM8 store without gamma (ray_tracer.comp:820-822): u8 = #{k : c >= U[k]},
+ * U[k] = float((k - 0.5) / 255). */
+static float g_unorm_T[256];
+static pthread_once_t g_unorm_once = PTHREAD_ONCE_INIT;
+static void unorm_init(void)
+{
+    g_unorm_T[0] = 0.0f;
+    for (int k = 1; k < 256; k++) g_unorm_T[k] = (float)((k - 0.5) / 255.0);
+}
+uint8_t rvcp_oracle_unorm_u8(float c)
+{
+    pthread_once(&g_unorm_once, unorm_init);
+    float x = (c > 0.0f) ? ((c < 1.0f) ? c : 1.0f) : 0.0f;
+    int n = 0;
+    for (int k = 1; k < 256; k++) n += (x >= g_unorm_T[k]);
+    return (uint8_t)n;
+}
+
+/* ------------------------------------------------------------------------------------- */
 /* Camera: sample_ray, :217-235                                                            */
 /* ------------------------------------------------------------------------------------- */
 typedef struct { v3 pos, fwd, up; float t_near, t_far, vfov; } cam_t;
@@ -386,17 +555,24 @@ static void render_pixel(job_t *J, uint32_t x, uint32_t y, uint32_t out_idx)
     ray_t ray = sample_ray(&J->cam, u_, v_, Wf, Hf);                    /* :491 */
     v3 color = mk(0, 0, 0);
     const float sppf = (float)J->P->spp;
-    for (uint32_t i = 0; i < J->P->spp; i++)                           /* :494-496 */
-        color = add(color, divs(ray_trace_games101(J->sc, J->P, &g, ray, &J->trav), sppf));
+    if (J->P->integrator == 1) {                                       /* ray_tracer.comp:815-819 */
+        for (uint32_t i = 0; i < J->P->spp; i++)
+            color = add(color, ray_trace_legacy(J->sc, J->P, &g, ray, &J->trav));
+        color = divs(color, sppf);
+    } else {
+        for (uint32_t i = 0; i < J->P->spp; i++)                       /* :494-496 */
+            color = add(color, divs(ray_trace_games101(J->sc, J->P, &g, ray, &J->trav), sppf));
+    }
     if (J->lin) {
         J->lin[3 * (size_t)out_idx + 0] = color.x;
         J->lin[3 * (size_t)out_idx + 1] = color.y;
         J->lin[3 * (size_t)out_idx + 2] = color.z;
     }
     if (J->rgba) {
-        J->rgba[4 * (size_t)out_idx + 0] = rvcp_oracle_gamma_u8(color.x);
-        J->rgba[4 * (size_t)out_idx + 1] = rvcp_oracle_gamma_u8(color.y);
-        J->rgba[4 * (size_t)out_idx + 2] = rvcp_oracle_gamma_u8(color.z);
+        uint8_t (*q)(float) = J->P->integrator == 1 ? rvcp_oracle_unorm_u8 : rvcp_oracle_gamma_u8;
+        J->rgba[4 * (size_t)out_idx + 0] = q(color.x);
+        J->rgba[4 * (size_t)out_idx + 1] = q(color.y);
+        J->rgba[4 * (size_t)out_idx + 2] = q(color.z);
         J->rgba[4 * (size_t)out_idx + 3] = 255;
     }
 }
@@ -419,6 +595,7 @@ static void *render_rows(void *arg)
 int rvcp_oracle_render(const rvcp_material_t *materials, uint32_t n_materials,
                        const rvcp_vertex_t *vertices, uint32_t n_vertices,
                        const rvcp_face_t *faces, uint32_t n_faces,
+                       const rvcp_sphere_t *spheres, uint32_t n_spheres,
                        const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
                        const rvcp_push_constant_t *push, const rvcp_config_t *cfg,
                        uint32_t W, uint32_t H, uint32_t x0, uint32_t y0, uint32_t tw,
@@ -433,12 +610,17 @@ int rvcp_oracle_render(const rvcp_material_t *materials, uint32_t n_materials,
     }
     for (uint32_t i = 0; i < n_lum_face_ids; i++)
         if (lum_face_ids[i] >= n_faces) return RVCP_E_INVALID;
+    for (uint32_t i = 0; i < n_spheres; i++)
+        if (spheres[i].material_id >= n_materials) return RVCP_E_INVALID;
+    if (cfg->integrator != 0 && cfg->integrator != 1) return RVCP_E_UNSUPPORTED;
     pthread_once(&g_gamma_once, gamma_init);
+    pthread_once(&g_unorm_once, unorm_init);
 
     scene_t sc = { materials, n_materials, vertices, n_vertices, faces, n_faces,
-                   lum_face_ids, n_lum_face_ids };
+                   lum_face_ids, n_lum_face_ids, spheres, cfg->integrator == 1 ? n_spheres : 0 };
     params_t P = { cfg->spp, cfg->max_bounces, cfg->attenuation_stop_eps, cfg->ray_t_min,
-                   cfg->ray_t_max, cfg->rr_probability, cfg->eps, cfg->lum_id_std140_quirk };
+                   cfg->ray_t_max, cfg->rr_probability, cfg->eps, cfg->lum_id_std140_quirk,
+                   cfg->integrator };
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     job_t *jobs = (job_t *)calloc((size_t)nthreads, sizeof(job_t));
@@ -492,7 +674,7 @@ int rvcp_oracle_intersect(const float *ray, const float *tri, float *out)
         v[k].position[2] = tri[3 * k + 2]; v[k].normal[1] = 1.0f;
     }
     rvcp_face_t f = { {0, 1, 2}, 0 };
-    scene_t sc = { NULL, 0, v, 3, &f, 1, NULL, 0 };
+    scene_t sc = { NULL, 0, v, 3, &f, 1, NULL, 0, NULL, 0 };
     ray_t r = { mk(ray[0], ray[1], ray[2]), mk(ray[3], ray[4], ray[5]), ray[6], ray[7] };
     hit_t h;
     if (!is_intersect_with_face(&sc, &r, &f, &h)) return 0;

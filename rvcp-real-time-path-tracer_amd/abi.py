@@ -34,14 +34,22 @@ DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop
 RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E_NOMEM = \
     0, -1, -2, -3, -4, -5
 
-EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_create", "rvcp_destroy",
+EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "rvcp_create", "rvcp_destroy",
             "rvcp_last_error", "rvcp_upload_scene", "rvcp_render", "rvcp_render_shard_async",
             "rvcp_sync_stats", "rvcp_shard_rows", "rvcp_assemble_frame_async"]
 
 
+# Integrator mode 2 (ray_tracer.comp ray_trace): its own #defines (ray_tracer.comp:5-13).
+LEGACY_DEFAULTS = dict(device=0, integrator=1, spp=5, max_bounces=3, attenuation_stop_eps=0.01,
+                       ray_t_min=0.01, ray_t_max=1000.0, rr_probability=1.0, eps=0.001,
+                       lum_id_std140_quirk=1, kernel_variant=0)
+INTEGRATOR_GAMES101, INTEGRATOR_LEGACY = 0, 1
+
+
 def make_config(**kw) -> np.ndarray:
+    """rvcp_config_t with the #define defaults of the selected integrator, overridden by kw."""
     cfg = np.zeros((), dtype=CONFIG_DTYPE)
-    vals = dict(DEFAULTS)
+    vals = dict(LEGACY_DEFAULTS if kw.get("integrator", 0) == INTEGRATOR_LEGACY else DEFAULTS)
     vals.update(kw)
     for k, v in vals.items():
         cfg[k] = v
@@ -88,6 +96,7 @@ def load():
     P, u32 = ctypes.c_void_p, ctypes.c_uint32
     L.rvcp_version.restype = ctypes.c_char_p
     L.rvcp_config_default.argtypes = [P]
+    L.rvcp_config_default_for.argtypes = [ctypes.c_int32, P]
     L.rvcp_create.argtypes = [P, ctypes.POINTER(ctypes.c_void_p)]
     L.rvcp_destroy.argtypes = [P]
     L.rvcp_last_error.argtypes = [P]
@@ -99,7 +108,7 @@ def load():
     L.rvcp_shard_rows.argtypes = [u32, u32, u32]
     L.rvcp_shard_rows.restype = u32
     L.rvcp_assemble_frame_async.argtypes = [P, P, u32, u32, u32, u32, P, P]
-    for name in ("rvcp_config_default", "rvcp_create", "rvcp_destroy", "rvcp_upload_scene",
+    for name in ("rvcp_config_default", "rvcp_config_default_for", "rvcp_create", "rvcp_destroy", "rvcp_upload_scene",
                  "rvcp_render", "rvcp_render_shard_async", "rvcp_sync_stats",
                  "rvcp_assemble_frame_async"):
         getattr(L, name).restype = ctypes.c_int

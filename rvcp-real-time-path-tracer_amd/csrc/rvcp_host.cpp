@@ -28,6 +28,7 @@ struct rvcp_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int grid_capacity[kMaxVariant + 1] = {};   // resident workgroups per kernel variant
+    int legacy_capacity = 0;                   // ... of the RVCP_INTEGRATOR_LEGACY kernel
 
     // scene (device)
     TriRecord *d_tri = nullptr;
@@ -36,9 +37,12 @@ struct rvcp_ctx {
     MatRecord *d_mats = nullptr;
     FaceShade *d_shade = nullptr;
     LightRecord *d_lights = nullptr;
+    rvcp_material_t *d_rawmats = nullptr;     // RVCP_INTEGRATOR_LEGACY: fuzz / ior needed
+    rvcp_sphere_t *d_spheres = nullptr;
     float *d_gamma = nullptr;
+    float *d_unorm = nullptr;
     unsigned long long *d_counters = nullptr;
-    uint32_t n_faces = 0, n_lights = 0, n_mats = 0, n_verts = 0;
+    uint32_t n_faces = 0, n_lights = 0, n_mats = 0, n_verts = 0, n_spheres = 0;
     float light_total = 0.0f, light_pdf = 0.0f;
     bool has_scene = false;
 
@@ -138,6 +142,8 @@ void free_scene(rvcp_ctx *ctx)
     (void)hipFree(ctx->d_mats); ctx->d_mats = nullptr;
     (void)hipFree(ctx->d_shade); ctx->d_shade = nullptr;
     (void)hipFree(ctx->d_lights); ctx->d_lights = nullptr;
+    (void)hipFree(ctx->d_rawmats); ctx->d_rawmats = nullptr;
+    (void)hipFree(ctx->d_spheres); ctx->d_spheres = nullptr;
     ctx->has_scene = false;
 }
 
@@ -146,6 +152,24 @@ void free_scene(rvcp_ctx *ctx)
 extern "C" {
 
 const char *rvcp_version(void) { return "rvcp-mi355x 0.1.0 (gfx950)"; }
+
+int rvcp_config_default_for(int32_t integrator, rvcp_config_t *cfg)
+{
+    if (!cfg) return RVCP_E_INVALID;
+    if (integrator == RVCP_INTEGRATOR_GAMES101) return rvcp_config_default(cfg);
+    if (integrator != RVCP_INTEGRATOR_LEGACY) return RVCP_E_UNSUPPORTED;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->integrator = RVCP_INTEGRATOR_LEGACY;
+    cfg->spp = 5;                       // ray_tracer.comp:8
+    cfg->max_bounces = 3;               // :9
+    cfg->attenuation_stop_eps = 0.01f;  // :10 (unused by ray_trace)
+    cfg->ray_t_min = 0.01f;             // :11
+    cfg->ray_t_max = 1000.0f;           // :12
+    cfg->rr_probability = 1.0f;         // :13
+    cfg->eps = 0.001f;                  // :5
+    cfg->lum_id_std140_quirk = 1;       // (unused by ray_trace)
+    return RVCP_OK;
+}
 
 int rvcp_config_default(rvcp_config_t *cfg)
 {
@@ -173,7 +197,7 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
 {
     if (!cfg || !out_ctx) return fail(nullptr, RVCP_E_INVALID, "null argument");
     *out_ctx = nullptr;
-    if (cfg->integrator != RVCP_INTEGRATOR_GAMES101)
+    if (cfg->integrator != RVCP_INTEGRATOR_GAMES101 && cfg->integrator != RVCP_INTEGRATOR_LEGACY)
         return fail(nullptr, RVCP_E_UNSUPPORTED, "unsupported integrator");
     if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
     if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant)
@@ -207,6 +231,9 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     for (int k = 1; k < 256; k++) T[k] = (float)std::pow((k - 0.5) / 255.0, 1.0 / 0.6);
     T[256] = INFINITY;
     if ((rc = dev_upload<float>(ctx, &ctx->d_gamma, T, 257)) != RVCP_OK) return bail(rc);
+    // UNORM8 thresholds U[k] = float((k - 0.5) / 255) for ray_tracer.comp's gamma-free store
+    for (int k = 1; k < 256; k++) T[k] = (float)((k - 0.5) / 255.0);
+    if ((rc = dev_upload<float>(ctx, &ctx->d_unorm, T, 257)) != RVCP_OK) return bail(rc);
     if (hipMalloc((void **)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "hipMalloc counters"));
 
@@ -222,6 +249,12 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         if (cap > 0 && cap < per_cu) per_cu = cap;
         ctx->grid_capacity[v] = per_cu * cus;
     }
+    {
+        int per_cu = 0;
+        if (rvcp_legacy_occupancy(&per_cu) != 0 || per_cu <= 0) per_cu = 1;
+        if (cap > 0 && cap < per_cu) per_cu = cap;
+        ctx->legacy_capacity = per_cu * cus;
+    }
     *out_ctx = ctx;
     return RVCP_OK;
 }
@@ -233,6 +266,7 @@ int rvcp_destroy(rvcp_ctx_t *ctx)
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_scene(ctx);
     (void)hipFree(ctx->d_gamma);
+    (void)hipFree(ctx->d_unorm);
     (void)hipFree(ctx->d_counters);
     (void)hipFree(ctx->d_rgba);
     (void)hipFree(ctx->d_lin);
@@ -251,11 +285,15 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
                       const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
                       const uint32_t *lum_sphere_ids, uint32_t n_lum_sphere_ids)
 {
-    (void)spheres; (void)n_spheres; (void)lum_sphere_ids; (void)n_lum_sphere_ids;
+    (void)lum_sphere_ids; (void)n_lum_sphere_ids;
     if (!ctx) return RVCP_E_INVALID;
     if (!materials || n_materials == 0) return fail(ctx, RVCP_E_INVALID, "need >= 1 material");
-    if ((n_vertices && !vertices) || (n_faces && !faces) || (n_lum_face_ids && !lum_face_ids))
+    if ((n_vertices && !vertices) || (n_faces && !faces) || (n_lum_face_ids && !lum_face_ids) ||
+        (n_spheres && !spheres))
         return fail(ctx, RVCP_E_INVALID, "null array with nonzero length");
+    for (uint32_t i = 0; i < n_spheres; i++)
+        if (spheres[i].material_id >= n_materials)
+            return fail(ctx, RVCP_E_INVALID, "sphere " + std::to_string(i) + " material out of range");
     for (uint32_t i = 0; i < n_faces; i++) {
         for (int k = 0; k < 3; k++)
             if (faces[i].vertices[k] >= n_vertices)
@@ -330,8 +368,11 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         (rc = dev_upload<rvcp_vertex_t>(ctx, &ctx->d_verts, vertices, n_vertices)) ||
         (rc = dev_upload<MatRecord>(ctx, &ctx->d_mats, mats.data(), n_materials)) ||
         (rc = dev_upload<FaceShade>(ctx, &ctx->d_shade, shade.data(), n_faces)) ||
-        (rc = dev_upload<LightRecord>(ctx, &ctx->d_lights, lights.data(), n_lum_face_ids)))
+        (rc = dev_upload<LightRecord>(ctx, &ctx->d_lights, lights.data(), n_lum_face_ids)) ||
+        (rc = dev_upload<rvcp_material_t>(ctx, &ctx->d_rawmats, materials, n_materials)) ||
+        (rc = dev_upload<rvcp_sphere_t>(ctx, &ctx->d_spheres, spheres, n_spheres)))
         return rc;
+    ctx->n_spheres = n_spheres;
     ctx->n_faces = n_faces;
     ctx->n_verts = n_vertices;
     ctx->n_mats = n_materials;
@@ -389,10 +430,13 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     A.want_linear = d_linear_rgb ? 1u : 0u;
     A.variant = ctx->cfg.kernel_variant != 0 ? ctx->cfg.kernel_variant
               : (ctx->n_faces >= kTiledMinFaces ? 4 : kDefaultVariant);
+    const bool legacy = ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY;
+    A.n_spheres = legacy ? ctx->n_spheres : 0u;
 
     // With MAX_BOUNCES == 0 or ATTENUATION_STOP_EPS > 1 every sample returns 0 before its
-    // first traversal (:413-419): the frame is black.
-    const bool trivial = A.max_bounces == 0 || 1.0f < A.att_stop;
+    // first traversal (:413-419): the frame is black.  ray_tracer.comp has no attenuation
+    // test before its first traversal (:629-634).
+    const bool trivial = A.max_bounces == 0 || (!legacy && 1.0f < A.att_stop);
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(unsigned long long), s));
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     if (A.n_pixels > 0) {
@@ -403,11 +447,16 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
         } else {
             const uint32_t waves_needed = (A.n_pixels + kChunk - 1) / kChunk;
             uint32_t blocks = (waves_needed + (kBlock / kWave) - 1) / (kBlock / kWave);
-            if (blocks > (uint32_t)ctx->grid_capacity[A.variant])
-                blocks = (uint32_t)ctx->grid_capacity[A.variant];
+            const uint32_t cap = (uint32_t)(legacy ? ctx->legacy_capacity
+                                                   : ctx->grid_capacity[A.variant]);
+            if (blocks > cap) blocks = cap;
             if (blocks == 0) blocks = 1;
             A.static_chunks = blocks * (kBlock / kWave) * kChunk;
-            if (A.variant >= 3) {
+            if (legacy) {
+                rc = rvcp_launch_legacy(&A, ctx->d_tri, ctx->d_shade, ctx->d_spheres,
+                                        ctx->d_rawmats, ctx->d_unorm, (uint32_t *)d_rgba8,
+                                        (float *)d_linear_rgb, ctx->d_counters, blocks, s);
+            } else if (A.variant >= 3) {
                 if (ctx->cap_surf < A.n_pixels) {
                     (void)hipFree(ctx->d_surf);
                     ctx->d_surf = nullptr;

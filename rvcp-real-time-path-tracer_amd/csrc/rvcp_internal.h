@@ -103,6 +103,7 @@ struct FrameArgs {
     uint32_t static_chunks;  // pixels handed out statically (one chunk per wave)
     uint32_t want_linear;
     int32_t variant;         // kernel schedule (rvcp_config_t::kernel_variant, resolved)
+    uint32_t n_spheres;      // integrator RVCP_INTEGRATOR_LEGACY only
 };
 
 }  // namespace rvcp
@@ -120,6 +121,13 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *
                             uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
                             rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
                             uint32_t grid_blocks, void *stream);
+// Integrator RVCP_INTEGRATOR_LEGACY (ray_tracer.comp): materials / spheres are the raw
+// rvcp_material_t / rvcp_sphere_t arrays, unorm_t the UNORM8 threshold table.
+int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
+                       const rvcp::FaceShade *shade, const void *spheres, const void *materials,
+                       const float *unorm_t, uint32_t *out_rgba, float *out_lin,
+                       unsigned long long *counters, uint32_t grid_blocks, void *stream);
+int rvcp_legacy_occupancy(int *blocks_per_cu);
 int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows, uint32_t width,
                          uint32_t height, uint32_t shard_count, uint32_t *frame, void *stream);
 int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n_pixels, uint32_t rgba,

@@ -1118,6 +1118,267 @@ __global__ void fill_kernel(uint32_t *__restrict__ out_rgba, float *__restrict__
     }
 }
 
+// ======================================================================================
+// Integrator RVCP_INTEGRATOR_LEGACY: ray_trace of assets/shaders/ray_tracer.comp
+// (:618-694, main :802-822) -- spheres then triangles, Lambertian / metal / dielectric
+// scattering, no light sampling, UNORM store without gamma.  Same machine as variant 1: one
+// ray per lane per iteration, the RNG-independent primary hit traced once per pixel and reused
+// by every sample, the per-lane rejection loops of random_in_unit_sphere run cooperatively.
+// ======================================================================================
+namespace {
+
+// GLSL reflect(I, N) = I - 2 dot(N, I) N
+__device__ __forceinline__ f3 reflect_glsl(f3 I, f3 N) { return sub(I, muls(N, 2.0f * dot(N, I))); }
+
+// GLSL refract(I, N, eta)
+__device__ __forceinline__ f3 refract_glsl(f3 I, f3 N, float eta) {
+    const float d = dot(N, I);
+    const float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return mk(0, 0, 0);
+    return sub(muls(I, eta), muls(N, eta * d + __builtin_sqrtf(k)));
+}
+
+// fresnel_schlick, :544-551; pow(x, 5.0) := ((x*x)*(x*x))*x
+__device__ __forceinline__ float fresnel_schlick(float cosine, float ratio) {
+    float r0 = (1.0f - ratio) / (1.0f + ratio);
+    r0 = r0 * r0;
+    const float x = 1.0f - cosine;
+    return r0 + (1.0f - r0) * (x * x * (x * x) * x);
+}
+
+// is_intersect_with_sphere + is_intersect_with_quadratic_equation (:260-321) under the
+// nearest-hit rule of get_intersection_with_scene (:376-381): true iff the shader would take
+// this sphere as the new nearest hit, whose time is written to t_out.  a = dot(d, d) and
+// two_a = 2 a are per-ray constants (the shader recomputes the same values per sphere).
+__device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d, float a,
+                                              float two_a, float tmin, float bt, float &t_out) {
+    const f3 co = mk(o.x - S.center[0], o.y - S.center[1], o.z - S.center[2]);
+    const float b = 2.0f * dot(d, co);
+    const float c = dot(co, co) - S.radius * S.radius;
+    const float delta = b * b - 4.0f * a * c;
+    const float sq = __builtin_sqrtf(delta);
+    float t0 = (-b + sq) / two_a;
+    float t1 = (-b - sq) / two_a;
+    if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
+    const bool h0 = (tmin <= t0) & (t0 <= bt);
+    const bool h1 = (tmin <= t1) & (t1 <= bt);
+    t_out = h0 ? t0 : t1;
+    return !(delta < 0.0f) & (h0 | h1);
+}
+
+constexpr int L_IDLE = 0, L_TRACE = 1, L_SCATTER = 2, L_END = 3;
+
+}  // namespace
+
+__global__ __launch_bounds__(kBlock) void legacy_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
+    const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
+    const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
+{
+    __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
+    uint8_t *tab = coop_tab[threadIdx.x / kWave];
+    const uint32_t lane = lane_id();
+    Queue q = queue_init(A);
+    const float sppf = (float)A.spp;
+
+    int st = L_IDLE;
+    bool need_pixel = true, done = false, primary = false;
+    uint32_t pix = 0, k = 0, left = 0, trav = 0, iters = 0;
+    float seed = 0.0f, ridx = 0.0f;
+    f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
+    f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0), P_dir = mk(0, 0, 1);   // cached primary hit
+    uint32_t P_mat = 0;
+    bool P_out = true;
+    f3 H_pos = mk(0, 0, 0), H_nrm = mk(0, 0, 0), H_dir = mk(0, 0, 1);   // hit being scattered
+    uint32_t H_mat = 0;
+    bool H_out = true;
+    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1);
+    float rtmin = 0.0f, rtmax = 0.0f;
+
+    for (;;) {
+        // ============ settle: advance every lane until it has a ray or is done ============
+        for (;;) {
+            if (st == L_END) {                                      // color += ray_trace (:817)
+                acc = add(acc, col);
+                k += 1;
+                if (k >= A.spp) {
+                    store_pixel(pix, divs(acc, sppf), A, unorm_t, out_rgba, out_lin);   // :819-821
+                    need_pixel = true;
+                    st = L_IDLE;
+                } else {                                            // next sample, cached hit
+                    att = mk(1, 1, 1);
+                    col = mk(0, 0, 0);
+                    left = A.max_bounces - 1u;
+                    H_pos = P_pos; H_nrm = P_nrm; H_dir = P_dir; H_mat = P_mat; H_out = P_out;
+                    st = L_SCATTER;
+                }
+            }
+            {   // take new pixels from the frame queue (wave-uniform control flow)
+                bool got;
+                uint32_t np = pix;
+                queue_take(q, __ballot(need_pixel && !done), lane, A, counters, got, np);
+                if (got) {
+                    pix = np;
+                    start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
+                    primary = true;
+                    need_pixel = false;
+                    k = 0;
+                    acc = mk(0, 0, 0);
+                    att = mk(1, 1, 1);
+                    col = mk(0, 0, 0);
+                    st = L_TRACE;
+                } else if (need_pixel && q.exhausted) {
+                    done = true;
+                }
+            }
+            if (__any(st == L_SCATTER)) {
+                // material_scatter (:585-602), then the tail of the bounce loop (:668-686)
+                const bool sc = st == L_SCATTER;
+                uint32_t ty = 0xFFFFFFFFu;
+                f3 alb = mk(0, 0, 0);
+                float fuzz = 0.0f, ior = 1.0f;
+                if (sc) {
+                    const rvcp_material_t &M = mats[H_mat];
+                    ty = M.ty;
+                    alb = ld3(M.albedo);
+                    fuzz = M.fuzz;
+                    ior = M.refraction_ratio;
+                }
+                f3 dir = mk(0, 0, 0);
+                f3 refl = reflect_glsl(H_dir, H_nrm);                       // metal :526-527
+                if (dot(refl, H_nrm) < 0.0f) refl = neg(refl);
+                bool pend = sc && (ty == 0u || ty == 1u);
+                while (__any(pend)) {
+                    f3 p = mk(0, 0, 0);
+                    coop_unit_sphere(pend, seed, ridx, p, lane, tab);
+                    if (pend) {
+                        const f3 u = normalize(p);          // random_in_unit_sphere_surface :225
+                        if (ty == 0u) {                     // lambertian_scatter :491-513
+                            dir = normalize(add(H_nrm, u));
+                            if (__builtin_fabsf(dir.x) < A.eps && __builtin_fabsf(dir.y) < A.eps &&
+                                __builtin_fabsf(dir.z) < A.eps)
+                                dir = H_nrm;
+                            pend = false;
+                        } else {                            // metal_scatter :528-530
+                            dir = normalize(add(refl, muls(u, fuzz)));
+                            pend = dot(dir, H_nrm) < 0.0f;
+                        }
+                    }
+                }
+                if (sc && ty == 2u) {                                       // :553-581
+                    const float ratio = H_out ? (1.0f / ior) : ior;
+                    const float cos_t = dot(neg(H_dir), H_nrm);
+                    const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+                    bool refracted = ratio * sin_t <= 1.0f;
+                    if (refracted) refracted = rnd(seed, ridx) >= fresnel_schlick(cos_t, ratio);
+                    dir = refracted ? refract_glsl(H_dir, H_nrm, ratio) : reflect_glsl(H_dir, H_nrm);
+                }
+                if (sc) {
+                    const f3 natt = (ty == 0u || ty == 1u) ? alb
+                                  : (ty == 2u ? mk(1, 1, 1) : mk(0, 0, 0));    // unknown: 0 (:655)
+                    att = mulv(att, natt);                                  // :667
+                    rd = dir;
+                    ro = add(H_pos, muls(dir, A.t_min));                    // :668-670
+                    rtmin = A.t_min;
+                    rtmax = A.t_max;
+                    if (att.x < A.eps && att.y < A.eps && att.z < A.eps) {  // :673-676
+                        st = L_END;
+                    } else if (rnd(seed, ridx) >= A.rr) {                   // :679-681
+                        st = L_END;
+                    } else {
+                        att = divs(att, A.rr);                              // :683
+                        if (left == 0u) {
+                            st = L_END;                                     // :633
+                        } else {
+                            left -= 1u;                                     // :634
+                            st = L_TRACE;
+                        }
+                    }
+                }
+            }
+            if (!__any(st == L_END)) break;
+        }
+        if (!__any(st == L_TRACE)) break;
+        iters += 1;
+
+        // ============ trace: get_intersection_with_scene, spheres then faces (:369-393) ============
+        int best = -1;
+        float bt = rtmax;
+        if (st == L_TRACE) {
+            trav += 1;
+            const float a = dot(rd, rd), two_a = 2.0f * a;
+            for (uint32_t i = 0; i < A.n_spheres; ++i) {
+                float t;
+                if (sphere_accept(sph[i], ro, rd, a, two_a, rtmin, bt, t)) { bt = t; best = (int)i; }
+            }
+#pragma unroll 2
+            for (uint32_t i = 0; i < A.n_faces; ++i) {
+                float t;
+                if (tri_accept(tri[i], ro, rd, rtmin, bt, t)) { bt = t; best = (int)(A.n_spheres + i); }
+            }
+        }
+
+        // ============ hit record + emission / miss (:636-661) ============
+        if (st == L_TRACE) {
+            if (best < 0) {
+                col = add(col, mulv(att, mk(0, 0, 0)));   // sample_infinite_light = 0 (:600-606)
+                st = L_END;
+            } else {
+                f3 hpos, hn;
+                uint32_t hm;
+                bool ho = true;
+                hpos = add(ro, muls(rd, bt));
+                if ((uint32_t)best < A.n_spheres) {                         // :314-319
+                    const rvcp_sphere_t S = sph[best];
+                    const f3 ce = ld3(S.center);
+                    hn = normalize(sub(hpos, ce));
+                    const f3 oc = sub(ro, ce);
+                    if (dot(oc, oc) < S.radius * S.radius) { hn = neg(hn); ho = false; }
+                    hm = S.material_id;
+                } else {                                                    // :348-363
+                    const int fi = best - (int)A.n_spheres;
+                    const TriRecord T = tri[fi];
+                    const FaceShade fs = shade[fi];
+                    const f3 s = mk(ro.x - T.v0[0], ro.y - T.v0[1], ro.z - T.v0[2]);
+                    const f3 s1 = cross(rd, ld3(T.e2));
+                    const f3 s2 = cross(s, ld3(T.e1));
+                    const float f = rcp_ieee(dot(s1, ld3(T.e1)));
+                    const float b1 = f * dot(s1, s);
+                    const float b2 = f * dot(s2, rd);
+                    hn = normalize(add(add(muls(ld3(fs.n0), 1.0f - b1 - b2), muls(ld3(fs.n1), b1)),
+                                       muls(ld3(fs.n2), b2)));
+                    if (dot(hn, rd) > 0.0f) { hn = neg(hn); ho = false; }
+                    hm = fs.mat;
+                }
+                const rvcp_material_t &M = mats[hm];
+                if (M.ty == kLight) {                                       // :656-660
+                    col = add(col, mulv(att, ld3(M.albedo)));
+                    st = L_END;
+                } else {
+                    H_pos = hpos; H_nrm = hn; H_dir = rd; H_mat = hm; H_out = ho;
+                    st = L_SCATTER;
+                }
+            }
+            if (primary) {
+                primary = false;
+                if (st == L_END) {
+                    // miss / light: every sample returns this same color without touching the
+                    // RNG; sum it SPP times in order (:816-818)
+                    for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, col);
+                    store_pixel(pix, divs(acc, sppf), A, unorm_t, out_rgba, out_lin);
+                    need_pixel = true;
+                    st = L_IDLE;
+                } else {
+                    P_pos = H_pos; P_nrm = H_nrm; P_dir = H_dir; P_mat = H_mat; P_out = H_out;
+                    left = A.max_bounces - 1u;
+                }
+            }
+        }
+    }
+    flush_counters(counters, lane, trav, iters);
+}
+
 }  // namespace rvcp
 
 extern "C" int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
@@ -1185,6 +1446,28 @@ extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_dual_kernel, rvcp::kBlock, 0)
         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_kernel, rvcp::kBlock, 0);
     if (e != hipSuccess) return -2;
+    *blocks_per_cu = b;
+    return 0;
+}
+
+extern "C" int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
+                                  const rvcp::FaceShade *shade, const void *spheres,
+                                  const void *materials, const float *unorm_t, uint32_t *out_rgba,
+                                  float *out_lin, unsigned long long *counters,
+                                  uint32_t grid_blocks, void *stream)
+{
+    hipLaunchKernelGGL(rvcp::legacy_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+                       (hipStream_t)stream, *args, tri, shade, (const rvcp_sphere_t *)spheres,
+                       (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int rvcp_legacy_occupancy(int *blocks_per_cu)
+{
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::legacy_kernel, rvcp::kBlock, 0) !=
+        hipSuccess)
+        return -2;
     *blocks_per_cu = b;
     return 0;
 }

@@ -403,3 +403,49 @@ def with_random_triangles(base: Scene, n: int, seed: int = C5_SEED) -> Scene:
     mesh = ArrayMesh(np.concatenate([bv, nv]), np.concatenate([bf, nf]))
     sc = Scene(base.camera, list(base.materials), list(base.spheres), mesh)
     return sc
+
+
+# --------------------------------------------------------------------------------------
+# Sphere scene of the deprecated host (integrator mode 2 fixture)
+# --------------------------------------------------------------------------------------
+def sphere_scene() -> Scene:
+    """``impl Default for Scene`` of src/ray_tracer_deprecated/scene/mod.rs:21-185: 8 spheres,
+    11 materials (Lambertian, metal, dielectric, light), an open-front room of 12 faces."""
+    camera = Camera.new(vec3(0.0, 1.0, 3.0), vec3(0.0, 0.0, 0.0), 0.1, 1000.0, 120.0, 3.0, 10.0)
+    materials = [
+        Material.new_lambertian(vec3(1.0, 1.0, 1.0)),
+        Material.new_lambertian(vec3(0.8, 0.3, 0.3)),
+        Material.new_lambertian(vec3(0.3, 0.7, 0.3)),
+        Material.new_metal(vec3(0.8, 0.8, 0.8), 0.3),
+        Material.new_metal(vec3(1.0, 1.0, 1.0), 0.0),
+        Material.new_metal(vec3(0.5, 0.4, 0.9), 0.3),
+        Material.new_dielectric(1.3),
+        Material.new_dielectric(2.5),
+        Material.new_light(vec3(1.0, 1.0, 1.0)),
+        Material.new_lambertian(vec3(1.0, 0.0, 0.0)),     # red
+        Material.new_lambertian(vec3(0.0, 1.0, 0.0)),     # green
+    ]
+    spheres = [Sphere(vec3(*c), float(np.float32(r)), m) for c, r, m in [
+        ((0.0, 1.0, 0.0), 1.0, 1), ((-1.5, 0.5, 2.0), 0.5, 2), ((-2.0, 1.0, 0.0), 1.0, 3),
+        ((0.0, 0.25, 1.75), 0.25, 4), ((1.5, 0.25, 1.75), 0.25, 5), ((1.25, 0.25, 1.25), 0.25, 6),
+        ((2.0, 1.0, 0.0), 1.0, 7), ((-1.0, 0.25, 1.0), 0.25, 8)]]
+    Hh, Ww, LW = f32(5.0), f32(5.0), f32(5.0)
+    ly = f32(Hh - f32(0.01))
+    V = []
+
+    def quad(ps, n):
+        for p in ps:
+            V.append(Vertex(np.asarray(p, dtype=f32), np.asarray(n, dtype=f32)))
+
+    quad([vec3(-LW, ly, -LW), vec3(-LW, ly, LW), vec3(LW, ly, LW), vec3(LW, ly, -LW)], vec3(0, 1, 0))
+    quad([vec3(-Ww, Hh, -Ww), vec3(-Ww, Hh, Ww), vec3(Ww, Hh, Ww), vec3(Ww, Hh, -Ww)], vec3(0, -1, 0))
+    quad([vec3(-Ww, 0, -Ww), vec3(-Ww, 0, Ww), vec3(-Ww, Hh, Ww), vec3(-Ww, Hh, -Ww)], vec3(1, 0, 0))
+    quad([vec3(Ww, 0, -Ww), vec3(Ww, 0, Ww), vec3(Ww, Hh, Ww), vec3(Ww, Hh, -Ww)], vec3(-1, 0, 0))
+    quad([vec3(-Ww, 0, Ww), vec3(Ww, 0, Ww), vec3(Ww, Hh, Ww), vec3(-Ww, Hh, Ww)], vec3(0, 0, -1))
+    quad([vec3(-Ww, 0, -Ww), vec3(Ww, 0, -Ww), vec3(Ww, Hh, -Ww), vec3(-Ww, Hh, -Ww)], vec3(0, 0, 1))
+    quad([vec3(-Ww, 0, -Ww), vec3(-Ww, 0, Ww), vec3(Ww, 0, Ww), vec3(Ww, 0, -Ww)], vec3(0, 1, 0))
+    F = []
+    for base, mat in ((0, 8), (4, 0), (8, 9), (12, 10), (20, 0), (24, 0)):   # front commented out
+        F.append(Face((base, base + 1, base + 2), mat))
+        F.append(Face((base, base + 2, base + 3), mat))
+    return Scene(camera, materials, spheres, Mesh(V, F))

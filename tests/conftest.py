@@ -38,7 +38,8 @@ def cornell():
 
 def scene_arrays(sc):
     return dict(materials=sc.aligned_materials(), vertices=sc.mesh.aligned_vertices(),
-                faces=sc.mesh.aligned_faces(), lum_face_ids=sc.luminous_face_ids())
+                faces=sc.mesh.aligned_faces(), lum_face_ids=sc.luminous_face_ids(),
+                spheres=sc.aligned_spheres())
 
 
 @pytest.fixture(scope="session")

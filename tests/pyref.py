@@ -109,8 +109,14 @@ INF = (F(np.inf), F(np.inf), F(np.inf))
 
 
 class Scene:
-    def __init__(self, materials, vertices, faces, lum_ids, quirk=True):
+    def __init__(self, materials, vertices, faces, lum_ids, quirk=True, spheres=()):
         self.mat = [(tuple(F(x) for x in m["albedo"]), int(m["ty"])) for m in materials]
+        names = getattr(getattr(materials, "dtype", None), "names", None) or ()
+        self.fuzz = [F(m["fuzz"]) if "fuzz" in names else F(0) for m in materials]
+        self.ior = [F(m["refraction_ratio"]) if "refraction_ratio" in names else F(1)
+                    for m in materials]
+        self.sph = [(tuple(F(x) for x in s_["center"]), F(s_["radius"]), int(s_["material_id"]))
+                    for s_ in spheres]
         self.pos = [tuple(F(x) for x in vv["position"][:3]) for vv in vertices]
         self.nrm = [tuple(F(x) for x in vv["normal"][:3]) for vv in vertices]
         self.faces = [(tuple(int(i) for i in f["vertices"]), int(f["material_id"])) for f in faces]
@@ -141,13 +147,13 @@ def intersect(sc, o, d, tmin, tmax, face):
     n = normalize(add(add(scale(sc.nrm[i0], w0), scale(sc.nrm[i1], b1)), scale(sc.nrm[i2], b2)))
     pos = add(o, scale(d, t))
     if dot(n, d) > 0:
-        n = neg(n)
-    return t, pos, n, mid
+        return t, pos, neg(n), mid, False
+    return t, pos, n, mid, True
 
 
 def scene_hit(sc, o, d, tmin, tmax, counter):
     counter[0] += 1
-    best = (F(tmax + F(1.0)), INF, (F(0), F(0), F(0)), 0)
+    best = (F(tmax + F(1.0)), INF, (F(0), F(0), F(0)), 0, True)
     for f in sc.faces:
         h = intersect(sc, o, d, tmin, tmax, f)
         if h is not None and h[0] <= tmax:
@@ -168,7 +174,7 @@ def trace(sc, P, g, o, d, tmin, tmax, counter):
     for depth in range(P["max_bounces"]):
         if att[0] < P["att_stop"] and att[1] < P["att_stop"] and att[2] < P["att_stop"]:
             break
-        t, p, n, mid = scene_hit(sc, o, d, tmin, tmax, counter)
+        t, p, n, mid, _ = scene_hit(sc, o, d, tmin, tmax, counter)
         if t > tmax:
             color = add(color, v(0.1, 0.1, 0.1))
             break
@@ -201,7 +207,7 @@ def trace(sc, P, g, o, d, tmin, tmax, counter):
                 Xn = normalize(sc.nrm[j0])
                 dist = length(sub(X, p))
                 ws = div(sub(X, p), dist)
-                _, bp, _, _ = scene_hit(sc, add(p, scale(ws, P["eps"])), ws, P["t_min"], P["t_max"],
+                _, bp, _, _, _ = scene_hit(sc, add(p, scale(ws, P["eps"])), ws, P["t_min"], P["t_max"],
                                         counter)
                 db = length(sub(bp, p))
                 if abs(F(dist - db)) < P["eps"]:
@@ -228,6 +234,122 @@ def trace(sc, P, g, o, d, tmin, tmax, counter):
     return color
 
 
+# ---- integrator mode 2: ray_tracer.comp ----
+def sphere_hit(o, d, tmin, tmax, sph):
+    """is_intersect_with_sphere + is_intersect_with_quadratic_equation (ray_tracer.comp:260-321)."""
+    ce, r, mid = sph
+    co = sub(o, ce)
+    a = dot(d, d)
+    b = F(F(2.0) * dot(d, co))
+    c = F(dot(co, co) - F(r * r))
+    with np.errstate(all="ignore"):
+        delta = F(F(b * b) - F(F(F(4.0) * a) * c))
+        if delta < 0:
+            return None
+        sq = F(np.sqrt(delta))
+        t0 = F(F(F(-b) + sq) / F(F(2.0) * a))
+        t1 = F(F(F(-b) - sq) / F(F(2.0) * a))
+    if t0 > t1:
+        t0, t1 = t1, t0
+    if tmin <= t0 <= tmax:
+        t = t0
+    elif tmin <= t1 <= tmax:
+        t = t1
+    else:
+        return None
+    pos = add(o, scale(d, t))
+    n = normalize(sub(pos, ce))
+    if dot(co, co) < F(r * r):
+        return t, pos, neg(n), mid, False
+    return t, pos, n, mid, True
+
+
+def scene_hit_legacy(sc, o, d, tmin, tmax, counter):
+    """get_intersection_with_scene, ray_tracer.comp:369-393 (spheres, then faces)."""
+    counter[0] += 1
+    best = (F(tmax + F(1.0)), INF, (F(0), F(0), F(0)), 0, True)
+    for s_ in sc.sph:
+        h = sphere_hit(o, d, tmin, tmax, s_)
+        if h is not None and h[0] <= tmax:
+            tmax, best = h[0], h
+    for f in sc.faces:
+        h = intersect(sc, o, d, tmin, tmax, f)
+        if h is not None and h[0] <= tmax:
+            tmax, best = h[0], h
+    return best
+
+
+def unit_sphere(g):
+    while True:
+        q = (F(F(F(2.0) * g()) - F(1.0)), F(F(F(2.0) * g()) - F(1.0)), F(F(F(2.0) * g()) - F(1.0)))
+        if not dot(q, q) >= 1.0:
+            return q
+
+
+def reflect(i, n):
+    return sub(i, scale(n, F(F(2.0) * dot(n, i))))
+
+
+def refract(i, n, eta):
+    d = dot(n, i)
+    k = F(F(1.0) - F(F(eta * eta) * F(F(1.0) - F(d * d))))
+    if k < 0:
+        return v(0, 0, 0)
+    return sub(scale(i, eta), scale(n, F(F(eta * d) + F(np.sqrt(k)))))
+
+
+def trace_legacy(sc, P, g, o, d, tmin, tmax, counter):
+    """ray_trace, ray_tracer.comp:618-694, with material_scatter :491-602."""
+    color = v(0, 0, 0)
+    att = v(1, 1, 1)
+    for _ in range(P["max_bounces"]):
+        t, p, n, mid, outward = scene_hit_legacy(sc, o, d, tmin, tmax, counter)
+        if t > tmax:
+            color = add(color, mul(att, v(0, 0, 0)))
+            break
+        alb, ty = sc.mat[mid]
+        if ty == 3:
+            color = add(color, mul(att, alb))
+            break
+        na, nd = v(0, 0, 0), v(0, 0, 0)
+        if ty == 0:
+            nd = normalize(add(n, normalize(unit_sphere(g))))
+            if all(abs(c) < P["eps"] for c in nd):
+                nd = n
+            na = alb
+        elif ty == 1:
+            r = reflect(d, n)
+            if dot(r, n) < 0:
+                r = neg(r)
+            while True:
+                nd = normalize(add(r, scale(normalize(unit_sphere(g)), sc.fuzz[mid])))
+                if not dot(nd, n) < 0:
+                    break
+            na = alb
+        elif ty == 2:
+            ratio = F(F(1.0) / sc.ior[mid]) if outward else sc.ior[mid]
+            ct = dot(neg(d), n)
+            with np.errstate(all="ignore"):
+                st = F(np.sqrt(F(F(1.0) - F(ct * ct))))
+            refr = F(ratio * st) <= 1.0
+            if refr:
+                r0 = F(F(F(1.0) - ratio) / F(F(1.0) + ratio))
+                r0 = F(r0 * r0)
+                x = F(F(1.0) - ct)
+                fr = F(r0 + F(F(F(1.0) - r0) * F(F(F(x * x) * F(x * x)) * x)))
+                refr = g() >= fr
+            nd = refract(d, n, ratio) if refr else reflect(d, n)
+            na = v(1, 1, 1)
+        att = mul(att, na)
+        o, d, tmin, tmax = add(p, scale(nd, P["t_min"])), nd, P["t_min"], P["t_max"]
+        if all(c < P["eps"] for c in att):
+            break
+        if g() >= P["rr"]:
+            break
+        att = div(att, P["rr"])
+    return color
+
+
 def render_pixel(sc, P, push, W, H, x, y):
     """Linear RGB of pixel (x, y) and the traversal count."""
     cam = push["camera"]
@@ -249,6 +371,10 @@ def render_pixel(sc, P, push, W, H, x, y):
     d = normalize(sub(uvp, cpos))
     counter = [0]
     color = v(0, 0, 0)
+    if P.get("integrator", 0) == 1:
+        for _ in range(P["spp"]):
+            color = add(color, trace_legacy(sc, P, g, cpos, d, F(tn * tc), F(tf * tc), counter))
+        return div(color, F(P["spp"])), counter[0]
     for _ in range(P["spp"]):
         L = trace(sc, P, g, cpos, d, F(tn * tc), F(tf * tc), counter)
         color = add(color, div(L, F(P["spp"])))
@@ -258,4 +384,5 @@ def render_pixel(sc, P, push, W, H, x, y):
 def params(cfg):
     return dict(spp=int(cfg["spp"]), max_bounces=int(cfg["max_bounces"]),
                 att_stop=F(cfg["attenuation_stop_eps"]), t_min=F(cfg["ray_t_min"]),
-                t_max=F(cfg["ray_t_max"]), rr=F(cfg["rr_probability"]), eps=F(cfg["eps"]))
+                t_max=F(cfg["ray_t_max"]), rr=F(cfg["rr_probability"]), eps=F(cfg["eps"]),
+                integrator=int(cfg["integrator"]))

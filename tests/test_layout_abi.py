@@ -117,6 +117,7 @@ def test_library_has_gfx950_code_object():
     blob = open(abi.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob          # the offload bundle targets gfx950
     assert b"games101_kernel" in blob
+    assert b"legacy_kernel" in blob
 
 
 def test_config_default_matches_reference_defines():
@@ -129,6 +130,21 @@ def test_config_default_matches_reference_defines():
     assert (int(c["spp"]), int(c["max_bounces"])) == (20, 15)
     assert np.float32(c["rr_probability"]) == np.float32(0.8)
     assert np.float32(c["eps"]) == np.float32(0.001)
+
+
+def test_config_default_for_legacy_matches_ray_tracer_comp():
+    L = abi.load()
+    c = np.zeros((), dtype=abi.CONFIG_DTYPE)
+    assert L.rvcp_config_default_for(abi.INTEGRATOR_LEGACY, abi.ptr(c)) == 0
+    assert c.tobytes() == abi.make_config(integrator=abi.INTEGRATOR_LEGACY).tobytes()
+    # ray_tracer.comp:5-13
+    assert (int(c["integrator"]), int(c["spp"]), int(c["max_bounces"])) == (1, 5, 3)
+    assert np.float32(c["rr_probability"]) == np.float32(1.0)
+    assert np.float32(c["ray_t_max"]) == np.float32(1000.0)
+    g = np.zeros((), dtype=abi.CONFIG_DTYPE)
+    assert L.rvcp_config_default_for(abi.INTEGRATOR_GAMES101, abi.ptr(g)) == 0
+    assert g.tobytes() == abi.make_config().tobytes()
+    assert L.rvcp_config_default_for(9, abi.ptr(g)) == abi.RVCP_E_UNSUPPORTED
 
 
 def test_create_rejects_bad_config_without_device():

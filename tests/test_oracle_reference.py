@@ -62,7 +62,8 @@ def _pyref_check(sc, cfg, W, H, pixels, time=TIME):
     arrays = scene_arrays(sc)
     lin, _, _ = O.render(arrays, sc.push_constant(time), cfg, W, H)
     ps = pyref.Scene(arrays["materials"], arrays["vertices"], arrays["faces"],
-                     arrays["lum_face_ids"], quirk=bool(cfg["lum_id_std140_quirk"]))
+                     arrays["lum_face_ids"], quirk=bool(cfg["lum_id_std140_quirk"]),
+                     spheres=arrays["spheres"] if int(cfg["integrator"]) == 1 else ())
     P = pyref.params(cfg)
     for (x, y) in pixels:
         c, _ = pyref.render_pixel(ps, P, sc.push_constant(time), W, H, x, y)
@@ -96,3 +97,46 @@ def test_pyref_moved_camera_random_mesh(cornell):
                           cornell.materials, [], cornell.mesh)
     sc = rvcp_amd.scene.with_random_triangles(base, 40)
     _pyref_check(sc, rvcp_amd.abi.make_config(spp=1), 16, 12, _pixels(16, 12, 8, 4))
+
+
+# ---- integrator mode 2 (ray_tracer.comp, the file north_star names) ----
+def test_pyref_legacy_sphere_scene():
+    sc = rvcp_amd.scene.sphere_scene()
+    _pyref_check(sc, rvcp_amd.abi.make_config(integrator=1, spp=2), 24, 24,
+                 _pixels(24, 24, 24, 5), time=3.25)
+
+
+def test_pyref_legacy_params():
+    sc = rvcp_amd.scene.sphere_scene()
+    cfg = rvcp_amd.abi.make_config(integrator=1, spp=1, max_bounces=6, rr_probability=0.8)
+    _pyref_check(sc, cfg, 20, 16, _pixels(20, 16, 16, 6), time=11.0)
+
+
+def test_pyref_legacy_cornell(cornell):
+    _pyref_check(cornell, rvcp_amd.abi.make_config(integrator=1, spp=2), 16, 16,
+                 _pixels(16, 16, 12, 7))
+
+
+def test_legacy_oracle_image_statistics():
+    """Mode 2 on the deprecated host's sphere scene: the room is lit only by the roof light
+    (miss = black, no NEE), every path ends on a light or a miss, and the image is UNORM
+    (no gamma): u8 = round-half-up(255 * c) for c in [0, 1]."""
+    sc = rvcp_amd.scene.sphere_scene()
+    cfg = rvcp_amd.abi.make_config(integrator=1)
+    arrays = scene_arrays(sc)
+    lin, rgba, trav = O.render(arrays, sc.push_constant(1.0), cfg, 64, 64)
+    assert np.isfinite(lin).all() and (lin >= 0).all() and (lin <= 1.0).all()
+    exp = np.floor(np.clip(lin, 0, 1) * 255.0 + 0.5).astype(np.uint8)
+    assert np.abs(exp.astype(int) - rgba[..., :3]).max() <= 1
+    assert (rgba[..., 3] == 255).all()
+    spp = int(cfg["spp"])
+    assert 64 * 64 * spp <= trav <= 64 * 64 * spp * int(cfg["max_bounces"])
+    assert 0.2 < float(lin.mean()) < 0.8
+
+
+def test_unorm_thresholds():
+    for k in range(1, 256):
+        t = np.float32((k - 0.5) / 255.0)
+        assert O.unorm_u8(float(t)) == k
+        assert O.unorm_u8(float(np.nextafter(t, np.float32(0)))) == k - 1
+    assert O.unorm_u8(-1.0) == 0 and O.unorm_u8(2.0) == 255 and O.unorm_u8(float("nan")) == 0

@@ -19,16 +19,19 @@ def main():
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=30)
     ap.add_argument("--tris", type=int, default=0)
+    ap.add_argument("--integrator", type=int, default=0)
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres"])
     a = ap.parse_args()
-    sc = rvcp_amd.Scene.default()
+    sc = rvcp_amd.Scene.default() if a.scene == "cornell" else rvcp_amd.scene.sphere_scene()
     if a.tris:
         sc = rvcp_amd.scene.with_random_triangles(sc, a.tris)
-    with rvcp_amd.RayTracer(spp=a.spp, kernel_variant=a.variant) as rt:
+    with rvcp_amd.RayTracer(spp=a.spp, kernel_variant=a.variant, integrator=a.integrator) as rt:
         rt.upload_scene(sc)
         for _ in range(a.frames):
             rt.render(a.size, a.size, 123.0)
             st = rt.last_stats
-            print(json.dumps({"variant": a.variant, "kernel_ms": round(float(st["kernel_ms"]), 3),
+            print(json.dumps({"variant": a.variant, "integrator": a.integrator,
+                              "traversals": int(st["traversals"]), "kernel_ms": round(float(st["kernel_ms"]), 3),
                               "executed": int(st["traversals_executed"]),
                               "wave_iterations": int(st["wave_iterations"])}), flush=True)
 

@@ -33,6 +33,8 @@ for s in $STEPS; do
     case $s in
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        legacy) run pytest_legacy 600 python -m pytest tests/test_gpu_legacy.py -m gpu -x -q ;;
+        lframes) run lframes 300 python tools/frames.py --integrator 1 --scene spheres --frames 5 --spp 5 ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
         bench2) run bench_c2 300 python bench.py --workload c2 --steps 50 --warmup 5 --no-cpu-baseline ;;
         rehearse2) run rehearse2 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
