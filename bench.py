@@ -14,11 +14,17 @@ Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
   c2: Cornell 384x384 SPP=10 (README benchmark row).
   c4: Cornell 2048x2048 SPP=64, fixed frame sharded over N GPUs ("scaling": "strong").
   c5: Cornell + 100k random triangles, 1024x1024 SPP=30.
+  spheres: integrator mode 2 (ray_tracer.comp) on the deprecated host's sphere room,
+      1024x1024 at its SPP=5 (not a BASELINE config; reported for coverage).
 
-Rank 0 prints ONE JSON line.  `roofline` uses the BASELINE.md definition: algorithmic bytes
-= traversals x F x 36 B per launch over the kernel's HIP-event time; `cpu_baseline` times the
-scalar C++ oracle (oracle/rvcp_oracle.c, the CPU re-execution of the same kernel) on a
-bounded sample of the workload, on rank 0 at N=1 only.
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the path-tracing kernel,
+>99% of the frame's GPU time): algorithmic bytes = its reference-algorithm traversals x F x
+36 B per launch (the primary rays the pre-pass traces once are the only
+traversals not attributed to it) over its HIP-event time (rvcp_stats_t.main_kernel_ms,
+events on the launch stream).  `traffic` is the same kernel's measured HBM bytes per launch
+from the rocprofv3 PMC summary committed under profiles/ (tools/pmc_traffic.py), when one
+exists for the workload.  `cpu_baseline` times the scalar C oracle (oracle/rvcp_oracle.c, the
+CPU re-execution of the same kernel) on a bounded sample of the workload, rank 0 at N=1 only.
 """
 import argparse
 import json
@@ -52,18 +58,36 @@ def workload(name, n_gpus):
     if name == "c5":
         return dict(workload="cornell_plus_100k_tris_1024sq_spp30", W=1024, H=1024, spp=30,
                     extra_tris=100000, scaling="strong")
+    if name == "spheres":
+        return dict(workload="spheres_mode2_1024sq_spp5", W=1024, H=1024, spp=5, extra_tris=0,
+                    scaling="strong", integrator=1)
     raise SystemExit(f"unknown workload {name}")
 
 
+def load_traffic(workload_name, kernel_substr):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{workload_name}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for name, k in d.get("kernels", {}).items():
+        if kernel_substr in name and k.get("bytes"):
+            return float(k["bytes"]), os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def cpu_baseline(sc, cfg_kw, W, H, threads):
-    """Time the CPU oracle (scalar C++ re-execution) on every 8th row of the workload."""
+    """Time the CPU oracle (scalar C re-execution) on a bounded sample of the workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     import rvcp_amd
     O.build()
     cfg = rvcp_amd.abi.make_config(**cfg_kw)
     arrays = dict(materials=sc.aligned_materials(), vertices=sc.mesh.aligned_vertices(),
-                  faces=sc.mesh.aligned_faces(), lum_face_ids=sc.luminous_face_ids())
+                  faces=sc.mesh.aligned_faces(), lum_face_ids=sc.luminous_face_ids(),
+                  spheres=sc.aligned_spheres())
     push = sc.push_constant(123.0)
     rows = list(range(0, H, 8))
     O.render(arrays, push, cfg, W, H, rect=(0, H // 2, min(W, 64), 1), threads=threads,
@@ -75,14 +99,23 @@ def cpu_baseline(sc, cfg_kw, W, H, threads):
         dt = time.perf_counter() - t0
         return dict(value=128 * 128 / dt / 1e6, unit="Msamples/s", cores=threads, kind="port",
                     sample="128x128 SPP=1 frame of the same scene", seconds=round(dt, 3))
+    # the whole frame on `threads` threads (a few seconds), then a single-thread figure on
+    # every 64th row
     t0 = time.perf_counter()
-    for y in rows:
-        O.render(arrays, push, cfg, W, H, rect=(0, y, W, 1), threads=threads, want_linear=False)
+    O.render(arrays, push, cfg, W, H, threads=threads, want_linear=False)
     dt = time.perf_counter() - t0
-    samples = len(rows) * W * cfg_kw["spp"]
+    samples = W * H * cfg_kw["spp"]
+    rows1 = list(range(0, H, 64))
+    t1 = time.perf_counter()
+    for y in rows1:
+        O.render(arrays, push, cfg, W, H, rect=(0, y, W, 1), threads=1, want_linear=False)
+    dt1 = time.perf_counter() - t1
     return dict(value=samples / dt / 1e6, unit="Msamples/s", cores=threads, kind="port",
-                sample=f"every 8th row ({len(rows)} of {H}) of the {W}x{H} SPP={cfg_kw['spp']} "
-                       f"frame, {threads} threads", seconds=round(dt, 3))
+                sample=f"the full {W}x{H} SPP={cfg_kw['spp']} frame on {threads} threads",
+                seconds=round(dt, 3),
+                single_thread_value=round(len(rows1) * W * cfg_kw["spp"] / dt1 / 1e6, 4),
+                single_thread_sample=f"every 64th row ({len(rows1)} rows), 1 thread",
+                single_thread_seconds=round(dt1, 3))
 
 
 def main():
@@ -90,7 +123,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5", "spheres"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--save-frame", default="")
@@ -120,14 +153,18 @@ def main():
 
     wl = workload(args.workload, world)
     W, H, spp = wl["W"], wl["H"], wl["spp"]
-    sc = rvcp_amd.Scene.default()
+    legacy = wl.get("integrator", 0) == 1
+    sc = rvcp_amd.scene.sphere_scene() if legacy else rvcp_amd.Scene.default()
     if wl["extra_tris"]:
         sc = rvcp_amd.scene.with_random_triangles(sc, wl["extra_tris"])
     cfg_kw = dict(spp=spp, device=local_rank)
+    if legacy:
+        cfg_kw["integrator"] = 1
     rt = rvcp_amd.RayTracer(**cfg_kw)
     rt.upload_scene(sc)
     push = sc.push_constant(123.0)
     n_faces = len(sc.mesh.aligned_faces())
+    n_spheres = len(sc.spheres) if legacy else 0
 
     rows = rvcp_amd.shard_rows(H, rank, world)
     slot = max(rvcp_amd.shard_rows(H, k, world) for k in range(world))
@@ -161,11 +198,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, trav, trav_exec = [], 0, 0
+    kernel_ms, main_ms, trav, trav_exec = [], [], 0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = step()
         kernel_ms.append(float(st["kernel_ms"]))
+        main_ms.append(float(st["main_kernel_ms"]))
         trav += int(st["traversals"])
         trav_exec += int(st["traversals_executed"])
     torch.cuda.synchronize()
@@ -182,12 +220,22 @@ def main():
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed * 1000.0 / args.steps
 
-    # roofline for the dominant kernel (this rank's launches)
-    avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1000.0
-    bytes_per_launch = trav / args.steps * n_faces * 36
+    # roofline for the dominant kernel (this rank's launches).  The pre-pass (variants 3/4,
+    # games101 only) traces each pixel's primary ray once; every other reference-algorithm
+    # traversal -- including the reused primary hits of samples 2..SPP -- belongs to the
+    # path kernel.
+    avg_frame_s = (sum(kernel_ms) / len(kernel_ms)) / 1000.0
+    avg_kernel_s = (sum(main_ms) / len(main_ms)) / 1000.0
+    prepass = 0 if legacy else rows * W
+    units = trav / args.steps - prepass                     # traversals per path-kernel launch
+    # a traversal tests F triangles (36 B each) and, in mode 2, S spheres (16 B each)
+    bytes_per_launch = units * (n_faces * 36 + n_spheres * 16)
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
-    tests_per_s = trav / args.steps * n_faces / avg_kernel_s
-    exec_tests_per_s = trav_exec / args.steps * n_faces / avg_kernel_s
+    tests_per_s = units * (n_faces + n_spheres) / avg_kernel_s
+    exec_tests_per_s = (trav_exec / args.steps - prepass) * (n_faces + n_spheres) / avg_kernel_s
+    kname = "legacy_kernel" if legacy else ("games101_tiled_kernel" if n_faces >= 4096
+                                             else "games101_path_kernel")
+    traffic, traffic_src = load_traffic(wl["workload"], kname)
 
     frame_check = None
     if world > 1 and rank == 0:
@@ -215,16 +263,24 @@ def main():
             "scaling": wl["scaling"],
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)",
+            "data": ("synthetic (the reference's deprecated sphere-room scene, integrator mode 2, "
+                     "fixed time seed 123.0)" if legacy else
+                     "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)"),
             "config": {"workload": wl["workload"], "width": W, "height": H, "spp": spp,
                        "faces": n_faces, "parallelism": f"pixel-stripes x{world}",
                        "gather": ("gloo-rehearsal" if rehearsal else "rccl") if world > 1 else "none"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_source": traffic_src,
+                         "kernel": kname,
                          "kernel_ms": round(avg_kernel_s * 1000.0, 4),
-                         "definition": "traversals x F x 36 B per launch / kernel time "
-                                       "(BASELINE.md §2; reference-algorithm traversals)",
+                         "frame_kernels_ms": round(avg_frame_s * 1000.0, 4),
+                         "algorithmic_bytes_per_launch": round(bytes_per_launch),
+                         "definition": "reference-algorithm traversals of the path kernel x "
+                                       "(F x 36 B + S x 16 B) per launch / its HIP-event time "
+                                       "(SURVEY.md §8(d))",
                          "traversals_per_sample": round(trav / args.steps / (W * H * spp / world), 4)
                          if world == 1 else None,
                          "executed_traversal_frac": round(trav_exec / max(trav, 1), 4),

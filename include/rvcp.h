@@ -143,6 +143,9 @@ typedef struct rvcp_stats {
     uint32_t _reserved;
     uint64_t wave_iterations;         /* wave-level trace iterations; lane utilisation of the
                                          scan = traversals_executed / (64 * wave_iterations) */
+    double main_kernel_ms;            /* device time of the dominant (path-tracing) kernel
+                                         alone, HIP events on the launch stream; kernel_ms
+                                         also covers the primary pre-pass and counter reset */
 } rvcp_stats_t;
 
 /* Layout checks: sizes/offsets the reference's Rust structs and std140/std430 blocks imply. */

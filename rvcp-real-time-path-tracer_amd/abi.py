@@ -22,8 +22,9 @@ CONFIG_DTYPE = np.dtype([("device", "<i4"), ("integrator", "<i4"), ("spp", "<u4"
                          ("_reserved", "<u4", 5)])
 STATS_DTYPE = np.dtype([("kernel_ms", "<f8"), ("traversals", "<u8"),
                         ("traversals_executed", "<u8"), ("samples", "<u8"), ("faces", "<u4"),
-                        ("_reserved", "<u4"), ("wave_iterations", "<u8")])
-assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 48
+                        ("_reserved", "<u4"), ("wave_iterations", "<u8"),
+                        ("main_kernel_ms", "<f8")])
+assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 56
 
 # Defaults == the shader's #defines (ray_tracer_games101_branch.comp:5-13).
 DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop_eps=0.05,

@@ -26,7 +26,7 @@ struct rvcp_ctx {
     rvcp_config_t cfg{};
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;   // start, main kernel, end
     int grid_capacity[kMaxVariant + 1] = {};   // resident workgroups per kernel variant
     int legacy_capacity = 0;                   // ... of the RVCP_INTEGRATOR_LEGACY kernel
 
@@ -222,7 +222,8 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     int rc;
     if (hipSetDevice(ctx->device) != hipSuccess) return bail(fail(ctx, RVCP_E_HIP, "hipSetDevice"));
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess)
+        hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->evm) != hipSuccess ||
+        hipEventCreate(&ctx->ev1) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "stream/event creation failed"));
 
     // Gamma thresholds T[k] = float(((k - 0.5) / 255)^(1/0.6)), DESIGN.md §3.3
@@ -272,6 +273,7 @@ int rvcp_destroy(rvcp_ctx_t *ctx)
     (void)hipFree(ctx->d_lin);
     (void)hipFree(ctx->d_surf);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->evm) (void)hipEventDestroy(ctx->evm);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -442,6 +444,7 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     if (A.n_pixels > 0) {
         int rc;
         if (trivial) {
+            HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
             rc = rvcp_launch_fill((uint32_t *)d_rgba8, (float *)d_linear_rgb, A.n_pixels,
                                   0xFF000000u, s);
         } else {
@@ -453,6 +456,7 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
             if (blocks == 0) blocks = 1;
             A.static_chunks = blocks * (kBlock / kWave) * kChunk;
             if (legacy) {
+                HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_legacy(&A, ctx->d_tri, ctx->d_shade, ctx->d_spheres,
                                         ctx->d_rawmats, ctx->d_unorm, (uint32_t *)d_rgba8,
                                         (float *)d_linear_rgb, ctx->d_counters, blocks, s);
@@ -468,8 +472,9 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
                                              ctx->d_mats, ctx->d_lights, ctx->d_gamma,
                                              (uint32_t *)d_rgba8, (float *)d_linear_rgb,
                                              ctx->d_counters, ctx->d_surf, ctx->d_shade,
-                                             blocks, s);
+                                             blocks, s, ctx->evm);
             } else {
+                HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_games101(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts, ctx->d_mats,
                                           ctx->d_lights, ctx->d_gamma, (uint32_t *)d_rgba8,
                                           (float *)d_linear_rgb, ctx->d_counters, blocks, s);
@@ -477,6 +482,8 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
         }
         if (rc != 0) return fail(ctx, RVCP_E_HIP, std::string("kernel launch failed: ") +
                                                       hipGetErrorString(hipGetLastError()));
+    } else {
+        HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
     }
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
     ctx->pending = true;
@@ -499,6 +506,9 @@ int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         unsigned long long c[4] = {0, 0, 0, 0};
         HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
         stats->kernel_ms = ms;
+        float ms_main = 0.0f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms_main, ctx->evm, ctx->ev1));
+        stats->main_kernel_ms = ms_main;
         stats->traversals_executed = c[0];
         // the reference re-traces the (RNG-independent) primary ray in every sample
         stats->traversals = ctx->last_trivial ? 0 : c[0] + ctx->last_pixels * (ctx->last_spp - 1);

@@ -120,7 +120,7 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *
                             const rvcp::LightRecord *lights, const float *gamma_t,
                             uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
                             rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
-                            uint32_t grid_blocks, void *stream);
+                            uint32_t grid_blocks, void *stream, void *main_event);
 // Integrator RVCP_INTEGRATOR_LEGACY (ray_tracer.comp): materials / spheres are the raw
 // rvcp_material_t / rvcp_sphere_t arrays, unorm_t the UNORM8 threshold table.
 int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,

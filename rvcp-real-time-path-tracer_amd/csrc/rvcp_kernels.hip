@@ -1402,13 +1402,15 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                                        uint32_t *out_rgba, float *out_lin,
                                        unsigned long long *counters, rvcp::SurfRecord *surf,
                                        const rvcp::FaceShade *shade, uint32_t grid_blocks,
-                                       void *stream)
+                                       void *stream, void *main_event)
 {
     const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
     hipLaunchKernelGGL(rvcp::games101_primary_kernel, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
                        (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
                        (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
                        surf, shade);
+    if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
+        return -2;
     auto kern = args->variant == 4 ? rvcp::games101_tiled_kernel : rvcp::games101_path_kernel;
     hipLaunchKernelGGL(kern, dim3(grid_blocks), dim3(rvcp::kBlock), 0, (hipStream_t)stream,
                        *args, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,

@@ -33,7 +33,7 @@ int main(void) {
   F(rvcp_config_t, rr_probability); F(rvcp_config_t, eps); F(rvcp_config_t, lum_id_std140_quirk);
   S(rvcp_stats_t); F(rvcp_stats_t, kernel_ms); F(rvcp_stats_t, traversals);
   F(rvcp_stats_t, traversals_executed); F(rvcp_stats_t, samples); F(rvcp_stats_t, faces);
-  F(rvcp_stats_t, wave_iterations);
+  F(rvcp_stats_t, wave_iterations); F(rvcp_stats_t, main_kernel_ms);
   S(rvcp_lengths_t);
   return 0;
 }

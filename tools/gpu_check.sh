@@ -50,6 +50,10 @@ for s in $STEPS; do
         sqpmc) run sqpmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 tools/frames.py --variant 2 --frames 2 ;;
         sqpmc2) run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 tools/frames.py --variant 2 --frames 2 ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
+        pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+        pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+        benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 ;;
+        profs) run profs 600 rocprofv3 --kernel-trace --stats -d "$OUT/profs_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 20 --warmup 2 --no-cpu-baseline ;;
         pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     esac
 done
