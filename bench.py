@@ -39,6 +39,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# the reference's published C3 row (README.md:26, 3 fps on an RTX 3060) and
+# C2 row (README.md:22, 51 fps), as Msamples/s
+REFERENCE_MSAMPLES = {"c3": 94.4, "c2": 75.2}
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (spec)
 FLOP_PER_TEST = 52
 
@@ -261,7 +264,8 @@ def main():
             "fps": round(1000.0 / ms_per_step, 2),
             "higher_is_better": True,
             "scaling": wl["scaling"],
-            "vs_baseline": None,
+            "vs_baseline": (round(value / REFERENCE_MSAMPLES[args.workload], 2)
+                            if args.workload in REFERENCE_MSAMPLES else None),
             "dtype": "f32",
             "data": ("synthetic (the reference's deprecated sphere-room scene, integrator mode 2, "
                      "fixed time seed 123.0)" if legacy else
