@@ -9,7 +9,8 @@ from .scene import (Camera, Face, Material, MaterialType, Mesh, Scene, Sphere, V
                     cornell_box, push_constant)
 from .ray_tracer import RayTracer, shard_row_ids, shard_rows
 from . import frame
+from . import interactive
 
-__all__ = ["abi", "scene", "frame", "Camera", "Face", "Material", "MaterialType", "Mesh", "Scene",
+__all__ = ["abi", "scene", "frame", "interactive", "Camera", "Face", "Material", "MaterialType", "Mesh", "Scene",
            "Sphere", "Vertex", "cornell_box", "push_constant", "RayTracer", "shard_rows",
            "shard_row_ids"]

@@ -10,6 +10,8 @@ component-wise cross), so the uploaded bytes equal what the Rust host uploads.
 """
 from __future__ import annotations
 
+import ctypes
+import ctypes.util
 import enum
 from dataclasses import dataclass, field
 from typing import List
@@ -17,6 +19,17 @@ from typing import List
 import numpy as np
 
 f32 = np.float32
+
+# Rust's f32 transcendental functions call the platform libm; use the same float functions.
+_libm = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+for _n in ("sinf", "cosf", "asinf", "tanf"):
+    getattr(_libm, _n).argtypes = [ctypes.c_float]
+    getattr(_libm, _n).restype = ctypes.c_float
+_libm.atan2f.argtypes = [ctypes.c_float, ctypes.c_float]
+_libm.atan2f.restype = ctypes.c_float
+# core::f32::to_radians / to_degrees constants
+RADS_PER_DEG = f32(f32(np.pi) / f32(180.0))
+DEGS_PER_RAD = f32(57.2957795130823208767981548141051703)
 
 # --------------------------------------------------------------------------------------
 # numpy record types == include/rvcp.h structs
@@ -89,8 +102,9 @@ class Camera:
         forward = normalize((look_at - position).astype(f32))
         right = normalize(cross(forward, Y))
         up = normalize(cross(right, forward))
-        yaw = float(np.degrees(np.arctan2(forward[2], forward[0])))
-        pitch = float(np.degrees(np.arcsin(forward[1])))
+        # forward.z.atan2(forward.x).to_degrees(), forward.y.asin().to_degrees() in f32
+        yaw = float(f32(f32(_libm.atan2f(float(forward[2]), float(forward[0]))) * DEGS_PER_RAD))
+        pitch = float(f32(f32(_libm.asinf(float(forward[1]))) * DEGS_PER_RAD))
         return Camera(position, float(f32(t_near)), float(f32(t_far)), float(f32(vertical_fov)),
                       float(move_speed), float(rotate_speed), up, forward, right, yaw, pitch)
 
