@@ -222,6 +222,14 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx,
                       const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
                       const uint32_t *lum_sphere_ids, uint32_t n_lum_sphere_ids);
 
+/* Load a binary scene file (.rvcpscn: "RVCPSCN1" header, rvcp_lengths_t, rvcp_camera_t,
+ * then the upload arrays in the layouts above; format in scene_io.py) and upload it as
+ * rvcp_upload_scene would.  The camera stored in the file is copied to *out_camera when
+ * non-NULL.  Replaces the reference's compiled-in scene (`Scene::default`,
+ * src/ray_tracer/scene/mod.rs:21) as the way to feed large meshes.
+ * RVCP_E_INVALID for an unreadable, truncated or malformed file. */
+int rvcp_upload_scene_file(rvcp_ctx_t *ctx, const char *path, rvcp_camera_t *out_camera);
+
 /* Render one full frame synchronously into host memory.  Replaces the per-frame
  * `push_constants(...)` + `dispatch([W/8, H/8, 1])` + present of vulkan.rs:406-452 and
  * :298-404.  out_rgba8: W*H*4 bytes, row-major, logical RGBA (the reference's swapchain was

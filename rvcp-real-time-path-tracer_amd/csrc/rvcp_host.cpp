@@ -385,6 +385,60 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     return RVCP_OK;
 }
 
+int rvcp_upload_scene_file(rvcp_ctx_t *ctx, const char *path, rvcp_camera_t *out_camera)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!path) return fail(ctx, RVCP_E_INVALID, "null path");
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return fail(ctx, RVCP_E_INVALID, std::string("cannot open scene file ") + path);
+    std::vector<unsigned char> data;
+    unsigned char buf[1 << 16];
+    size_t got;
+    while ((got = std::fread(buf, 1, sizeof(buf), f)) > 0) data.insert(data.end(), buf, buf + got);
+    const bool read_error = std::ferror(f) != 0;
+    std::fclose(f);
+    if (read_error) return fail(ctx, RVCP_E_INVALID, "error reading scene file");
+    constexpr size_t kHeader = 128;
+    if (data.size() < kHeader || std::memcmp(data.data(), "RVCPSCN1", 8) != 0)
+        return fail(ctx, RVCP_E_INVALID, "not an RVCPSCN1 scene file");
+    uint32_t version, header_bytes;
+    rvcp_lengths_t L;
+    std::memcpy(&version, data.data() + 8, 4);
+    std::memcpy(&header_bytes, data.data() + 12, 4);
+    std::memcpy(&L, data.data() + 16, sizeof(L));
+    if (version != 1 || header_bytes != kHeader)
+        return fail(ctx, RVCP_E_INVALID, "unsupported scene file version");
+    const uint64_t need = kHeader + 32ull * L.materials_len + 32ull * L.spheres_len +
+                          32ull * L.vertices_len + 16ull * L.faces_len +
+                          4ull * L.luminous_sphere_id_len + 4ull * L.luminous_face_id_len;
+    if (need != data.size())
+        return fail(ctx, RVCP_E_INVALID, "scene file size does not match its lengths");
+    // copy each array into storage of its own type (the byte buffer has no alignment promise)
+    size_t off = kHeader;
+    auto take = [&](auto &vec, uint32_t n) {
+        vec.resize(n);
+        if (n) std::memcpy(vec.data(), data.data() + off, n * sizeof(vec[0]));
+        off += (size_t)n * sizeof(vec[0]);
+    };
+    std::vector<rvcp_material_t> mats;
+    std::vector<rvcp_sphere_t> sph;
+    std::vector<rvcp_vertex_t> verts;
+    std::vector<rvcp_face_t> faces;
+    std::vector<uint32_t> lsph, lface;
+    take(mats, L.materials_len);
+    take(sph, L.spheres_len);
+    take(verts, L.vertices_len);
+    take(faces, L.faces_len);
+    take(lsph, L.luminous_sphere_id_len);
+    take(lface, L.luminous_face_id_len);
+    const int rc = rvcp_upload_scene(ctx, mats.data(), L.materials_len, verts.data(),
+                                     L.vertices_len, faces.data(), L.faces_len, sph.data(),
+                                     L.spheres_len, lface.data(), L.luminous_face_id_len,
+                                     lsph.data(), L.luminous_sphere_id_len);
+    if (rc == RVCP_OK && out_camera) std::memcpy(out_camera, data.data() + 40, sizeof(*out_camera));
+    return rc;
+}
+
 uint32_t rvcp_shard_rows(uint32_t height, uint32_t shard_index, uint32_t shard_count)
 {
     if (shard_count == 0 || shard_index >= shard_count) return 0;

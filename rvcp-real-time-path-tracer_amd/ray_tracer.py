@@ -19,8 +19,8 @@ from typing import Optional
 
 import numpy as np
 
-from . import abi
-from .scene import PUSH_DTYPE, Scene, push_constant
+from . import abi, scene_io
+from .scene import CAMERA_DTYPE, PUSH_DTYPE, Scene, push_constant
 
 
 class RayTracer:
@@ -87,6 +87,14 @@ class RayTracer:
                            scene.mesh.aligned_faces(), scene.luminous_face_ids(),
                            scene.aligned_spheres(), scene.luminous_sphere_ids())
         self.scene = scene
+
+    def upload_scene_file(self, path: str) -> np.ndarray:
+        """Upload a binary scene file natively (rvcp_upload_scene_file); returns the stored
+        AlignedCamera record and keeps the Python-side Scene for render()."""
+        cam = np.zeros((), dtype=CAMERA_DTYPE)
+        self._check(self._lib.rvcp_upload_scene_file(self._ctx, str(path).encode(), abi.ptr(cam)))
+        self.scene = scene_io.load(path)
+        return cam
 
     # ------------------------------------------------------------------ render
     def render_push(self, push: np.ndarray, width: int, height: int, want_linear: bool = False):
