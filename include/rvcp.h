@@ -81,6 +81,13 @@ typedef struct rvcp_sphere {
     uint32_t _padding[3];
 } rvcp_sphere_t;
 
+/* == CameraData push constant of the Mandelbrot operator, src/mandelbrot/shader.rs:9-12 /
+ *    assets/shaders/mandelbrot.comp:5-8 (vec2 position @0, float scale @8; 12 B). */
+typedef struct rvcp_mandelbrot_push {
+    float position[2];
+    float scale;
+} rvcp_mandelbrot_push_t;
+
 /* == the 6 x u32 LengthBuffer, vulkan.rs:481-500 / ray_tracer_games101_branch.comp:58-65. */
 typedef struct rvcp_lengths {
     uint32_t materials_len;
@@ -168,6 +175,7 @@ RVCP_STATIC_ASSERT(offsetof(rvcp_vertex_t, normal) == 16, "Vertex.normal @16");
 RVCP_STATIC_ASSERT(sizeof(rvcp_face_t) == 16, "AlignedFace is 16 B");
 RVCP_STATIC_ASSERT(sizeof(rvcp_sphere_t) == 32, "AlignedSphere is 32 B");
 RVCP_STATIC_ASSERT(sizeof(rvcp_lengths_t) == 24, "LengthBuffer is 24 B");
+RVCP_STATIC_ASSERT(sizeof(rvcp_mandelbrot_push_t) == 12, "Mandelbrot CameraData is 12 B");
 
 typedef struct rvcp_ctx rvcp_ctx_t;
 
@@ -240,6 +248,15 @@ int rvcp_upload_scene_file(rvcp_ctx_t *ctx, const char *path, rvcp_camera_t *out
 int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
                 uint32_t width, uint32_t height,
                 uint8_t *out_rgba8, float *out_linear_rgb, rvcp_stats_t *stats);
+
+/* The reference's second compute operator, assets/shaders/mandelbrot.comp (dispatched by
+ * src/mandelbrot/vulkan.rs:380-400 with CameraData {position, scale}; defaults [0, 0] and 1.0,
+ * src/mandelbrot/config.rs:11-12).  Writes the W x H grey RGBA8 frame (escape time i,
+ * UNORM8, alpha 255) and optionally the float i per pixel.  Synchronous, like rvcp_render;
+ * needs no scene.  stats (optional) gets kernel_ms only. */
+int rvcp_mandelbrot(rvcp_ctx_t *ctx, const rvcp_mandelbrot_push_t *push,
+                    uint32_t width, uint32_t height,
+                    uint8_t *out_rgba8, float *out_value, rvcp_stats_t *stats);
 
 /* Asynchronous shard render into device memory, for multi-GPU frame assembly.
  * The frame is cut into 8-row stripes (the reference's 8x8 workgroup rows); stripe s is

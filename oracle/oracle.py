@@ -50,6 +50,8 @@ def lib():
         L.rvcp_oracle_unorm_u8.argtypes = [ctypes.c_float]
         L.rvcp_oracle_unorm_u8.restype = ctypes.c_uint8
         L.rvcp_oracle_render.restype = ctypes.c_int
+        L.rvcp_oracle_mandelbrot.argtypes = [P, u32, u32, P, P]
+        L.rvcp_oracle_mandelbrot.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -118,3 +120,15 @@ def render(scene_arrays: dict, push, cfg, W, H, rect=None, threads=None, want_li
     if rc != 0:
         raise ValueError(f"rvcp_oracle_render failed: {rc}")
     return lin, rgba, int(trav[0])
+
+
+def mandelbrot(push, W, H):
+    """The Mandelbrot operator (mandelbrot.comp): returns (rgba [H,W,4] u8, i [H,W] f32).
+    push: a MANDELBROT_PUSH_DTYPE record (position[2], scale)."""
+    push = np.ascontiguousarray(push)
+    rgba = np.zeros((H, W, 4), dtype=np.uint8)
+    val = np.zeros((H, W), dtype=np.float32)
+    rc = lib().rvcp_oracle_mandelbrot(_ptr(push), W, H, _ptr(rgba), _ptr(val))
+    if rc != 0:
+        raise ValueError(f"rvcp_oracle_mandelbrot failed: {rc}")
+    return rgba, val

@@ -651,6 +651,44 @@ int rvcp_oracle_render(const rvcp_material_t *materials, uint32_t n_materials,
 }
 
 /* ------------------------------------------------------------------------------------- */
+/* The Mandelbrot operator, assets/shaders/mandelbrot.comp:12-33 (single-threaded).       */
+/* out_rgba: W*H*4 grey UNORM8 of the escape time i; out_value (optional): i per pixel.    */
+/* ------------------------------------------------------------------------------------- */
+int rvcp_oracle_mandelbrot(const rvcp_mandelbrot_push_t *push, uint32_t W, uint32_t H,
+                           uint8_t *out_rgba, float *out_value)
+{
+    if (!push || !out_rgba || !W || !H) return RVCP_E_INVALID;
+    pthread_once(&g_unorm_once, unorm_init);
+    for (uint32_t y = 0; y < H; y++) {
+        for (uint32_t x = 0; x < W; x++) {
+            float nx = ((float)x + 0.5f) / (float)W;                  /* :13 */
+            float ny = ((float)y + 0.5f) / (float)H;
+            float cx = (nx - 0.5f) * 2.0f, cy = (ny - 0.5f) * 2.0f;   /* :15 */
+            cx = cx / push->scale + push->position[0];                /* :16 */
+            cy = cy / push->scale + push->position[1];
+            cx = cx - 1.0f;                                           /* :17 */
+            cy = cy - 0.0f;
+            float zx = 0.0f, zy = 0.0f, i;
+            for (i = 0.0f; i < 1.0f; i += 0.005f) {                    /* :21 */
+                float nzx = zx * zx - zy * zy + cx;
+                float nzy = zy * zx + zx * zy + cy;
+                zx = nzx;
+                zy = nzy;
+                if (sqrtf(zx * zx + zy * zy) > 4.0f) break;          /* length(z) > 4 */
+            }
+            const size_t p = (size_t)y * W + x;
+            const uint8_t u = rvcp_oracle_unorm_u8(i);                /* vec4(vec3(i), 1) */
+            out_rgba[4 * p + 0] = u;
+            out_rgba[4 * p + 1] = u;
+            out_rgba[4 * p + 2] = u;
+            out_rgba[4 * p + 3] = 255;
+            if (out_value) out_value[p] = i;
+        }
+    }
+    return RVCP_OK;
+}
+
+/* ------------------------------------------------------------------------------------- */
 /* Known-answer-test helpers (tests/test_oracle_kat.py)                                    */
 /* ------------------------------------------------------------------------------------- */
 

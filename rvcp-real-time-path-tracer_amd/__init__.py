@@ -11,7 +11,8 @@ from .ray_tracer import RayTracer, shard_row_ids, shard_rows
 from . import frame
 from . import interactive
 from . import scene_io
+from . import mandelbrot
 
-__all__ = ["abi", "scene", "frame", "interactive", "scene_io", "Camera", "Face", "Material", "MaterialType", "Mesh", "Scene",
+__all__ = ["abi", "scene", "frame", "interactive", "scene_io", "mandelbrot", "Camera", "Face", "Material", "MaterialType", "Mesh", "Scene",
            "Sphere", "Vertex", "cornell_box", "push_constant", "RayTracer", "shard_rows",
            "shard_row_ids"]

@@ -605,6 +605,48 @@ int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t widt
     return RVCP_OK;
 }
 
+int rvcp_mandelbrot(rvcp_ctx_t *ctx, const rvcp_mandelbrot_push_t *push, uint32_t width,
+                    uint32_t height, uint8_t *out_rgba8, float *out_value, rvcp_stats_t *stats)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!push || !out_rgba8 || width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 31))
+        return fail(ctx, RVCP_E_INVALID, "invalid mandelbrot arguments");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t npx = (size_t)width * height;
+    if (ctx->cap_rgba < npx) {
+        (void)hipFree(ctx->d_rgba);
+        ctx->d_rgba = nullptr;
+        ctx->cap_rgba = 0;
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_rgba, npx * 4));
+        ctx->cap_rgba = npx;
+    }
+    // the float escape values reuse the linear-RGB staging buffer (npx floats <= 3 npx)
+    if (out_value && ctx->cap_lin < npx) {
+        (void)hipFree(ctx->d_lin);
+        ctx->d_lin = nullptr;
+        ctx->cap_lin = 0;
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_lin, npx * 12));
+        ctx->cap_lin = npx;
+    }
+    HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    if (rvcp_launch_mandelbrot(push->position[0], push->position[1], push->scale, width, height,
+                               ctx->d_unorm, ctx->d_rgba, out_value ? ctx->d_lin : nullptr,
+                               ctx->stream) != 0)
+        return fail(ctx, RVCP_E_HIP, "mandelbrot launch failed");
+    HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ev1));
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        float ms = 0.0f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        stats->kernel_ms = ms;
+        stats->main_kernel_ms = ms;
+    }
+    HIP_TRY(ctx, hipMemcpy(out_rgba8, ctx->d_rgba, npx * 4, hipMemcpyDeviceToHost));
+    if (out_value) HIP_TRY(ctx, hipMemcpy(out_value, ctx->d_lin, npx * 4, hipMemcpyDeviceToHost));
+    return RVCP_OK;
+}
+
 int rvcp_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t slot_rows,
                               uint32_t width, uint32_t height, uint32_t shard_count,
                               void *d_frame, void *stream)

@@ -128,6 +128,10 @@ int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
                        const float *unorm_t, uint32_t *out_rgba, float *out_lin,
                        unsigned long long *counters, uint32_t grid_blocks, void *stream);
 int rvcp_legacy_occupancy(int *blocks_per_cu);
+// mandelbrot.comp (rvcp_mandelbrot.hip)
+int rvcp_launch_mandelbrot(float pos_x, float pos_y, float scale, uint32_t width,
+                           uint32_t height, const float *unorm_t, uint32_t *out_rgba,
+                           float *out_value, void *stream);
 int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows, uint32_t width,
                          uint32_t height, uint32_t shard_count, uint32_t *frame, void *stream);
 int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n_pixels, uint32_t rgba,

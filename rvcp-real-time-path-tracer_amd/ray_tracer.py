@@ -126,6 +126,18 @@ class RayTracer:
             self.fps_last_time = now
         return img
 
+    def mandelbrot(self, push: np.ndarray, width: int, height: int, want_value: bool = False):
+        """The Mandelbrot operator (rvcp_mandelbrot): grey RGBA8 frame [, escape values]."""
+        from .mandelbrot import MANDELBROT_PUSH_DTYPE
+        push = np.ascontiguousarray(push, dtype=MANDELBROT_PUSH_DTYPE)
+        rgba = np.empty((height, width, 4), dtype=np.uint8)
+        val = np.empty((height, width), dtype=np.float32) if want_value else None
+        stats = np.zeros((), dtype=abi.STATS_DTYPE)
+        self._check(self._lib.rvcp_mandelbrot(self._ctx, abi.ptr(push), width, height,
+                                              abi.ptr(rgba), abi.ptr(val), abi.ptr(stats)))
+        self.last_stats = stats
+        return (rgba, val) if want_value else rgba
+
     # ------------------------------------------------------------------ device-side API
     def render_shard_async(self, push, width, height, shard_index, shard_count, d_rgba: int,
                            d_linear: int = 0, stream: int = 0):

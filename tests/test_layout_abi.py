@@ -35,6 +35,7 @@ int main(void) {
   F(rvcp_stats_t, traversals_executed); F(rvcp_stats_t, samples); F(rvcp_stats_t, faces);
   F(rvcp_stats_t, wave_iterations); F(rvcp_stats_t, main_kernel_ms);
   S(rvcp_lengths_t);
+  S(rvcp_mandelbrot_push_t); F(rvcp_mandelbrot_push_t, position); F(rvcp_mandelbrot_push_t, scale);
   return 0;
 }
 """
@@ -42,7 +43,8 @@ int main(void) {
 DTYPES = {"rvcp_camera_t": scene.CAMERA_DTYPE, "rvcp_push_constant_t": scene.PUSH_DTYPE,
           "rvcp_material_t": scene.MATERIAL_DTYPE, "rvcp_vertex_t": scene.VERTEX_DTYPE,
           "rvcp_face_t": scene.FACE_DTYPE, "rvcp_sphere_t": scene.SPHERE_DTYPE,
-          "rvcp_config_t": abi.CONFIG_DTYPE, "rvcp_stats_t": abi.STATS_DTYPE}
+          "rvcp_config_t": abi.CONFIG_DTYPE, "rvcp_stats_t": abi.STATS_DTYPE,
+          "rvcp_mandelbrot_push_t": __import__("rvcp_amd").mandelbrot.MANDELBROT_PUSH_DTYPE}
 
 
 @pytest.fixture(scope="module")

@@ -33,7 +33,7 @@ for s in $STEPS; do
     case $s in
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
-        newtests) run pytest_new 600 python -m pytest tests/test_golden_frames.py tests/test_interactive.py tests/test_scene_io.py -m gpu -x -q ;;
+        newtests) run pytest_new 600 python -m pytest tests/test_golden_frames.py tests/test_interactive.py tests/test_scene_io.py tests/test_mandelbrot.py -m gpu -x -q ;;
         headless) run headless 300 python tools/headless.py --frames 120 --size 384 --spp 10 --dump gpurun_out/headless --format png --script walk ;;
         legacy) run pytest_legacy 600 python -m pytest tests/test_gpu_legacy.py -m gpu -x -q ;;
         lframes) run lframes 300 python tools/frames.py --integrator 1 --scene spheres --frames 5 --spp 5 ;;
