@@ -55,6 +55,10 @@ struct rvcp_ctx {
     float *d_lin = nullptr;
     size_t cap_rgba = 0, cap_lin = 0;
 
+    // RVCP_DEBUG_TIMELINE=<file>: per-wave timeline of the path kernel appended per render
+    unsigned long long *d_timeline = nullptr;
+    size_t cap_timeline = 0, last_timeline_waves = 0;
+
     // last launch
     bool pending = false;
     bool last_trivial = false;
@@ -272,6 +276,7 @@ int rvcp_destroy(rvcp_ctx_t *ctx)
     (void)hipFree(ctx->d_rgba);
     (void)hipFree(ctx->d_lin);
     (void)hipFree(ctx->d_surf);
+    (void)hipFree(ctx->d_timeline);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->evm) (void)hipEventDestroy(ctx->evm);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -509,6 +514,30 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
             if (blocks > cap) blocks = cap;
             if (blocks == 0) blocks = 1;
             A.static_chunks = blocks * (kBlock / kWave) * kChunk;
+            A.dyn_chunk = kDynChunk;
+            A.chunk_min = kMinChunk;
+            A.chunk_window = kChunkWindow;
+            if (const char *c = std::getenv("RVCP_DEBUG_CHUNK")) {   // fixed grab (experiments)
+                const int v = std::atoi(c);
+                if (v >= 1 && v <= 4096) A.dyn_chunk = A.chunk_min = (uint32_t)v;
+            }
+            if (const char *c = std::getenv("RVCP_DEBUG_CHUNK_WINDOW")) {
+                const int v = std::atoi(c);
+                if (v >= 1) A.chunk_window = (uint32_t)v;
+            }
+            ctx->last_timeline_waves = 0;
+            if (std::getenv("RVCP_DEBUG_TIMELINE") && !legacy && A.variant >= 3) {
+                const size_t waves = (size_t)blocks * (kBlock / kWave);
+                if (ctx->cap_timeline < waves) {
+                    (void)hipFree(ctx->d_timeline);
+                    ctx->d_timeline = nullptr;
+                    ctx->cap_timeline = 0;
+                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_timeline, waves * 32));
+                    ctx->cap_timeline = waves;
+                }
+                A.timeline = ctx->d_timeline;
+                ctx->last_timeline_waves = waves;
+            }
             if (legacy) {
                 HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_legacy(&A, ctx->d_tri, ctx->d_shade, ctx->d_spheres,
@@ -569,6 +598,15 @@ int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         stats->samples = ctx->last_pixels * ctx->last_spp;
         stats->faces = ctx->n_faces;
         stats->wave_iterations = c[2];
+    }
+    if (ctx->last_timeline_waves) {
+        std::vector<unsigned long long> t(4 * ctx->last_timeline_waves);
+        HIP_TRY(ctx, hipMemcpy(t.data(), ctx->d_timeline, t.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE *f = std::fopen(std::getenv("RVCP_DEBUG_TIMELINE"), "ab")) {
+            std::fwrite(t.data(), 8, t.size(), f);
+            std::fclose(f);
+        }
+        ctx->last_timeline_waves = 0;
     }
     return RVCP_OK;
 }

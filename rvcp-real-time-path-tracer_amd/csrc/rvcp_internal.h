@@ -12,6 +12,12 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 // Pixels a wave takes from the frame queue per atomic.
 constexpr uint32_t kChunk = 64;
+// Frame-queue grabs after a wave's static chunk: what the wave consumes in kChunkWindow
+// s_memrealtime ticks (100 MHz), between kMinChunk and kDynChunk pixels (queue_take,
+// DESIGN.md §4.1).
+constexpr uint32_t kDynChunk = 64;
+constexpr uint32_t kMinChunk = 2;
+constexpr uint32_t kChunkWindow = 10000;    // 100 us
 // Kernel schedules (rvcp_config_t::kernel_variant): 1 = one ray per lane per iteration,
 // 2 = shadow + continuation ray per lane per iteration, 3 = primary pre-pass kernel + the
 // variant-2 loop over surface pixels only.
@@ -104,6 +110,12 @@ struct FrameArgs {
     uint32_t want_linear;
     int32_t variant;         // kernel schedule (rvcp_config_t::kernel_variant, resolved)
     uint32_t n_spheres;      // integrator RVCP_INTEGRATOR_LEGACY only
+    uint32_t dyn_chunk;      // largest frame-queue grab after the static chunk
+    uint32_t chunk_min;      // smallest grab
+    uint32_t chunk_window;   // grab = pixels this wave consumes in chunk_window ticks (10 ns)
+    // debug (RVCP_DEBUG_TIMELINE): per-wave {start, queue exhausted, end, iterations}
+    // of the path kernel, s_memrealtime ticks (100 MHz); nullptr otherwise
+    unsigned long long *timeline;
 };
 
 }  // namespace rvcp

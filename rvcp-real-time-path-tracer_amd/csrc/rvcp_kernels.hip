@@ -339,9 +339,12 @@ __device__ __forceinline__ bool att_stop(const FrameArgs &A, f3 att) {          
 }
 
 
-// Wave-uniform frame-queue state: [next, end) pixels owned by this wave.
+// Wave-uniform frame-queue state: [next, end) pixels owned by this wave; the pixels it has
+// handed to its lanes since t0 (s_memrealtime ticks) set the size of its next grab.
 struct Queue {
     uint32_t next, end;
+    uint32_t taken;
+    uint64_t t0;
     bool exhausted;
 };
 
@@ -353,12 +356,21 @@ __device__ __forceinline__ Queue queue_init(const FrameArgs &A) {
     q.end = q.next + kChunk;
     if (q.next > A.n_pixels) q.next = A.n_pixels;
     if (q.end > A.n_pixels) q.end = A.n_pixels;
+    q.taken = 0;
+    q.t0 = __builtin_amdgcn_s_memrealtime();
     q.exhausted = false;
     return q;
 }
 
 // Hand pixels to the lanes in `need` (must be called in wave-uniform control flow).  Lanes
 // that receive one get got=true and their pixel index.
+//
+// Grab size: pixels a wave grabs but has not yet handed out wait for ITS lanes to free up
+// (a pixel is a serial chain of SPP samples), so when the queue runs dry a large grab strands
+// up to a grab's worth of work behind busy lanes while other waves idle.  Each wave therefore
+// grabs what it consumes in a short window: chunk = clamp(rate x chunk_window, chunk_min,
+// dyn_chunk), rate = pixels it handed out / time since its start.  Expensive pixels (C3: ~4)
+// keep the stranded tail short; cheap ones (mode 2: 64) keep the head atomic uncontended.
 __device__ __forceinline__ void queue_take(Queue &q, uint64_t need, uint32_t lane,
                                            const FrameArgs &A,
                                            unsigned long long *__restrict__ counters,
@@ -368,12 +380,16 @@ __device__ __forceinline__ void queue_take(Queue &q, uint64_t need, uint32_t lan
         if (q.next >= q.end) {
             if (q.exhausted) break;
             const int leader = (int)__builtin_ctzll(need);
+            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - q.t0 + 1ull;
+            const uint64_t want = (uint64_t)q.taken * A.chunk_window / dt;
+            uint32_t c = want > A.dyn_chunk ? A.dyn_chunk : (uint32_t)want;
+            c = __builtin_amdgcn_readfirstlane(c < A.chunk_min ? A.chunk_min : c);
             uint32_t base = 0;
-            if (lane == (uint32_t)leader) base = atomicAdd((unsigned int *)&counters[1], kChunk);
+            if (lane == (uint32_t)leader) base = atomicAdd((unsigned int *)&counters[1], c);
             base = __builtin_amdgcn_readfirstlane(__shfl(base, leader)) + A.static_chunks;
             if (base >= A.n_pixels) { q.exhausted = true; break; }
             q.next = base;
-            q.end = base + kChunk < A.n_pixels ? base + kChunk : A.n_pixels;
+            q.end = base + c < A.n_pixels ? base + c : A.n_pixels;
         }
         const uint32_t avail = q.end - q.next;
         const uint32_t r = rank_in(need);
@@ -381,6 +397,7 @@ __device__ __forceinline__ void queue_take(Queue &q, uint64_t need, uint32_t lan
         const uint64_t given = __ballot(mine);
         if (mine) { pix = q.next + r; got = true; }
         q.next += __builtin_popcountll(given);
+        q.taken += __builtin_popcountll(given);
         need &= ~given;
     }
 }
@@ -810,6 +827,8 @@ __device__ __forceinline__ void path_body(
     const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile)
 {
     const uint32_t lane = lane_id();
+    const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long t_exhausted = 0ull;
     // the queue runs over the pre-pass's compact list; its length is in counters[3]
     FrameArgs Q = A;
     Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
@@ -909,6 +928,7 @@ __device__ __forceinline__ void path_body(
         }
         if (wave_active) iters += 1;
         trav += (hasA ? 1u : 0u) + (hasB ? 1u : 0u);
+        if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
 
         int bestA = -1, bestB = -1;
         float btA = A.t_max, btB = A.t_max;
@@ -1067,6 +1087,14 @@ __device__ __forceinline__ void path_body(
         hasB = false;
     }
     flush_counters(counters, lane, trav, iters);
+    if (A.timeline && lane == 0) {
+        const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;
+        unsigned long long *rec = A.timeline + 4ull * w;
+        rec[0] = t_start;
+        rec[1] = t_exhausted;
+        rec[2] = __builtin_amdgcn_s_memrealtime();
+        rec[3] = iters;
+    }
 }
 
 __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_kernel(

@@ -35,6 +35,10 @@ for s in $STEPS; do
         tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
         newtests) run pytest_new 600 python -m pytest tests/test_golden_frames.py tests/test_interactive.py tests/test_scene_io.py tests/test_mandelbrot.py -m gpu -x -q ;;
         headless) run headless 300 python tools/headless.py --frames 120 --size 384 --spp 10 --dump gpurun_out/headless --format png --script walk ;;
+        timeline) run timeline 300 bash -c "rm -f /tmp/tl.bin && RVCP_DEBUG_TIMELINE=/tmp/tl.bin python tools/frames.py --frames 3 && python tools/timeline.py /tmp/tl.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl.bin\")//96)')" ;;
+        timeline5) run timeline5 300 bash -c "rm -f /tmp/tl5.bin && RVCP_DEBUG_TIMELINE=/tmp/tl5.bin python tools/frames.py --variant 5 --frames 3 && python tools/timeline.py /tmp/tl5.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl5.bin\")//96)')" ;;
+        chunks) run chunks 500 bash -c "for w in 10000 3000 30000; do echo c3 window=\$w; RVCP_DEBUG_CHUNK_WINDOW=\$w python tools/frames.py --variant 3 --frames 10 || exit 1; done; echo c3 fixed4; RVCP_DEBUG_CHUNK=4 python tools/frames.py --variant 3 --frames 10 || exit 1; for w in 10000 3000; do echo c2 window=\$w; RVCP_DEBUG_CHUNK_WINDOW=\$w python tools/frames.py --variant 3 --frames 10 --size 384 --spp 10 || exit 1; done; for w in 10000 3000 30000; do echo sph window=\$w; RVCP_DEBUG_CHUNK_WINDOW=\$w python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; done; echo sph fixed64; RVCP_DEBUG_CHUNK=64 python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; echo c5small; python tools/frames.py --frames 2 --tris 100000 --size 256 --spp 2" ;;
+        v35) run v35 300 bash -c "python tools/frames.py --variant 3 --frames 6 && python tools/frames.py --variant 5 --frames 6 && python tools/frames.py --variant 3 --frames 6 --size 384 --spp 10 && python tools/frames.py --variant 5 --frames 6 --size 384 --spp 10" ;;
         legacy) run pytest_legacy 600 python -m pytest tests/test_gpu_legacy.py -m gpu -x -q ;;
         lframes) run lframes 300 python tools/frames.py --integrator 1 --scene spheres --frames 5 --spp 5 ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
