@@ -29,6 +29,7 @@ struct rvcp_ctx {
     hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;   // start, main kernel, end
     int grid_capacity[kMaxVariant + 1] = {};   // resident workgroups per kernel variant
     int legacy_capacity = 0;                   // ... of the RVCP_INTEGRATOR_LEGACY kernel
+    uint32_t n_simds = 1024;
 
     // scene (device)
     TriRecord *d_tri = nullptr;
@@ -248,6 +249,7 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     // RVCP_DEBUG_BLOCKS_PER_CU caps the persistent grid (occupancy experiments only)
     const char *cap_env = std::getenv("RVCP_DEBUG_BLOCKS_PER_CU");
     const int cap = cap_env ? std::atoi(cap_env) : 0;
+    ctx->n_simds = (uint32_t)cus * 4u;
     for (int v = 1; v <= kMaxVariant; v++) {
         int per_cu = 0;
         if (rvcp_games101_occupancy(v, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
@@ -507,13 +509,16 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
             rc = rvcp_launch_fill((uint32_t *)d_rgba8, (float *)d_linear_rgb, A.n_pixels,
                                   0xFF000000u, s);
         } else {
-            const uint32_t waves_needed = (A.n_pixels + kChunk - 1) / kChunk;
-            uint32_t blocks = (waves_needed + (kBlock / kWave) - 1) / (kBlock / kWave);
             const uint32_t cap = (uint32_t)(legacy ? ctx->legacy_capacity
                                                    : ctx->grid_capacity[A.variant]);
+            A.n_simds = ctx->n_simds;
+            uint32_t waves = 0, chunk = 0;
+            rvcp_static_split(A.n_pixels, cap * (kBlock / kWave), A.n_simds, &waves, &chunk);
+            uint32_t blocks = (waves + (kBlock / kWave) - 1) / (kBlock / kWave);
             if (blocks > cap) blocks = cap;
             if (blocks == 0) blocks = 1;
-            A.static_chunks = blocks * (kBlock / kWave) * kChunk;
+            A.static_chunk = chunk;
+            A.static_chunks = waves * chunk;
             A.dyn_chunk = kDynChunk;
             A.chunk_min = kMinChunk;
             A.chunk_window = kChunkWindow;

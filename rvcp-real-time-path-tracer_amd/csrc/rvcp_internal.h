@@ -12,6 +12,9 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 // Pixels a wave takes from the frame queue per atomic.
 constexpr uint32_t kChunk = 64;
+// Small frames: the grid is sized so that a wave starts with at least kMinStatic pixels, and
+// the pixels are spread over all those waves (more waves per SIMD to hide latency).
+constexpr uint32_t kMinStatic = 8;
 // Frame-queue grabs after a wave's static chunk: what the wave consumes in kChunkWindow
 // s_memrealtime ticks (100 MHz), between kMinChunk and kDynChunk pixels (queue_take,
 // DESIGN.md §4.1).
@@ -107,6 +110,8 @@ struct FrameArgs {
     uint32_t n_faces, n_lights;
     float light_total, light_pdf;
     uint32_t static_chunks;  // pixels handed out statically (one chunk per wave)
+    uint32_t static_chunk;   // pixels of each wave's static chunk (<= kChunk)
+    uint32_t n_simds;        // SIMDs of the device (CUs x 4), for static_split
     uint32_t want_linear;
     int32_t variant;         // kernel schedule (rvcp_config_t::kernel_variant, resolved)
     uint32_t n_spheres;      // integrator RVCP_INTEGRATOR_LEGACY only
@@ -149,4 +154,6 @@ int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows, uint32_t 
 int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n_pixels, uint32_t rgba,
                      void *stream);
 int rvcp_games101_occupancy(int variant, int *blocks_per_cu);
+void rvcp_static_split(uint32_t n, uint32_t grid_waves, uint32_t n_simds, uint32_t *waves,
+                       uint32_t *chunk);
 }

@@ -339,6 +339,22 @@ __device__ __forceinline__ bool att_stop(const FrameArgs &A, f3 att) {          
 }
 
 
+// Static chunks: full 64-pixel waves (fewest wave-instructions for the work) unless that
+// leaves fewer than two waves per SIMD, in which case the pixels are spread over up to two
+// waves per SIMD, at least kMinStatic each (latency hiding matters more for tiny frames).  Returns the waves that get a static chunk and its size.
+__host__ __device__ inline void static_split(uint32_t n, uint32_t grid_waves, uint32_t n_simds,
+                                             uint32_t &waves, uint32_t &chunk) {
+    uint32_t w = (n + kChunk - 1) / kChunk;
+    const uint32_t spread = (n + kMinStatic - 1) / kMinStatic;
+    const uint32_t floor_w = spread < 2u * n_simds ? spread : 2u * n_simds;
+    if (w < floor_w) w = floor_w;
+    if (w > grid_waves) w = grid_waves;
+    if (w < 1u) w = 1u;
+    uint32_t c = (n + w - 1) / w;
+    chunk = c < 1u ? 1u : (c > kChunk ? kChunk : c);
+    waves = w;
+}
+
 // Wave-uniform frame-queue state: [next, end) pixels owned by this wave; the pixels it has
 // handed to its lanes since t0 (s_memrealtime ticks) set the size of its next grab.
 struct Queue {
@@ -352,8 +368,8 @@ __device__ __forceinline__ Queue queue_init(const FrameArgs &A) {
     const uint32_t wave_global =
         __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) / kWave);
     Queue q;
-    q.next = wave_global * kChunk;
-    q.end = q.next + kChunk;
+    q.next = wave_global * A.static_chunk;
+    q.end = q.next + A.static_chunk;
     if (q.next > A.n_pixels) q.next = A.n_pixels;
     if (q.end > A.n_pixels) q.end = A.n_pixels;
     q.taken = 0;
@@ -832,6 +848,12 @@ __device__ __forceinline__ void path_body(
     // the queue runs over the pre-pass's compact list; its length is in counters[3]
     FrameArgs Q = A;
     Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
+    {   // static chunks over the surface list, same rule as the host's (static_split)
+        uint32_t waves, c;
+        static_split(Q.n_pixels, gridDim.x * (kBlock / kWave), A.n_simds, waves, c);
+        Q.static_chunk = c;
+        Q.static_chunks = c * waves;
+    }
     Queue q = queue_init(Q);
     const float sppf = (float)A.spp;
 
@@ -1444,6 +1466,12 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                        *args, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
                        shade);
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" void rvcp_static_split(uint32_t n, uint32_t grid_waves, uint32_t n_simds,
+                                  uint32_t *waves, uint32_t *chunk)
+{
+    rvcp::static_split(n, grid_waves, n_simds, *waves, *chunk);
 }
 
 extern "C" int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows, uint32_t width,

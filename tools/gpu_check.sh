@@ -37,7 +37,7 @@ for s in $STEPS; do
         headless) run headless 300 python tools/headless.py --frames 120 --size 384 --spp 10 --dump gpurun_out/headless --format png --script walk ;;
         timeline) run timeline 300 bash -c "rm -f /tmp/tl.bin && RVCP_DEBUG_TIMELINE=/tmp/tl.bin python tools/frames.py --frames 3 && python tools/timeline.py /tmp/tl.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl.bin\")//96)')" ;;
         timeline5) run timeline5 300 bash -c "rm -f /tmp/tl5.bin && RVCP_DEBUG_TIMELINE=/tmp/tl5.bin python tools/frames.py --variant 5 --frames 3 && python tools/timeline.py /tmp/tl5.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl5.bin\")//96)')" ;;
-        chunks) run chunks 500 bash -c "for w in 10000 3000 30000; do echo c3 window=\$w; RVCP_DEBUG_CHUNK_WINDOW=\$w python tools/frames.py --variant 3 --frames 10 || exit 1; done; echo c3 fixed4; RVCP_DEBUG_CHUNK=4 python tools/frames.py --variant 3 --frames 10 || exit 1; for w in 10000 3000; do echo c2 window=\$w; RVCP_DEBUG_CHUNK_WINDOW=\$w python tools/frames.py --variant 3 --frames 10 --size 384 --spp 10 || exit 1; done; for w in 10000 3000 30000; do echo sph window=\$w; RVCP_DEBUG_CHUNK_WINDOW=\$w python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; done; echo sph fixed64; RVCP_DEBUG_CHUNK=64 python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; echo c5small; python tools/frames.py --frames 2 --tris 100000 --size 256 --spp 2" ;;
+        chunks) run chunks 500 bash -c "echo c3; python tools/frames.py --frames 10 || exit 1; echo c2; python tools/frames.py --frames 10 --size 384 --spp 10 || exit 1; echo sph; python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; echo small128; python tools/frames.py --frames 10 --size 128 --spp 30 || exit 1" ;;
         v35) run v35 300 bash -c "python tools/frames.py --variant 3 --frames 6 && python tools/frames.py --variant 5 --frames 6 && python tools/frames.py --variant 3 --frames 6 --size 384 --spp 10 && python tools/frames.py --variant 5 --frames 6 --size 384 --spp 10" ;;
         legacy) run pytest_legacy 600 python -m pytest tests/test_gpu_legacy.py -m gpu -x -q ;;
         lframes) run lframes 300 python tools/frames.py --integrator 1 --scene spheres --frames 5 --spp 5 ;;
@@ -53,8 +53,8 @@ for s in $STEPS; do
         c5cmp) run c5cmp 600 bash -c "python tools/frames.py --variant 4 --frames 2 --tris 100000 --size 512 --spp 4 && python tools/frames.py --variant 3 --frames 1 --tris 100000 --size 512 --spp 4" ;;
         split3) run split3 300 env RVCP_KERNEL_VARIANT=3 python tools/exp_split.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
-        sqpmc) run sqpmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 tools/frames.py --variant 2 --frames 2 ;;
-        sqpmc2) run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 tools/frames.py --variant 2 --frames 2 ;;
+        sqpmc) run sqpmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 tools/frames.py --frames 2 ;;
+        sqpmc2) run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 tools/frames.py --frames 2 ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
