@@ -999,9 +999,13 @@ __device__ __forceinline__ void path_body(
                         }
                     }
                 } else if (wave_active) {
+                    // software-pipelined: the next triangle's LDS read is in flight while
+                    // the current one is tested
+                    TriRecord Tn = tile[0];
 #pragma unroll 2
                     for (uint32_t i = 0; i < n; ++i) {
-                        const TriRecord T = tile[i];
+                        const TriRecord T = Tn;
+                        Tn = tile[i + 1 < n ? i + 1 : i];
                         float tA, tB;
                         if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
                         if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }

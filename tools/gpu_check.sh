@@ -38,6 +38,8 @@ for s in $STEPS; do
         timeline) run timeline 300 bash -c "rm -f /tmp/tl.bin && RVCP_DEBUG_TIMELINE=/tmp/tl.bin python tools/frames.py --frames 3 && python tools/timeline.py /tmp/tl.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl.bin\")//96)')" ;;
         timeline5) run timeline5 300 bash -c "rm -f /tmp/tl5.bin && RVCP_DEBUG_TIMELINE=/tmp/tl5.bin python tools/frames.py --variant 5 --frames 3 && python tools/timeline.py /tmp/tl5.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl5.bin\")//96)')" ;;
         chunks) run chunks 500 bash -c "echo c3; python tools/frames.py --frames 10 || exit 1; echo c2; python tools/frames.py --frames 10 --size 384 --spp 10 || exit 1; echo sph; python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; echo small128; python tools/frames.py --frames 10 --size 128 --spp 30 || exit 1" ;;
+        c5t) run c5t 400 bash -c "echo c5-512-v4; python tools/frames.py --variant 4 --frames 3 --tris 100000 --size 512 --spp 4 || exit 1; echo c5-512-v3; python tools/frames.py --variant 3 --frames 2 --tris 100000 --size 512 --spp 4" ;;
+        w5) run w5 300 bash -c "echo c3-default; python tools/frames.py --frames 10 || exit 1; echo c3-w5; RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/variants/librvcp_w5.so python tools/frames.py --frames 10 || exit 1; echo c2-w5; RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/variants/librvcp_w5.so python tools/frames.py --frames 10 --size 384 --spp 10" ;;
         v35) run v35 300 bash -c "python tools/frames.py --variant 3 --frames 6 && python tools/frames.py --variant 5 --frames 6 && python tools/frames.py --variant 3 --frames 6 --size 384 --spp 10 && python tools/frames.py --variant 5 --frames 6 --size 384 --spp 10" ;;
         legacy) run pytest_legacy 600 python -m pytest tests/test_gpu_legacy.py -m gpu -x -q ;;
         lframes) run lframes 300 python tools/frames.py --integrator 1 --scene spheres --frames 5 --spp 5 ;;
@@ -55,9 +57,12 @@ for s in $STEPS; do
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
         sqpmc) run sqpmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 tools/frames.py --frames 2 ;;
         sqpmc2) run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 tools/frames.py --frames 2 ;;
+        c5pmc) run c5pmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c5pmc_$TAG" -o run --output-format csv -- python3 tools/frames.py --frames 2 --tris 100000 --size 512 --spp 4 ;;
+        c5pmc2) run c5pmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d "$OUT/c5pmc2_$TAG" -o run --output-format csv -- python3 tools/frames.py --frames 2 --tris 100000 --size 512 --spp 4 ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+        benchc5) run bench_c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
         benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 ;;
         profs) run profs 600 rocprofv3 --kernel-trace --stats -d "$OUT/profs_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 20 --warmup 2 --no-cpu-baseline ;;
         pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
