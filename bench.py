@@ -130,6 +130,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--save-frame", default="")
+    ap.add_argument("--accel", default="none", choices=["none", "bvh"],
+                    help="bvh: the opt-in BVH (not the parity path; never the default line)")
     args = ap.parse_args()
 
     import torch
@@ -163,6 +165,8 @@ def main():
     cfg_kw = dict(spp=spp, device=local_rank)
     if legacy:
         cfg_kw["integrator"] = 1
+    if args.accel == "bvh":
+        cfg_kw["accel"] = 1
     rt = rvcp_amd.RayTracer(**cfg_kw)
     rt.upload_scene(sc)
     push = sc.push_constant(123.0)
@@ -236,8 +240,8 @@ def main():
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
     tests_per_s = units * (n_faces + n_spheres) / avg_kernel_s
     exec_tests_per_s = (trav_exec / args.steps - prepass) * (n_faces + n_spheres) / avg_kernel_s
-    kname = "legacy_kernel" if legacy else ("games101_tiled_kernel" if n_faces >= 4096
-                                             else "games101_path_kernel")
+    kname = ("legacy_kernel" if legacy else "games101_bvh_path_kernel" if args.accel == "bvh"
+             else "games101_tiled_kernel" if n_faces >= 4096 else "games101_path_kernel")
     traffic, traffic_src = load_traffic(wl["workload"], kname)
 
     frame_check = None
@@ -272,6 +276,7 @@ def main():
                      "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)"),
             "config": {"workload": wl["workload"], "width": W, "height": H, "spp": spp,
                        "faces": n_faces, "parallelism": f"pixel-stripes x{world}",
+                       "accel": args.accel,
                        "gather": ("gloo-rehearsal" if rehearsal else "rccl") if world > 1 else "none"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

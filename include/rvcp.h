@@ -114,6 +114,11 @@ enum {
     RVCP_INTEGRATOR_LEGACY = 1,
 };
 
+enum {
+    RVCP_ACCEL_NONE = 0,              /* brute-force scan, as the shader (parity) */
+    RVCP_ACCEL_BVH = 1,               /* opt-in BVH (README.md:28-32 TODO "BVH") */
+};
+
 typedef struct rvcp_config {
     int32_t device;                   /* HIP device ordinal */
     int32_t integrator;               /* RVCP_INTEGRATOR_* */
@@ -135,7 +140,14 @@ typedef struct rvcp_config {
      * the scan staged through LDS tiles shared by the workgroup.  Every schedule produces
      * bit-identical frames. */
     int32_t kernel_variant;
-    uint32_t _reserved[5];
+    /* Acceleration structure: RVCP_ACCEL_NONE (default) scans every triangle like the
+     * shader (bit-exact, the parity path).  RVCP_ACCEL_BVH (opt-in, games101 only) builds a
+     * bounding-volume hierarchy at upload and tests only the triangles whose (slightly
+     * enlarged) boxes the ray reaches, with the same exact triangle test and nearest-hit
+     * rule; frames match the brute-force ones except where a ray runs almost parallel to a
+     * triangle's plane. */
+    int32_t accel;
+    uint32_t _reserved[4];
 } rvcp_config_t;
 
 /* Per-render statistics (all optional). */

@@ -1,0 +1,198 @@
+// rvcp_bvh.cpp -- host-side builder of the opt-in BVH (rvcp_config_t.accel = RVCP_ACCEL_BVH).
+//
+// Binary tree, binned SAH (16 bins on centroids, along the widest centroid axis) down to
+// kBvhLeafMax triangles; below depth kSahDepth (or when SAH finds no useful split) the node is
+// split at the centroid median; the SAH depth is capped so that SAH levels + median levels
+// (ceil(log2(n / leaf)) + 1) stay below the device traversal stack (kBvhStack).  Triangles are stored in leaf order
+// (TriRecord copies) together with their original face index, which the device uses for the
+// scan's tie rule and the hit record.
+//
+// Box enlargement: every child box grows by 1e-5 of the scene diagonal plus 1e-6 of its own
+// largest coordinate magnitude.  An exact triangle test (tri_accept) that accepts a hit on a
+// well-conditioned ray (not nearly parallel to the triangle plane) puts the hit point within a
+// few ulps of the triangle, far inside that margin, so culling never drops a hit the
+// brute-force scan would find (DESIGN.md §4.6 for the nearly-parallel exception).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rvcp.h"
+#include "rvcp_internal.h"
+
+namespace rvcp {
+
+namespace {
+
+struct Box {
+    float lo[3] = {INFINITY, INFINITY, INFINITY};
+    float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const float *p) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], p[k]);
+            hi[k] = std::max(hi[k], p[k]);
+        }
+    }
+    void grow(const Box &b) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    float area() const {
+        if (!(hi[0] >= lo[0])) return 0.0f;
+        const float x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+        return 2.0f * (x * y + y * z + z * x);
+    }
+};
+
+struct Prim {
+    Box box;
+    float c[3];
+    uint32_t id;
+};
+
+constexpr int kBins = 16;
+constexpr int kSahDepthMax = 16;
+
+struct Builder {
+    std::vector<Prim> prims;
+    std::vector<BvhNode> nodes;
+    std::vector<uint32_t> order;
+    float pad_abs = 0.0f;
+    int max_depth = 0;
+    int sah_depth = kSahDepthMax;
+
+    void store_box(float *dst, const Box &b) const {
+        for (int k = 0; k < 3; k++) {
+            const float mag = std::max(std::fabs(b.lo[k]), std::fabs(b.hi[k]));
+            const float pad = pad_abs + 1e-6f * mag;
+            dst[k] = b.lo[k] - pad;
+            dst[3 + k] = b.hi[k] + pad;
+        }
+    }
+
+    int32_t leaf(uint32_t first, uint32_t count) {
+        const uint32_t start = (uint32_t)order.size();
+        for (uint32_t i = first; i < first + count; i++) order.push_back(prims[i].id);
+        return ~(int32_t)((start << 5) | (count - 1));
+    }
+
+    // Build [first, first + count) and return its reference.
+    int32_t build(uint32_t first, uint32_t count, int depth, Box *out_box) {
+        Box bounds, cbounds;
+        for (uint32_t i = first; i < first + count; i++) {
+            bounds.grow(prims[i].box);
+            cbounds.grow(prims[i].c);
+        }
+        *out_box = bounds;
+        max_depth = std::max(max_depth, depth);
+        if (count <= (uint32_t)kBvhLeafMax) return leaf(first, count);
+
+        int axis = 0;
+        for (int k = 1; k < 3; k++)
+            if (cbounds.hi[k] - cbounds.lo[k] > cbounds.hi[axis] - cbounds.lo[axis]) axis = k;
+        const float ext = cbounds.hi[axis] - cbounds.lo[axis];
+        uint32_t mid = first + count / 2;
+        bool sah_ok = false;
+        if (depth < sah_depth && ext > 0.0f) {
+            Box bb[kBins];
+            uint32_t bn[kBins] = {};
+            auto bin_of = [&](const Prim &p) {
+                int b = (int)((p.c[axis] - cbounds.lo[axis]) / ext * kBins);
+                return std::min(std::max(b, 0), kBins - 1);
+            };
+            for (uint32_t i = first; i < first + count; i++) {
+                const int b = bin_of(prims[i]);
+                bb[b].grow(prims[i].box);
+                bn[b]++;
+            }
+            float best = INFINITY;
+            int best_split = -1;
+            for (int s = 1; s < kBins; s++) {
+                Box l, r;
+                uint32_t nl = 0, nr = 0;
+                for (int b = 0; b < s; b++) { if (bn[b]) l.grow(bb[b]); nl += bn[b]; }
+                for (int b = s; b < kBins; b++) { if (bn[b]) r.grow(bb[b]); nr += bn[b]; }
+                if (!nl || !nr) continue;
+                const float cost = l.area() * nl + r.area() * nr;
+                if (cost < best) { best = cost; best_split = s; }
+            }
+            if (best_split > 0 && best < bounds.area() * count) {
+                auto it = std::partition(prims.begin() + first, prims.begin() + first + count,
+                                         [&](const Prim &p) { return bin_of(p) < best_split; });
+                mid = (uint32_t)(it - prims.begin());
+                sah_ok = mid > first && mid < first + count;
+            }
+        }
+        if (!sah_ok) {
+            std::nth_element(prims.begin() + first, prims.begin() + first + count / 2,
+                             prims.begin() + first + count,
+                             [&](const Prim &a, const Prim &b) {
+                                 return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.id < b.id);
+                             });
+            mid = first + count / 2;
+        }
+        const uint32_t self = (uint32_t)nodes.size();
+        nodes.emplace_back();
+        Box lb, rb;
+        const int32_t l = build(first, mid - first, depth + 1, &lb);
+        const int32_t r = build(mid, first + count - mid, depth + 1, &rb);
+        BvhNode &N = nodes[self];
+        store_box(N.lbox, lb);
+        store_box(N.rbox, rb);
+        N.left = l;
+        N.right = r;
+        N.pad[0] = N.pad[1] = 0;
+        return (int32_t)self;
+    }
+};
+
+}  // namespace
+
+// Build over `n` faces given their three vertex positions.  Outputs the node array, the
+// leaf-ordered original face ids and the root reference; returns the tree depth.
+int bvh_build(const float (*pos)[3][3], uint32_t n, std::vector<BvhNode> &nodes,
+              std::vector<uint32_t> &order, int32_t &root)
+{
+    Builder B;
+    B.prims.resize(n);
+    Box scene;
+    for (uint32_t i = 0; i < n; i++) {
+        Prim &p = B.prims[i];
+        bool finite = true;
+        for (int v = 0; v < 3; v++)
+            for (int k = 0; k < 3; k++) finite = finite && std::isfinite(pos[i][v][k]);
+        if (finite) {
+            for (int v = 0; v < 3; v++) p.box.grow(pos[i][v]);
+        } else {            // never accepted by the exact test (NaN/inf arithmetic): park it
+            const float z[3] = {0.0f, 0.0f, 0.0f};
+            p.box.grow(z);
+        }
+        for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
+        p.id = i;
+        scene.grow(p.box);
+    }
+    if (n == 0) {
+        nodes.clear();
+        order.clear();
+        root = 0;
+        return 0;
+    }
+    const float dx = scene.hi[0] - scene.lo[0], dy = scene.hi[1] - scene.lo[1],
+                dz = scene.hi[2] - scene.lo[2];
+    B.pad_abs = 1e-5f * std::sqrt(dx * dx + dy * dy + dz * dz);
+    int median_levels = 1;
+    for (uint64_t leaves = ((uint64_t)n + kBvhLeafMax - 1) / kBvhLeafMax; leaves > 1; leaves = (leaves + 1) / 2)
+        median_levels++;
+    B.sah_depth = std::max(0, std::min(kSahDepthMax, kBvhStack - 1 - median_levels));
+    B.nodes.reserve(2 * (size_t)n / kBvhLeafMax + 2);
+    B.order.reserve(n);
+    Box rootbox;
+    root = B.build(0, n, 0, &rootbox);
+    nodes.swap(B.nodes);
+    order.swap(B.order);
+    return B.max_depth;     // the caller rejects max_depth >= kBvhStack
+}
+
+}  // namespace rvcp

@@ -29,6 +29,7 @@ struct rvcp_ctx {
     hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;   // start, main kernel, end
     int grid_capacity[kMaxVariant + 1] = {};   // resident workgroups per kernel variant
     int legacy_capacity = 0;                   // ... of the RVCP_INTEGRATOR_LEGACY kernel
+    int bvh_capacity = 0;                      // ... of the RVCP_ACCEL_BVH path kernel
     uint32_t n_simds = 1024;
 
     // scene (device)
@@ -40,6 +41,12 @@ struct rvcp_ctx {
     LightRecord *d_lights = nullptr;
     rvcp_material_t *d_rawmats = nullptr;     // RVCP_INTEGRATOR_LEGACY: fuzz / ior needed
     rvcp_sphere_t *d_spheres = nullptr;
+    // opt-in BVH (RVCP_ACCEL_BVH): nodes, leaf-ordered triangles and their face ids
+    BvhNode *d_bvh_nodes = nullptr;
+    TriRecord *d_bvh_tris = nullptr;
+    uint32_t *d_bvh_ids = nullptr;
+    int32_t bvh_root = 0;
+    int bvh_depth = 0;
     float *d_gamma = nullptr;
     float *d_unorm = nullptr;
     unsigned long long *d_counters = nullptr;
@@ -149,6 +156,9 @@ void free_scene(rvcp_ctx *ctx)
     (void)hipFree(ctx->d_lights); ctx->d_lights = nullptr;
     (void)hipFree(ctx->d_rawmats); ctx->d_rawmats = nullptr;
     (void)hipFree(ctx->d_spheres); ctx->d_spheres = nullptr;
+    (void)hipFree(ctx->d_bvh_nodes); ctx->d_bvh_nodes = nullptr;
+    (void)hipFree(ctx->d_bvh_tris); ctx->d_bvh_tris = nullptr;
+    (void)hipFree(ctx->d_bvh_ids); ctx->d_bvh_ids = nullptr;
     ctx->has_scene = false;
 }
 
@@ -207,6 +217,10 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
     if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant)
         return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
+    if (cfg->accel != RVCP_ACCEL_NONE && cfg->accel != RVCP_ACCEL_BVH)
+        return fail(nullptr, RVCP_E_INVALID, "unknown accel");
+    if (cfg->accel == RVCP_ACCEL_BVH && cfg->integrator != RVCP_INTEGRATOR_GAMES101)
+        return fail(nullptr, RVCP_E_UNSUPPORTED, "RVCP_ACCEL_BVH is implemented for the games101 integrator");
     if (!(cfg->ray_t_max < 16777216.0f))
         return fail(nullptr, RVCP_E_INVALID, "ray_t_max must be < 2^24 (miss test t_max + 1)");
     int ndev = 0;
@@ -261,6 +275,10 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         if (rvcp_legacy_occupancy(&per_cu) != 0 || per_cu <= 0) per_cu = 1;
         if (cap > 0 && cap < per_cu) per_cu = cap;
         ctx->legacy_capacity = per_cu * cus;
+        per_cu = 0;
+        if (rvcp_games101_occupancy(5, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
+        if (cap > 0 && cap < per_cu) per_cu = cap;
+        ctx->bvh_capacity = per_cu * cus;
     }
     *out_ctx = ctx;
     return RVCP_OK;
@@ -382,6 +400,26 @@ int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         (rc = dev_upload<rvcp_sphere_t>(ctx, &ctx->d_spheres, spheres, n_spheres)))
         return rc;
     ctx->n_spheres = n_spheres;
+    if (ctx->cfg.accel == RVCP_ACCEL_BVH && n_faces > 0) {
+        std::vector<float> pos((size_t)n_faces * 9);
+        for (uint32_t i = 0; i < n_faces; i++)
+            for (int v = 0; v < 3; v++)
+                std::memcpy(&pos[(size_t)i * 9 + 3 * v], vertices[faces[i].vertices[v]].position, 12);
+        std::vector<BvhNode> nodes;
+        std::vector<uint32_t> order;
+        int32_t root = 0;
+        const int depth = bvh_build(reinterpret_cast<const float (*)[3][3]>(pos.data()), n_faces,
+                                    nodes, order, root);
+        if (depth >= kBvhStack) return fail(ctx, RVCP_E_UNSUPPORTED, "BVH deeper than the traversal stack");
+        std::vector<TriRecord> btri(order.size());
+        for (size_t j = 0; j < order.size(); j++) btri[j] = tri[order[j]];
+        if ((rc = dev_upload<BvhNode>(ctx, &ctx->d_bvh_nodes, nodes.data(), nodes.size())) ||
+            (rc = dev_upload<TriRecord>(ctx, &ctx->d_bvh_tris, btri.data(), btri.size())) ||
+            (rc = dev_upload<uint32_t>(ctx, &ctx->d_bvh_ids, order.data(), order.size())))
+            return rc;
+        ctx->bvh_root = root;
+        ctx->bvh_depth = depth;
+    }
     ctx->n_faces = n_faces;
     ctx->n_verts = n_vertices;
     ctx->n_mats = n_materials;
@@ -493,6 +531,9 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     A.want_linear = d_linear_rgb ? 1u : 0u;
     A.variant = ctx->cfg.kernel_variant != 0 ? ctx->cfg.kernel_variant
               : (ctx->n_faces >= kTiledMinFaces ? 4 : kDefaultVariant);
+    A.accel = (ctx->cfg.accel == RVCP_ACCEL_BVH && ctx->n_faces > 0) ? RVCP_ACCEL_BVH : RVCP_ACCEL_NONE;
+    if (A.accel == RVCP_ACCEL_BVH) A.variant = 3;    // the BVH traversal lives in the v3 kernels
+    A.bvh_root = ctx->bvh_root;
     const bool legacy = ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY;
     A.n_spheres = legacy ? ctx->n_spheres : 0u;
 
@@ -510,7 +551,8 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
                                   0xFF000000u, s);
         } else {
             const uint32_t cap = (uint32_t)(legacy ? ctx->legacy_capacity
-                                                   : ctx->grid_capacity[A.variant]);
+                                           : A.accel ? ctx->bvh_capacity
+                                                     : ctx->grid_capacity[A.variant]);
             A.n_simds = ctx->n_simds;
             uint32_t waves = 0, chunk = 0;
             rvcp_static_split(A.n_pixels, cap * (kBlock / kWave), A.n_simds, &waves, &chunk);
@@ -560,6 +602,7 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
                                              ctx->d_mats, ctx->d_lights, ctx->d_gamma,
                                              (uint32_t *)d_rgba8, (float *)d_linear_rgb,
                                              ctx->d_counters, ctx->d_surf, ctx->d_shade,
+                                             ctx->d_bvh_nodes, ctx->d_bvh_tris, ctx->d_bvh_ids,
                                              blocks, s, ctx->evm);
             } else {
                 HIP_TRY(ctx, hipEventRecord(ctx->evm, s));

@@ -4,6 +4,8 @@
 
 #include <stdint.h>
 
+#include <vector>
+
 namespace rvcp {
 
 // Wave width on CDNA4.
@@ -92,6 +94,21 @@ struct alignas(16) MatRecord {
 };
 static_assert(sizeof(MatRecord) == 32, "MatRecord is 32 B");
 
+// Opt-in BVH (rvcp_config_t.accel = RVCP_ACCEL_BVH): a binary tree whose nodes hold both
+// children's boxes, so a traversal step tests two boxes and descends into the nearer child.
+// Child reference: >= 0 an internal node, < 0 a leaf ~ref = first << 3 | (count - 1) over
+// the leaf-ordered triangle arrays.  Boxes are enlarged at build time (bvh_build) so that a
+// triangle the exact test accepts is never culled by rounding in the box test.
+struct alignas(16) BvhNode {
+    float lbox[6];      // left child: lo xyz, hi xyz
+    float rbox[6];      // right child
+    int32_t left, right;
+    int32_t pad[2];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
+constexpr int kBvhLeafMax = 4;
+constexpr int kBvhStack = 32;           // traversal stack entries per lane (tree depth bound)
+
 // Frame-constant parameters of one render launch.
 struct FrameArgs {
     // camera, precomputed on the host exactly as sample_ray (:217-235) computes it
@@ -118,10 +135,16 @@ struct FrameArgs {
     uint32_t dyn_chunk;      // largest frame-queue grab after the static chunk
     uint32_t chunk_min;      // smallest grab
     uint32_t chunk_window;   // grab = pixels this wave consumes in chunk_window ticks (10 ns)
+    int32_t accel;           // RVCP_ACCEL_*
+    int32_t bvh_root;        // root reference (see BvhNode) when accel == RVCP_ACCEL_BVH
     // debug (RVCP_DEBUG_TIMELINE): per-wave {start, queue exhausted, end, iterations}
     // of the path kernel, s_memrealtime ticks (100 MHz); nullptr otherwise
     unsigned long long *timeline;
 };
+
+// rvcp_bvh.cpp: build the BVH over n faces (three vertex positions each); returns the depth.
+int bvh_build(const float (*pos)[3][3], uint32_t n, std::vector<BvhNode> &nodes,
+              std::vector<uint32_t> &order, int32_t &root);
 
 }  // namespace rvcp
 
@@ -137,7 +160,9 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *
                             const rvcp::LightRecord *lights, const float *gamma_t,
                             uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
                             rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
-                            uint32_t grid_blocks, void *stream, void *main_event);
+                            const rvcp::BvhNode *bvh_nodes, const rvcp::TriRecord *bvh_tris,
+                            const uint32_t *bvh_ids, uint32_t grid_blocks, void *stream,
+                            void *main_event);
 // Integrator RVCP_INTEGRATOR_LEGACY (ray_tracer.comp): materials / spheres are the raw
 // rvcp_material_t / rvcp_sphere_t arrays, unorm_t the UNORM8 threshold table.
 int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,

@@ -142,6 +142,65 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
     return (b1 >= 0.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f) & (t >= tmin) & (t <= bt);
 }
 
+// Opt-in BVH (RVCP_ACCEL_BVH): nearest hit of ray (o, d) over the tree, with the scan's exact
+// triangle test and its order rule -- the brute-force scan keeps the smallest t and, among
+// equal t, the later face (:288-295), so candidates met in any order are kept iff
+// t < bt or (t == bt and face > best).  Boxes were enlarged at build (rvcp_bvh.cpp), so the
+// slab test may use a fast reciprocal.  Per-lane traversal with a private stack.
+__device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, float bt,
+                                     float &tnear) {
+    const float x0 = (b[0] - o.x) * inv.x, x1 = (b[3] - o.x) * inv.x;
+    const float y0 = (b[1] - o.y) * inv.y, y1 = (b[4] - o.y) * inv.y;
+    const float z0 = (b[2] - o.z) * inv.z, z1 = (b[5] - o.z) * inv.z;
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
+                                     __builtin_fmaxf(__builtin_fminf(z0, z1), tmin));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
+                                     __builtin_fminf(__builtin_fmaxf(z0, z1), bt));
+    tnear = tn;
+    return tn <= tf;
+}
+
+__device__ __noinline__ void bvh_nearest(const BvhNode *__restrict__ nodes,
+                                         const TriRecord *__restrict__ btri,
+                                         const uint32_t *__restrict__ bids, int32_t root, f3 o,
+                                         f3 d, float tmin, float &bt, int &best) {
+    const f3 inv = mk(__builtin_amdgcn_rcpf(d.x != 0.0f ? d.x : 1e-30f),
+                      __builtin_amdgcn_rcpf(d.y != 0.0f ? d.y : 1e-30f),
+                      __builtin_amdgcn_rcpf(d.z != 0.0f ? d.z : 1e-30f));
+    int32_t stack[kBvhStack];
+    int sp = 0;
+    int32_t ref = root;
+    for (;;) {
+        if (ref >= 0) {
+            const BvhNode &N = nodes[ref];
+            float nl, nr;
+            const bool hl = slab(N.lbox, o, inv, tmin, bt, nl);
+            const bool hr = slab(N.rbox, o, inv, tmin, bt, nr);
+            if (hl && hr) {
+                const bool lfirst = nl <= nr;
+                stack[sp++] = lfirst ? N.right : N.left;
+                ref = lfirst ? N.left : N.right;
+                continue;
+            }
+            if (hl) { ref = N.left; continue; }
+            if (hr) { ref = N.right; continue; }
+        } else {
+            const uint32_t code = ~(uint32_t)ref;
+            const uint32_t first = code >> 5, cnt = (code & 31u) + 1u;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                float t;
+                const int id = (int)bids[first + k];
+                if (tri_accept(btri[first + k], o, d, tmin, bt, t) && (t < bt || id > best)) {
+                    bt = t;
+                    best = id;
+                }
+            }
+        }
+        if (sp == 0) break;
+        ref = stack[--sp];
+    }
+}
+
 // Hit record of face `best` for ray (o, d) hit at time t (:262-278).
 __device__ __forceinline__ void hit_record(const TriRecord *__restrict__ tri,
                                            const rvcp_face_t *__restrict__ faces,
@@ -758,12 +817,15 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
 // ======================================================================================
 constexpr uint32_t kPrimaryBlock = 1024;   // one list append (global atomic) per 1024 pixels
 
+template <bool BVH>
 __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
     const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
     const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade)
+    SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade,
+    const BvhNode *__restrict__ bvh_nodes, const TriRecord *__restrict__ bvh_tris,
+    const uint32_t *__restrict__ bvh_ids)
 {
     __shared__ uint32_t block_count, block_base;
     const uint32_t lane = lane_id();
@@ -781,10 +843,14 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
         primary_ray(A, u_, v_, o, d, tmin, tmax);
         int best = -1;
         float bt = tmax;
+        if (BVH) {
+            bvh_nearest(bvh_nodes, bvh_tris, bvh_ids, A.bvh_root, o, d, tmin, bt, best);
+        } else {
 #pragma unroll 2
-        for (uint32_t i = 0; i < A.n_faces; ++i) {
-            float t;
-            if (tri_accept(tri[i], o, d, tmin, bt, t)) { bt = t; best = (int)i; }
+            for (uint32_t i = 0; i < A.n_faces; ++i) {
+                float t;
+                if (tri_accept(tri[i], o, d, tmin, bt, t)) { bt = t; best = (int)i; }
+            }
         }
         FaceShade fs;
         fs.ty = 0;
@@ -834,13 +900,15 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_PATH_MIN_WAVES
 #define RVCP_PATH_MIN_WAVES 1
 #endif
-template <bool TILED>
+template <bool TILED, bool BVH>
 __device__ __forceinline__ void path_body(
     const FrameArgs &A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
     unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
-    const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile)
+    const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile,
+    const BvhNode *__restrict__ bvh_nodes = nullptr, const TriRecord *__restrict__ bvh_tris = nullptr,
+    const uint32_t *__restrict__ bvh_ids = nullptr)
 {
     const uint32_t lane = lane_id();
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -956,7 +1024,7 @@ __device__ __forceinline__ void path_body(
         float btA = A.t_max, btB = A.t_max;
         const uint32_t na = (uint32_t)__builtin_popcountll(mA);
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
-        const bool tail = wave_active && q.exhausted && nr <= kWave / 2;
+        const bool tail = wave_active && q.exhausted && nr <= kWave / 2 && !BVH;
         if (TILED) {
             // ---- LDS-tiled scan (optionally with the tail partition below) ----
             uint32_t R = 1, part = 0;
@@ -1026,6 +1094,10 @@ __device__ __forceinline__ void path_body(
                 if (hasA) { btA = tA_; bestA = iA_; }
                 if (hasB) { btB = tB_; bestB = iB_; }
             }
+        } else if (BVH) {
+            // ---- opt-in BVH: each lane traverses for its own rays ----
+            if (hasA) bvh_nearest(bvh_nodes, bvh_tris, bvh_ids, A.bvh_root, a_o, a_d, A.t_min, btA, bestA);
+            if (hasB) bvh_nearest(bvh_nodes, bvh_tris, bvh_ids, A.bvh_root, b_o, b_d, A.t_min, btB, bestB);
         } else if (tail) {
             // ---- tail: R lanes per ray, each scanning every R-th triangle ----
             // The frame queue is empty, so what is left are the serial sample chains of the
@@ -1131,8 +1203,23 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
     const FaceShade *__restrict__ shade)
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];   // tail: ray rank -> owner lane
-    path_body<false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade,
-                     tail_tab, nullptr);
+    path_body<false, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
+                            shade, tail_tab, nullptr);
+}
+
+// Opt-in BVH (RVCP_ACCEL_BVH): the variant-3 machine with per-lane BVH traversal in place of
+// the brute-force scan.
+__global__ __launch_bounds__(kBlock) void games101_bvh_path_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade, const BvhNode *__restrict__ bvh_nodes,
+    const TriRecord *__restrict__ bvh_tris, const uint32_t *__restrict__ bvh_ids)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    path_body<false, true>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
+                           shade, tail_tab, nullptr, bvh_nodes, bvh_tris, bvh_ids);
 }
 
 __global__ __launch_bounds__(kBlock) void games101_tiled_kernel(
@@ -1144,8 +1231,8 @@ __global__ __launch_bounds__(kBlock) void games101_tiled_kernel(
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ TriRecord tile[kTile];
-    path_body<true>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade,
-                    tail_tab, tile);
+    path_body<true, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
+                           shade, tail_tab, tile);
 }
 
 // Frame assembly after the RCCL gather: slot k holds shard k's stripes packed.
@@ -1455,20 +1542,31 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                                        const rvcp::LightRecord *lights, const float *gamma_t,
                                        uint32_t *out_rgba, float *out_lin,
                                        unsigned long long *counters, rvcp::SurfRecord *surf,
-                                       const rvcp::FaceShade *shade, uint32_t grid_blocks,
-                                       void *stream, void *main_event)
+                                       const rvcp::FaceShade *shade,
+                                       const rvcp::BvhNode *bvh_nodes,
+                                       const rvcp::TriRecord *bvh_tris, const uint32_t *bvh_ids,
+                                       uint32_t grid_blocks, void *stream, void *main_event)
 {
     const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
-    hipLaunchKernelGGL(rvcp::games101_primary_kernel, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
+    auto pre = args->accel ? rvcp::games101_primary_kernel<true> : rvcp::games101_primary_kernel<false>;
+    hipLaunchKernelGGL(pre, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
                        (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
                        (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
-                       surf, shade);
+                       surf, shade, bvh_nodes, bvh_tris, bvh_ids);
     if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
         return -2;
-    auto kern = args->variant == 4 ? rvcp::games101_tiled_kernel : rvcp::games101_path_kernel;
-    hipLaunchKernelGGL(kern, dim3(grid_blocks), dim3(rvcp::kBlock), 0, (hipStream_t)stream,
-                       *args, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
-                       shade);
+    if (args->accel)
+        hipLaunchKernelGGL(rvcp::games101_bvh_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+                           (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
+                           out_lin, counters, surf, shade, bvh_nodes, bvh_tris, bvh_ids);
+    else if (args->variant == 4)
+        hipLaunchKernelGGL(rvcp::games101_tiled_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+                           (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
+                           out_lin, counters, surf, shade);
+    else
+        hipLaunchKernelGGL(rvcp::games101_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+                           (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
+                           out_lin, counters, surf, shade);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1500,7 +1598,9 @@ extern "C" int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n, 
 extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
 {
     int b = 0;
-    const hipError_t e = variant == 4
+    const hipError_t e = variant == 5
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_bvh_path_kernel, rvcp::kBlock, 0)
+        : variant == 4
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_kernel, rvcp::kBlock, 0)
         : variant == 3
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel, rvcp::kBlock, 0)

@@ -20,12 +20,14 @@ def main():
     ap.add_argument("--spp", type=int, default=30)
     ap.add_argument("--tris", type=int, default=0)
     ap.add_argument("--integrator", type=int, default=0)
+    ap.add_argument("--accel", type=int, default=0)
     ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres"])
     a = ap.parse_args()
     sc = rvcp_amd.Scene.default() if a.scene == "cornell" else rvcp_amd.scene.sphere_scene()
     if a.tris:
         sc = rvcp_amd.scene.with_random_triangles(sc, a.tris)
-    with rvcp_amd.RayTracer(spp=a.spp, kernel_variant=a.variant, integrator=a.integrator) as rt:
+    with rvcp_amd.RayTracer(spp=a.spp, kernel_variant=a.variant, integrator=a.integrator,
+                            accel=a.accel) as rt:
         rt.upload_scene(sc)
         for _ in range(a.frames):
             rt.render(a.size, a.size, 123.0)

@@ -41,6 +41,8 @@ for s in $STEPS; do
         c5t) run c5t 400 bash -c "echo c5-512-v4; python tools/frames.py --variant 4 --frames 3 --tris 100000 --size 512 --spp 4 || exit 1; echo c5-512-v3; python tools/frames.py --variant 3 --frames 2 --tris 100000 --size 512 --spp 4" ;;
         w5) run w5 300 bash -c "echo c3-default; python tools/frames.py --frames 10 || exit 1; echo c3-w5; RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/variants/librvcp_w5.so python tools/frames.py --frames 10 || exit 1; echo c2-w5; RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/variants/librvcp_w5.so python tools/frames.py --frames 10 --size 384 --spp 10" ;;
         v35) run v35 300 bash -c "python tools/frames.py --variant 3 --frames 6 && python tools/frames.py --variant 5 --frames 6 && python tools/frames.py --variant 3 --frames 6 --size 384 --spp 10 && python tools/frames.py --variant 5 --frames 6 --size 384 --spp 10" ;;
+        bvh) run pytest_bvh 600 python -m pytest tests/test_gpu_bvh.py -m gpu -x -q ;;
+        bvhperf) run bvhperf 600 bash -c "echo c3-bvh; python tools/frames.py --frames 5 --accel 1 || exit 1; echo c5-bvh; python tools/frames.py --frames 3 --tris 100000 --accel 1 || exit 1" ;;
         legacy) run pytest_legacy 600 python -m pytest tests/test_gpu_legacy.py -m gpu -x -q ;;
         lframes) run lframes 300 python tools/frames.py --integrator 1 --scene spheres --frames 5 --spp 5 ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
