@@ -87,15 +87,15 @@ __device__ __forceinline__ float rnd(float seed, float &idx) {
 }
 
 // 1 / den, IEEE round-to-nearest (the shader's `1.0 / dot(s1, e1)`, :254).
-// Fast path: v_rcp_f32 plus one FMA Newton step.  tools/rcp_check.hip compares it with the
-// IEEE division for every normal |den| in [2^-126, 2^126) (all 2^23 mantissas, both signs):
-// 0 mismatches.  Outside that range (zero, denormal, huge, inf, NaN) -- a degenerate or
-// grazing triangle -- the lanes concerned take the full IEEE division.
+// Fast path: v_rcp_f32 plus one FMA Newton step, kept whenever the result is a normal number
+// (one v_cmp_class); otherwise -- zero, subnormal, inf or NaN result, i.e. a degenerate,
+// grazing or astronomically large triangle -- the lane takes the full IEEE division.
+// tools/rcp_check2.hip runs all 2^32 inputs on gfx950: the fast path is taken for
+// 4,227,858,434 of them and equals the IEEE quotient bit for bit on every one.
 __device__ __forceinline__ float rcp_ieee(float den) {
     const float r = __builtin_amdgcn_rcpf(den);
     float f = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
-    const float a = __builtin_fabsf(den);
-    if (__builtin_expect(!(a >= 0x1p-126f && a < 0x1p126f), 0)) f = 1.0f / den;
+    if (__builtin_expect(!__builtin_amdgcn_class(f, (1 << 8) | (1 << 3)), 0)) f = 1.0f / den;
     return f;
 }
 
@@ -1209,7 +1209,7 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
 
 // Opt-in BVH (RVCP_ACCEL_BVH): the variant-3 machine with per-lane BVH traversal in place of
 // the brute-force scan.
-__global__ __launch_bounds__(kBlock) void games101_bvh_path_kernel(
+__global__ __launch_bounds__(kBlock, 4) void games101_bvh_path_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,

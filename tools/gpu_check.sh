@@ -40,7 +40,7 @@ for s in $STEPS; do
         chunks) run chunks 500 bash -c "echo c3; python tools/frames.py --frames 10 || exit 1; echo c2; python tools/frames.py --frames 10 --size 384 --spp 10 || exit 1; echo sph; python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; echo small128; python tools/frames.py --frames 10 --size 128 --spp 30 || exit 1" ;;
         c5t) run c5t 400 bash -c "echo c5-512-v4; python tools/frames.py --variant 4 --frames 3 --tris 100000 --size 512 --spp 4 || exit 1; echo c5-512-v3; python tools/frames.py --variant 3 --frames 2 --tris 100000 --size 512 --spp 4" ;;
         w5) run w5 300 bash -c "echo c3-default; python tools/frames.py --frames 10 || exit 1; echo c3-w5; RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/variants/librvcp_w5.so python tools/frames.py --frames 10 || exit 1; echo c2-w5; RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/variants/librvcp_w5.so python tools/frames.py --frames 10 --size 384 --spp 10" ;;
-        v35) run v35 300 bash -c "python tools/frames.py --variant 3 --frames 6 && python tools/frames.py --variant 5 --frames 6 && python tools/frames.py --variant 3 --frames 6 --size 384 --spp 10 && python tools/frames.py --variant 5 --frames 6 --size 384 --spp 10" ;;
+        v35) run v35 400 bash -c "for i in 1 2; do echo c3; python tools/frames.py --frames 10 || exit 1; done; echo c5-512; python tools/frames.py --frames 2 --tris 100000 --size 512 --spp 4" ;;
         bvh) run pytest_bvh 600 python -m pytest tests/test_gpu_bvh.py -m gpu -x -q ;;
         bvhperf) run bvhperf 600 bash -c "echo c3-bvh; python tools/frames.py --frames 5 --accel 1 || exit 1; echo c5-bvh; python tools/frames.py --frames 3 --tris 100000 --accel 1 || exit 1" ;;
         legacy) run pytest_legacy 600 python -m pytest tests/test_gpu_legacy.py -m gpu -x -q ;;
@@ -50,6 +50,7 @@ for s in $STEPS; do
         rehearse2) run rehearse2 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
         rehearse4) run rehearse4 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 4 --steps 3 --warmup 1 ;;
         rcp) run rcp_check 120 tools/build/rcp_check ;;
+        rcp2) run rcp_check2 300 tools/build/rcp_check2 ;;
         split) run split 300 python tools/exp_split.py ;;
         split2) run split2 300 env RVCP_KERNEL_VARIANT=2 python tools/exp_split.py ;;
         occ) run occ 400 bash tools/exp_occ.sh ;;
