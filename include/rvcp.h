@@ -147,7 +147,15 @@ typedef struct rvcp_config {
      * rule; frames match the brute-force ones except where a ray runs almost parallel to a
      * triangle's plane. */
     int32_t accel;
-    uint32_t _reserved[4];
+    /* GPUs one context drives (0 or 1 = one).  With n_gpus = N > 1, rvcp_create opens devices
+     * device, device+1, ... (mod the device count), rvcp_upload_scene uploads to all of them,
+     * and rvcp_render deals the frame's 8-row stripes round-robin over them (stripe s -> GPU
+     * s mod N), renders all shards concurrently and copies each shard's stripes into the frame
+     * on `device` with one strided peer copy per shard (xGMI); the frame is bit-identical to
+     * a 1-GPU render.  The single-process form of SURVEY.md §8(e); one process per GPU with
+     * rvcp_render_shard_async + an RCCL gather (bench.py) is the other. */
+    int32_t n_gpus;
+    uint32_t _reserved[3];
 } rvcp_config_t;
 
 /* Per-render statistics (all optional). */

@@ -62,10 +62,20 @@ struct rvcp_ctx {
     uint32_t *d_rgba = nullptr;
     float *d_lin = nullptr;
     size_t cap_rgba = 0, cap_lin = 0;
+    // n_gpus > 1: shard 0's packed stripes
+    uint32_t *d_pack_rgba = nullptr;
+    float *d_pack_lin = nullptr;
+    size_t cap_surf_pack = 0;
 
     // RVCP_DEBUG_TIMELINE=<file>: per-wave timeline of the path kernel appended per render
     unsigned long long *d_timeline = nullptr;
     size_t cap_timeline = 0, last_timeline_waves = 0;
+
+    // n_gpus > 1: contexts of the other GPUs (shards 1..N-1) and their packed shard buffers
+    std::vector<rvcp_ctx *> subs;
+    std::vector<uint32_t *> shard_rgba;
+    std::vector<float *> shard_lin;
+    std::vector<size_t> shard_cap;
 
     // last launch
     bool pending = false;
@@ -183,6 +193,7 @@ int rvcp_config_default_for(int32_t integrator, rvcp_config_t *cfg)
     cfg->rr_probability = 1.0f;         // :13
     cfg->eps = 0.001f;                  // :5
     cfg->lum_id_std140_quirk = 1;       // (unused by ray_trace)
+    cfg->n_gpus = 1;
     return RVCP_OK;
 }
 
@@ -200,6 +211,7 @@ int rvcp_config_default(rvcp_config_t *cfg)
     cfg->rr_probability = 0.8f;         // :13
     cfg->eps = 0.001f;                  // :5
     cfg->lum_id_std140_quirk = 1;
+    cfg->n_gpus = 1;
     return RVCP_OK;
 }
 
@@ -217,6 +229,8 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
     if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant)
         return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
+    if (cfg->n_gpus < 0 || cfg->n_gpus > 64)
+        return fail(nullptr, RVCP_E_INVALID, "n_gpus must be in [0, 64]");
     if (cfg->accel != RVCP_ACCEL_NONE && cfg->accel != RVCP_ACCEL_BVH)
         return fail(nullptr, RVCP_E_INVALID, "unknown accel");
     if (cfg->accel == RVCP_ACCEL_BVH && cfg->integrator != RVCP_INTEGRATOR_GAMES101)
@@ -280,6 +294,33 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         if (cap > 0 && cap < per_cu) per_cu = cap;
         ctx->bvh_capacity = per_cu * cus;
     }
+    if (cfg->n_gpus > 1) {   // one sub-context per further GPU (shards 1..N-1)
+        for (int i = 1; i < cfg->n_gpus; i++) {
+            rvcp_config_t sub_cfg = *cfg;
+            sub_cfg.n_gpus = 1;
+            sub_cfg.device = (cfg->device + i) % ndev;
+            rvcp_ctx_t *sub = nullptr;
+            if ((rc = rvcp_create(&sub_cfg, &sub)) != RVCP_OK) {
+                ctx->err = "sub-context on device " + std::to_string(sub_cfg.device) + ": " + g_create_error;
+                return bail(rc);
+            }
+            ctx->subs.push_back(sub);
+            ctx->shard_rgba.push_back(nullptr);
+            ctx->shard_lin.push_back(nullptr);
+            ctx->shard_cap.push_back(0);
+            if (sub_cfg.device != cfg->device) {   // direct xGMI copies into the frame's GPU
+                int ok = 0;
+                if (hipDeviceCanAccessPeer(&ok, cfg->device, sub_cfg.device) == hipSuccess && ok) {
+                    (void)hipSetDevice(cfg->device);
+                    const hipError_t pe = hipDeviceEnablePeerAccess(sub_cfg.device, 0);
+                    if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+                        return bail(fail(ctx, RVCP_E_HIP, "hipDeviceEnablePeerAccess failed"));
+                    (void)hipGetLastError();
+                }
+            }
+        }
+        (void)hipSetDevice(cfg->device);
+    }
     *out_ctx = ctx;
     return RVCP_OK;
 }
@@ -287,6 +328,14 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
 int rvcp_destroy(rvcp_ctx_t *ctx)
 {
     if (!ctx) return RVCP_OK;
+    for (size_t i = 0; i < ctx->subs.size(); i++) {
+        if (!ctx->subs[i]) continue;
+        (void)hipSetDevice(ctx->subs[i]->device);
+        (void)hipFree(ctx->shard_rgba[i]);
+        (void)hipFree(ctx->shard_lin[i]);
+        rvcp_destroy(ctx->subs[i]);
+    }
+    ctx->subs.clear();
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_scene(ctx);
@@ -297,6 +346,8 @@ int rvcp_destroy(rvcp_ctx_t *ctx)
     (void)hipFree(ctx->d_lin);
     (void)hipFree(ctx->d_surf);
     (void)hipFree(ctx->d_timeline);
+    (void)hipFree(ctx->d_pack_rgba);
+    (void)hipFree(ctx->d_pack_lin);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->evm) (void)hipEventDestroy(ctx->evm);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -305,7 +356,36 @@ int rvcp_destroy(rvcp_ctx_t *ctx)
     return RVCP_OK;
 }
 
+static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_t n_materials,
+                      const rvcp_vertex_t *vertices, uint32_t n_vertices,
+                      const rvcp_face_t *faces, uint32_t n_faces,
+                      const rvcp_sphere_t *spheres, uint32_t n_spheres,
+                      const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
+                      const uint32_t *lum_sphere_ids, uint32_t n_lum_sphere_ids);
+
 int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_t n_materials,
+                      const rvcp_vertex_t *vertices, uint32_t n_vertices,
+                      const rvcp_face_t *faces, uint32_t n_faces,
+                      const rvcp_sphere_t *spheres, uint32_t n_spheres,
+                      const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
+                      const uint32_t *lum_sphere_ids, uint32_t n_lum_sphere_ids)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    int rc = upload_one(ctx, materials, n_materials, vertices, n_vertices, faces, n_faces,
+                        spheres, n_spheres, lum_face_ids, n_lum_face_ids, lum_sphere_ids,
+                        n_lum_sphere_ids);
+    for (rvcp_ctx *sub : ctx->subs) {
+        if (rc != RVCP_OK) break;
+        rc = upload_one(sub, materials, n_materials, vertices, n_vertices, faces, n_faces,
+                        spheres, n_spheres, lum_face_ids, n_lum_face_ids, lum_sphere_ids,
+                        n_lum_sphere_ids);
+        if (rc != RVCP_OK) ctx->err = "sub-context upload: " + sub->err;
+    }
+    (void)hipSetDevice(ctx->device);
+    return rc;
+}
+
+static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_t n_materials,
                       const rvcp_vertex_t *vertices, uint32_t n_vertices,
                       const rvcp_face_t *faces, uint32_t n_faces,
                       const rvcp_sphere_t *spheres, uint32_t n_spheres,
@@ -659,6 +739,102 @@ int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
     return RVCP_OK;
 }
 
+// n_gpus > 1: every GPU renders its stripes packed (shard k of N on GPU k), then each shard
+// is copied into the frame on ctx->device with one strided copy (stripe j of shard k ->
+// frame rows 8(jN + k) .. +8), over xGMI when the GPUs differ.  Stats are summed over shards;
+// kernel_ms is the slowest shard's.
+static int render_multi(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t W,
+                        uint32_t H, bool want_lin, rvcp_stats_t *stats)
+{
+    const uint32_t N = (uint32_t)ctx->subs.size() + 1;
+    int rc;
+    // 1. launch every shard (shard 0 renders on ctx itself, into a packed buffer of its own)
+    for (uint32_t k = 0; k < N; k++) {
+        rvcp_ctx *c = k == 0 ? ctx : ctx->subs[k - 1];
+        const size_t rows = rvcp_shard_rows(H, k, N), px = rows * W;
+        if (k > 0 && (ctx->shard_cap[k - 1] < px || (want_lin && !ctx->shard_lin[k - 1]))) {
+            HIP_TRY(ctx, hipSetDevice(c->device));
+            (void)hipFree(ctx->shard_rgba[k - 1]);
+            (void)hipFree(ctx->shard_lin[k - 1]);
+            ctx->shard_rgba[k - 1] = nullptr;
+            ctx->shard_lin[k - 1] = nullptr;
+            ctx->shard_cap[k - 1] = 0;
+            HIP_TRY(ctx, hipMalloc((void **)&ctx->shard_rgba[k - 1], px * 4 + 4));
+            HIP_TRY(ctx, hipMalloc((void **)&ctx->shard_lin[k - 1], px * 12 + 12));
+            ctx->shard_cap[k - 1] = px;
+        }
+    }
+    // shard 0 needs its own packed buffer too: reuse the staging's tail is not possible, so
+    // keep it in shard_rgba[-1] semantics via a dedicated allocation on ctx
+    const size_t px0 = (size_t)rvcp_shard_rows(H, 0, N) * W;
+    if (ctx->cap_surf_pack < px0 || (want_lin && !ctx->d_pack_lin)) {
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        (void)hipFree(ctx->d_pack_rgba);
+        (void)hipFree(ctx->d_pack_lin);
+        ctx->d_pack_rgba = nullptr;
+        ctx->d_pack_lin = nullptr;
+        ctx->cap_surf_pack = 0;
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_pack_rgba, px0 * 4 + 4));
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_pack_lin, px0 * 12 + 12));
+        ctx->cap_surf_pack = px0;
+    }
+    for (uint32_t k = 0; k < N; k++) {
+        rvcp_ctx *c = k == 0 ? ctx : ctx->subs[k - 1];
+        uint32_t *d_rgba = k == 0 ? ctx->d_pack_rgba : ctx->shard_rgba[k - 1];
+        float *d_lin = want_lin ? (k == 0 ? ctx->d_pack_lin : ctx->shard_lin[k - 1]) : nullptr;
+        if ((rc = rvcp_render_shard_async(c, push, W, H, k, N, d_rgba, d_lin, c->stream)) != RVCP_OK) {
+            if (k > 0) ctx->err = "shard " + std::to_string(k) + ": " + c->err;
+            (void)hipSetDevice(ctx->device);
+            return rc;
+        }
+    }
+    // 2. wait for each shard and copy its stripes into the frame on ctx->device
+    rvcp_stats_t total;
+    std::memset(&total, 0, sizeof(total));
+    for (uint32_t k = 0; k < N; k++) {
+        rvcp_ctx *c = k == 0 ? ctx : ctx->subs[k - 1];
+        rvcp_stats_t st;
+        if ((rc = rvcp_sync_stats(c, &st)) != RVCP_OK) {
+            if (k > 0) ctx->err = "shard " + std::to_string(k) + ": " + c->err;
+            (void)hipSetDevice(ctx->device);
+            return rc;
+        }
+        total.kernel_ms = st.kernel_ms > total.kernel_ms ? st.kernel_ms : total.kernel_ms;
+        total.main_kernel_ms = st.main_kernel_ms > total.main_kernel_ms ? st.main_kernel_ms : total.main_kernel_ms;
+        total.traversals += st.traversals;
+        total.traversals_executed += st.traversals_executed;
+        total.samples += st.samples;
+        total.wave_iterations += st.wave_iterations;
+        total.faces = st.faces;
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        const uint32_t stripes = (H + 7) / 8;
+        const uint32_t full = H / 8;                       // stripes with 8 rows
+        uint32_t n_full = 0;                               // full stripes of shard k
+        for (uint32_t s = k; s < full; s += N) n_full++;
+        const uint8_t *src = (const uint8_t *)(k == 0 ? ctx->d_pack_rgba : ctx->shard_rgba[k - 1]);
+        const float *srcl = k == 0 ? ctx->d_pack_lin : ctx->shard_lin[k - 1];
+        for (int pass = 0; pass < (want_lin ? 2 : 1); pass++) {
+            const size_t bpp = pass == 0 ? 4 : 12;
+            const uint8_t *sp = pass == 0 ? src : (const uint8_t *)srcl;
+            uint8_t *dp = pass == 0 ? (uint8_t *)ctx->d_rgba : (uint8_t *)ctx->d_lin;
+            if (n_full)
+                HIP_TRY(ctx, hipMemcpy2DAsync(dp + (size_t)8 * k * W * bpp, (size_t)8 * N * W * bpp,
+                                              sp, (size_t)8 * W * bpp, (size_t)8 * W * bpp, n_full,
+                                              hipMemcpyDefault, ctx->stream));
+            // a last, partial stripe (H % 8 rows), if it is shard k's
+            if (full < stripes && (full % N) == k) {
+                const size_t rows = H - 8 * full;
+                HIP_TRY(ctx, hipMemcpyAsync(dp + (size_t)8 * full * W * bpp,
+                                            sp + (size_t)8 * n_full * W * bpp, rows * W * bpp,
+                                            hipMemcpyDefault, ctx->stream));
+            }
+        }
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (stats) *stats = total;
+    return RVCP_OK;
+}
+
 int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
                 uint32_t height, uint8_t *out_rgba8, float *out_linear_rgb, rvcp_stats_t *stats)
 {
@@ -682,10 +858,15 @@ int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t widt
         HIP_TRY(ctx, hipMalloc((void **)&ctx->d_lin, npx * 12));
         ctx->cap_lin = npx;
     }
-    int rc = rvcp_render_shard_async(ctx, push, width, height, 0, 1, ctx->d_rgba,
+    int rc;
+    if (ctx->subs.empty()) {
+        rc = rvcp_render_shard_async(ctx, push, width, height, 0, 1, ctx->d_rgba,
                                      out_linear_rgb ? ctx->d_lin : nullptr, ctx->stream);
-    if (rc != RVCP_OK) return rc;
-    if ((rc = rvcp_sync_stats(ctx, stats)) != RVCP_OK) return rc;
+        if (rc != RVCP_OK) return rc;
+        if ((rc = rvcp_sync_stats(ctx, stats)) != RVCP_OK) return rc;
+    } else if ((rc = render_multi(ctx, push, width, height, out_linear_rgb != nullptr, stats)) != RVCP_OK) {
+        return rc;
+    }
     HIP_TRY(ctx, hipMemcpy(out_rgba8, ctx->d_rgba, npx * 4, hipMemcpyDeviceToHost));
     if (out_linear_rgb) HIP_TRY(ctx, hipMemcpy(out_linear_rgb, ctx->d_lin, npx * 12, hipMemcpyDeviceToHost));
     return RVCP_OK;

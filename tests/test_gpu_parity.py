@@ -220,3 +220,24 @@ def test_shard_assembly_bitexact(cornell, n_shards):
         torch.cuda.synchronize()
     got = frame.cpu().numpy().view(np.uint8).reshape(H, W, 4)
     assert np.array_equal(got, full)
+
+
+@pytest.mark.parametrize("n_gpus", [2, 3, 8])
+@pytest.mark.parametrize("W,H,spp", [(64, 64, 2), (37, 29, 3), (130, 3, 2), (256, 200, 1)])
+def test_single_process_multi_gpu(cornell, n_gpus, W, H, spp):
+    """rvcp_config_t.n_gpus > 1 (single process, strided peer copies of the stripes into the
+    frame's GPU): bit-identical to one GPU.  On a 1-GPU box every shard runs on device 0,
+    which exercises the sharding and the copy geometry."""
+    one = _gpu(cornell, rvcp_amd.abi.make_config(spp=spp), W, H)
+    many = _gpu(cornell, rvcp_amd.abi.make_config(spp=spp, n_gpus=n_gpus), W, H)
+    assert np.array_equal(many[0], one[0])
+    assert np.array_equal(many[1].view(np.uint32), one[1].view(np.uint32))
+    assert int(many[2]["traversals"]) == int(one[2]["traversals"])
+    assert int(many[2]["samples"]) == int(one[2]["samples"])
+
+
+def test_single_process_multi_gpu_legacy():
+    sc = rvcp_amd.scene.sphere_scene()
+    one = _gpu(sc, rvcp_amd.abi.make_config(integrator=1), 96, 80)
+    many = _gpu(sc, rvcp_amd.abi.make_config(integrator=1, n_gpus=4), 96, 80)
+    assert np.array_equal(many[1].view(np.uint32), one[1].view(np.uint32))
