@@ -30,7 +30,10 @@ constexpr uint32_t kChunkWindow = 10000;    // 100 us
 // (selected automatically for meshes of kTiledMinFaces faces or more).
 constexpr int kDefaultVariant = 3;
 constexpr int kMaxVariant = 4;
-constexpr uint32_t kTile = 256;             // triangles per LDS tile (12 KiB)
+#ifndef RVCP_TILE
+#define RVCP_TILE 256
+#endif
+constexpr uint32_t kTile = RVCP_TILE;       // triangles per LDS tile (12 KiB at 256)
 constexpr uint32_t kTiledMinFaces = 4096;
 
 // One triangle as the brute-force scan reads it: v0, e1 = v1 - v0, e2 = v2 - v0, computed on

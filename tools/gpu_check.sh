@@ -40,7 +40,7 @@ for s in $STEPS; do
         chunks) run chunks 500 bash -c "echo c3; python tools/frames.py --frames 10 || exit 1; echo c2; python tools/frames.py --frames 10 --size 384 --spp 10 || exit 1; echo sph; python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; echo small128; python tools/frames.py --frames 10 --size 128 --spp 30 || exit 1" ;;
         c5t) run c5t 400 bash -c "echo c5-512-v4; python tools/frames.py --variant 4 --frames 3 --tris 100000 --size 512 --spp 4 || exit 1; echo c5-512-v3; python tools/frames.py --variant 3 --frames 2 --tris 100000 --size 512 --spp 4" ;;
         w5) run w5 300 bash -c "echo c3-default; python tools/frames.py --frames 10 || exit 1; echo c3-w5; RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/variants/librvcp_w5.so python tools/frames.py --frames 10 || exit 1; echo c2-w5; RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/variants/librvcp_w5.so python tools/frames.py --frames 10 --size 384 --spp 10" ;;
-        v35) run v35 400 bash -c "for i in 1 2; do echo c3; python tools/frames.py --frames 10 || exit 1; done; echo c5-512; python tools/frames.py --frames 2 --tris 100000 --size 512 --spp 4" ;;
+        v35) run v35 900 bash -c "for v in 4 5 3; do echo c5 v\$v; python tools/frames.py --variant \$v --frames 2 --tris 100000 --size 512 --spp 4 || exit 1; done; for v in 3 5; do echo c3 v\$v; python tools/frames.py --variant \$v --frames 6 || exit 1; done; for v in 4 5; do echo c5-2k v\$v; python tools/frames.py --variant \$v --frames 2 --tris 2000 --size 512 --spp 8 || exit 1; done" ;;
         bvh) run pytest_bvh 600 python -m pytest tests/test_gpu_bvh.py -m gpu -x -q ;;
         bvhperf) run bvhperf 600 bash -c "echo c3-bvh; python tools/frames.py --frames 5 --accel 1 || exit 1; echo c5-bvh; python tools/frames.py --frames 3 --tris 100000 --accel 1 || exit 1" ;;
         legacy) run pytest_legacy 600 python -m pytest tests/test_gpu_legacy.py -m gpu -x -q ;;
