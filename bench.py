@@ -67,6 +67,20 @@ def workload(name, n_gpus):
     raise SystemExit(f"unknown workload {name}")
 
 
+def load_valu_busy(workload_name, kernel_substr):
+    """VALU issue utilisation of the dominant kernel from the newest committed SQ PMC summary."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_valu_{workload_name}.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for name, k in d.get("kernels", {}).items():
+        if kernel_substr in name:
+            return k.get("valu_busy")
+    return None
+
+
 def load_traffic(workload_name, kernel_substr):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary."""
     import glob
@@ -243,6 +257,7 @@ def main():
     kname = ("legacy_kernel" if legacy else "games101_bvh_path_kernel" if args.accel == "bvh"
              else "games101_tiled_kernel" if n_faces >= 4096 else "games101_path_kernel")
     traffic, traffic_src = load_traffic(wl["workload"], kname)
+    valu_busy = load_valu_busy(wl["workload"], kname)
 
     frame_check = None
     if world > 1 and rank == 0:
@@ -295,6 +310,7 @@ def main():
                          "executed_traversal_frac": round(trav_exec / max(trav, 1), 4),
                          "valu_tflops": round(tests_per_s * FLOP_PER_TEST / 1e12, 2),
                          "valu_frac": round(tests_per_s * FLOP_PER_TEST / 1e12 / FP32_PEAK_TFLOPS, 4),
+                         "valu_busy_pmc": valu_busy,
                          "executed_tests_per_s": round(exec_tests_per_s, 1)},
             "cpu_baseline": None,
         }

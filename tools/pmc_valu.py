@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""VALU issue utilisation of each kernel from a rocprofv3 SQ/GRBM PMC pass:
+
+  valu_busy = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction occupies a SIMD for two
+              cycles on CDNA4, MI355X_MICROARCH.md) / (GRBM_GUI_ACTIVE per XCD x SIMDs)
+
+GRBM_GUI_ACTIVE is summed over the 8 XCDs by rocprofv3, so it is divided by 8 to get the
+kernel's cycles.  Writes the JSON bench.py reads into roofline.valu_busy.
+
+  python tools/pmc_valu.py SQ.csv GRBM.csv OUT.json --workload NAME [--simds 1024 --xcds 8]
+"""
+import argparse
+import csv
+import json
+import re
+from collections import defaultdict
+
+
+def per_kernel(path, counter):
+    vals = defaultdict(list)
+    with open(path, newline="") as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] == counter:
+                vals[re.sub(r"\(.*", "", row["Kernel_Name"]).strip('"')].append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("sq_csv")
+    ap.add_argument("grbm_csv")
+    ap.add_argument("out_json")
+    ap.add_argument("--workload", required=True)
+    ap.add_argument("--simds", type=int, default=1024)
+    ap.add_argument("--xcds", type=int, default=8)
+    a = ap.parse_args()
+    valu = per_kernel(a.sq_csv, "SQ_INSTS_VALU")
+    grbm = per_kernel(a.grbm_csv, "GRBM_GUI_ACTIVE")
+    out = {"workload": a.workload, "sources": [a.sq_csv, a.grbm_csv],
+           "method": "SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE / xcds x simds), per launch",
+           "kernels": {}}
+    for k in sorted(set(valu) & set(grbm)):
+        v = sum(valu[k]) / len(valu[k])
+        g = sum(grbm[k]) / len(grbm[k]) / a.xcds
+        out["kernels"][k] = {"valu_insts": v, "cycles": g,
+                             "valu_busy": round(2.0 * v / (g * a.simds), 4) if g else None}
+    with open(a.out_json, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
