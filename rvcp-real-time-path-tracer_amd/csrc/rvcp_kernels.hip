@@ -95,7 +95,7 @@ __device__ __forceinline__ float rnd(float seed, float &idx) {
 __device__ __forceinline__ float rcp_ieee(float den) {
     const float r = __builtin_amdgcn_rcpf(den);
     float f = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
-    if (__builtin_expect(!__builtin_amdgcn_class(f, (1 << 8) | (1 << 3)), 0)) f = 1.0f / den;
+    if (__builtin_expect(!__builtin_amdgcn_classf(f, (1 << 8) | (1 << 3)), 0)) f = 1.0f / den;
     return f;
 }
 

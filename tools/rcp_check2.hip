@@ -16,7 +16,7 @@ __global__ void check(uint32_t hi, unsigned long long *bad, unsigned long long *
     const float r = __builtin_amdgcn_rcpf(d);
     const float f = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
     // class mask: bit 8 = +normal, bit 3 = -normal (v_cmp_class_f32 encoding)
-    const bool normal = __builtin_amdgcn_class(f, (1 << 8) | (1 << 3));
+    const bool normal = __builtin_amdgcn_classf(f, (1 << 8) | (1 << 3));
     if (!normal) return;
     atomicAdd(used, 1ull);
     const float exact = 1.0f / d;
