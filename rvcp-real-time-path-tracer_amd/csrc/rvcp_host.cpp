@@ -492,7 +492,10 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
                                     nodes, order, root);
         if (depth >= kBvhStack) return fail(ctx, RVCP_E_UNSUPPORTED, "BVH deeper than the traversal stack");
         std::vector<TriRecord> btri(order.size());
-        for (size_t j = 0; j < order.size(); j++) btri[j] = tri[order[j]];
+        for (size_t j = 0; j < order.size(); j++) {       // leaf order, face id in pad[0]
+            btri[j] = tri[order[j]];
+            std::memcpy(&btri[j].pad[0], &order[j], 4);
+        }
         if ((rc = dev_upload<BvhNode>(ctx, &ctx->d_bvh_nodes, nodes.data(), nodes.size())) ||
             (rc = dev_upload<TriRecord>(ctx, &ctx->d_bvh_tris, btri.data(), btri.size())) ||
             (rc = dev_upload<uint32_t>(ctx, &ctx->d_bvh_ids, order.data(), order.size())))

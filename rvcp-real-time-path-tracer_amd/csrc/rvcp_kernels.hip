@@ -160,14 +160,48 @@ __device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, f
     return tn <= tf;
 }
 
+// One leaf: its (at most kBvhLeafMax) triangles are loaded before any is tested, so the
+// leaf costs one memory round trip instead of one per triangle.  The original face id rides in
+// TriRecord::pad[0] of the leaf-ordered copy (rvcp_host.cpp).
+__device__ __forceinline__ void bvh_leaf(const TriRecord *__restrict__ btri, int32_t ref, f3 o, f3 d,
+                                         float tmin, float &bt, int &best) {
+    const uint32_t code = ~(uint32_t)ref;
+    const uint32_t first = code >> 5, cnt = (code & 31u) + 1u;
+    TriRecord L[kBvhLeafMax];
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)kBvhLeafMax; ++k)
+        if (k < cnt) L[k] = btri[first + k];
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)kBvhLeafMax; ++k) {
+        if (k < cnt) {
+            float t;
+            const int id = __float_as_int(L[k].pad[0]);
+            if (tri_accept(L[k], o, d, tmin, bt, t) && (t < bt || id > best)) {
+                bt = t;
+                best = id;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ f3 slab_inv(f3 d) {
+    return mk(__builtin_amdgcn_rcpf(d.x != 0.0f ? d.x : 1e-30f),
+              __builtin_amdgcn_rcpf(d.y != 0.0f ? d.y : 1e-30f),
+              __builtin_amdgcn_rcpf(d.z != 0.0f ? d.z : 1e-30f));
+}
+
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+
+// LDS = true: the traversal stack is the caller's LDS column (stk[i * kBlock], one column per
+// thread, so the lanes of a wave hit distinct banks whatever their depths); LDS = false: a
+// private array (the pre-pass kernel, whose 1024-thread blocks would need 128 KiB of LDS).
+template <bool LDS>
 __device__ __noinline__ void bvh_nearest(const BvhNode *__restrict__ nodes,
-                                         const TriRecord *__restrict__ btri,
-                                         const uint32_t *__restrict__ bids, int32_t root, f3 o,
-                                         f3 d, float tmin, float &bt, int &best) {
-    const f3 inv = mk(__builtin_amdgcn_rcpf(d.x != 0.0f ? d.x : 1e-30f),
-                      __builtin_amdgcn_rcpf(d.y != 0.0f ? d.y : 1e-30f),
-                      __builtin_amdgcn_rcpf(d.z != 0.0f ? d.z : 1e-30f));
-    int32_t stack[kBvhStack];
+                                         const TriRecord *__restrict__ btri, int32_t root,
+                                         lds_i32 *stk, f3 o, f3 d, float tmin, float &bt,
+                                         int &best) {
+    const f3 inv = slab_inv(d);
+    int32_t priv[LDS ? 1 : kBvhStack];
     int sp = 0;
     int32_t ref = root;
     for (;;) {
@@ -178,26 +212,20 @@ __device__ __noinline__ void bvh_nearest(const BvhNode *__restrict__ nodes,
             const bool hr = slab(N.rbox, o, inv, tmin, bt, nr);
             if (hl && hr) {
                 const bool lfirst = nl <= nr;
-                stack[sp++] = lfirst ? N.right : N.left;
+                const int32_t far = lfirst ? N.right : N.left;
+                if (LDS) stk[sp * kBlock] = far; else priv[sp] = far;
+                sp += 1;
                 ref = lfirst ? N.left : N.right;
                 continue;
             }
             if (hl) { ref = N.left; continue; }
             if (hr) { ref = N.right; continue; }
         } else {
-            const uint32_t code = ~(uint32_t)ref;
-            const uint32_t first = code >> 5, cnt = (code & 31u) + 1u;
-            for (uint32_t k = 0; k < cnt; ++k) {
-                float t;
-                const int id = (int)bids[first + k];
-                if (tri_accept(btri[first + k], o, d, tmin, bt, t) && (t < bt || id > best)) {
-                    bt = t;
-                    best = id;
-                }
-            }
+            bvh_leaf(btri, ref, o, d, tmin, bt, best);
         }
         if (sp == 0) break;
-        ref = stack[--sp];
+        sp -= 1;
+        ref = LDS ? stk[sp * kBlock] : priv[sp];
     }
 }
 
@@ -844,7 +872,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
         int best = -1;
         float bt = tmax;
         if (BVH) {
-            bvh_nearest(bvh_nodes, bvh_tris, bvh_ids, A.bvh_root, o, d, tmin, bt, best);
+            bvh_nearest<false>(bvh_nodes, bvh_tris, A.bvh_root, nullptr, o, d, tmin, bt, best);
         } else {
 #pragma unroll 2
             for (uint32_t i = 0; i < A.n_faces; ++i) {
@@ -908,7 +936,7 @@ __device__ __forceinline__ void path_body(
     unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
     const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile,
     const BvhNode *__restrict__ bvh_nodes = nullptr, const TriRecord *__restrict__ bvh_tris = nullptr,
-    const uint32_t *__restrict__ bvh_ids = nullptr)
+    const uint32_t *__restrict__ bvh_ids = nullptr, int32_t *bvh_stack = nullptr)
 {
     const uint32_t lane = lane_id();
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1096,8 +1124,9 @@ __device__ __forceinline__ void path_body(
             }
         } else if (BVH) {
             // ---- opt-in BVH: each lane traverses for its own rays ----
-            if (hasA) bvh_nearest(bvh_nodes, bvh_tris, bvh_ids, A.bvh_root, a_o, a_d, A.t_min, btA, bestA);
-            if (hasB) bvh_nearest(bvh_nodes, bvh_tris, bvh_ids, A.bvh_root, b_o, b_d, A.t_min, btB, bestB);
+            lds_i32 *stk = (lds_i32 *)bvh_stack;
+            if (hasA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, a_o, a_d, A.t_min, btA, bestA);
+            if (hasB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB);
         } else if (tail) {
             // ---- tail: R lanes per ray, each scanning every R-th triangle ----
             // The frame queue is empty, so what is left are the serial sample chains of the
@@ -1218,8 +1247,10 @@ __global__ __launch_bounds__(kBlock, 4) void games101_bvh_path_kernel(
     const TriRecord *__restrict__ bvh_tris, const uint32_t *__restrict__ bvh_ids)
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    __shared__ int32_t bvh_stack[kBvhStack * kBlock];     // traversal stacks, column per thread
     path_body<false, true>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
-                           shade, tail_tab, nullptr, bvh_nodes, bvh_tris, bvh_ids);
+                           shade, tail_tab, nullptr, bvh_nodes, bvh_tris, bvh_ids,
+                           bvh_stack + threadIdx.x);
 }
 
 __global__ __launch_bounds__(kBlock) void games101_tiled_kernel(
