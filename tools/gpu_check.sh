@@ -66,6 +66,7 @@ for s in $STEPS; do
         pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         bvhvar) run bvhvar 900 bash -c 'for v in tools/build/var_*/librvcp.so; do echo "$v"; RVCP_LIB=$v python tools/frames.py --frames 2 --tris 100000 --accel 1 || exit 1; done' ;;
+        c5var) run c5var 1100 bash -c 'for v in tools/build/var_*/librvcp.so; do echo "$v"; RVCP_LIB=$v python tools/frames.py --frames 2 --tris 100000 || exit 1; done' ;;
         benchc5bvh) run bench_c5_bvh 600 python bench.py --workload c5 --steps 3 --warmup 1 --accel bvh --no-cpu-baseline ;;
         benchc5) run bench_c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
         benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 ;;
