@@ -255,7 +255,7 @@ def main():
     tests_per_s = units * (n_faces + n_spheres) / avg_kernel_s
     exec_tests_per_s = (trav_exec / args.steps - prepass) * (n_faces + n_spheres) / avg_kernel_s
     kname = ("legacy_kernel" if legacy else "games101_bvh_path_kernel" if args.accel == "bvh"
-             else "games101_tiled_kernel" if n_faces >= 4096 else "games101_path_kernel")
+             else "games101_tiled_single_kernel" if n_faces >= 256 else "games101_path_kernel")
     traffic, traffic_src = load_traffic(wl["workload"], kname)
     valu_busy = load_valu_busy(wl["workload"], kname)
 

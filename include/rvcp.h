@@ -134,10 +134,11 @@ typedef struct rvcp_config {
      * (ray_tracer_games101_branch.comp:109-111 vs vulkan.rs:473-478): element i is
      * ids[4*i] when 4*i < n_ids, else 0.  0 = the intended packed semantics. */
     int32_t lum_id_std140_quirk;
-    /* Kernel schedule, for A/B measurement only: 0 = automatic (3, or 4 for meshes of 4096+
+    /* Kernel schedule, for A/B measurement only: 0 = automatic (3, or 5 for meshes of 256+
      * faces), 1 = one ray per lane per iteration, 2 = shadow + continuation ray per lane per
      * iteration, 3 = primary pre-pass + 2 over surface pixels (scalar-cache scan), 4 = 3 with
-     * the scan staged through LDS tiles shared by the workgroup.  Every schedule produces
+     * the scan staged through LDS tiles shared by the workgroup, 5 = 4 with one ray per lane
+     * per iteration (shadow ray, then path ray: no empty ray slots).  Every schedule produces
      * bit-identical frames. */
     int32_t kernel_variant;
     /* Acceleration structure: RVCP_ACCEL_NONE (default) scans every triangle like the

@@ -290,7 +290,7 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         if (cap > 0 && cap < per_cu) per_cu = cap;
         ctx->legacy_capacity = per_cu * cus;
         per_cu = 0;
-        if (rvcp_games101_occupancy(5, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
+        if (rvcp_games101_occupancy(kOccupancyBvh, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
         if (cap > 0 && cap < per_cu) per_cu = cap;
         ctx->bvh_capacity = per_cu * cus;
     }
@@ -613,7 +613,7 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     A.light_pdf = ctx->light_pdf;
     A.want_linear = d_linear_rgb ? 1u : 0u;
     A.variant = ctx->cfg.kernel_variant != 0 ? ctx->cfg.kernel_variant
-              : (ctx->n_faces >= kTiledMinFaces ? 4 : kDefaultVariant);
+              : (ctx->n_faces >= kTiledMinFaces ? 5 : kDefaultVariant);
     A.accel = (ctx->cfg.accel == RVCP_ACCEL_BVH && ctx->n_faces > 0) ? RVCP_ACCEL_BVH : RVCP_ACCEL_NONE;
     if (A.accel == RVCP_ACCEL_BVH) A.variant = 3;    // the BVH traversal lives in the v3 kernels
     A.bvh_root = ctx->bvh_root;

@@ -27,14 +27,18 @@ constexpr uint32_t kChunkWindow = 10000;    // 100 us
 // 2 = shadow + continuation ray per lane per iteration, 3 = primary pre-pass kernel + the
 // variant-2 loop over surface pixels only.
 // 4 = variant 3 with the triangle scan staged through LDS tiles shared by the workgroup
-// (selected automatically for meshes of kTiledMinFaces faces or more).
+// (selectable; variant 5 is the automatic choice for meshes of kTiledMinFaces faces or more).
+// 5 = variant 4 with one ray per lane per iteration (the shadow ray, then the path ray), so no
+// ray slot is empty; for scan-bound meshes.
 constexpr int kDefaultVariant = 3;
-constexpr int kMaxVariant = 4;
+constexpr int kMaxVariant = 5;
+constexpr int kOccupancyBvh = 100;          // rvcp_games101_occupancy code of the BVH kernel
 #ifndef RVCP_TILE
 #define RVCP_TILE 256
 #endif
 constexpr uint32_t kTile = RVCP_TILE;       // triangles per LDS tile (12 KiB at 256)
-constexpr uint32_t kTiledMinFaces = 4096;
+constexpr uint32_t kTiledMinFaces = 256;   // auto: variant 5 from here (measured crossover
+                                            // vs variant 3 at ~230 faces)
 
 // One triangle as the brute-force scan reads it: v0, e1 = v1 - v0, e2 = v2 - v0, computed on
 // the host with the same float subtractions the shader performs per test

@@ -933,7 +933,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_PATH_MIN_WAVES
 #define RVCP_PATH_MIN_WAVES 1
 #endif
-template <bool TILED, bool BVH>
+template <bool TILED, bool BVH, bool SINGLE = false>
 __device__ __forceinline__ void path_body(
     const FrameArgs &A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
@@ -1041,7 +1041,14 @@ __device__ __forceinline__ void path_body(
             }
             if (!__any(ended)) break;
         }
-        const uint64_t mA = __ballot(hasA), mB = __ballot(hasB);
+        // The scan's view of the lane's rays.  SINGLE (variant 5): one ray per lane per
+        // iteration -- the shadow ray A while it is pending, else the path ray B; a B left
+        // pending is traced on the next iteration, without a new surface event.
+        const bool sA = SINGLE ? (hasA || hasB) : hasA;
+        const bool sB = SINGLE ? false : hasB;
+        const f3 s_ao = (SINGLE && !hasA) ? b_o : a_o;
+        const f3 s_ad = (SINGLE && !hasA) ? b_d : a_d;
+        const uint64_t mA = __ballot(sA), mB = __ballot(sB);
         const bool wave_active = (mA | mB) != 0ull;
         if (TILED) {
             // every wave of the workgroup keeps loading tiles until the whole group is done
@@ -1050,7 +1057,7 @@ __device__ __forceinline__ void path_body(
             break;
         }
         if (wave_active) iters += 1;
-        trav += (hasA ? 1u : 0u) + (hasB ? 1u : 0u);
+        trav += (sA ? 1u : 0u) + (sB ? 1u : 0u);
         if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
 
         int bestA = -1, bestB = -1;
@@ -1062,13 +1069,13 @@ __device__ __forceinline__ void path_body(
             // ---- LDS-tiled scan (optionally with the tail partition below) ----
             uint32_t R = 1, part = 0;
             bool worker = false;
-            f3 o = a_o, d = a_d;
+            f3 o = s_ao, d = s_ad;
             if (tail) {
                 R = 2;
                 while (nr * R * 2 <= (uint32_t)kWave) R *= 2;
                 uint8_t *tab = tail_tab[threadIdx.x / kWave];
-                if (hasA) tab[rank_in(mA)] = (uint8_t)lane;
-                if (hasB) tab[na + rank_in(mB)] = (uint8_t)lane;
+                if (sA) tab[rank_in(mA)] = (uint8_t)lane;
+                if (sB) tab[na + rank_in(mB)] = (uint8_t)lane;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1077,8 +1084,8 @@ __device__ __forceinline__ void path_body(
                 worker = j < nr;
                 const int owner = worker ? (int)tab[j] : (int)lane;
                 const bool isA = j < na;
-                const f3 oa = mk(__shfl(a_o.x, owner), __shfl(a_o.y, owner), __shfl(a_o.z, owner));
-                const f3 da = mk(__shfl(a_d.x, owner), __shfl(a_d.y, owner), __shfl(a_d.z, owner));
+                const f3 oa = mk(__shfl(s_ao.x, owner), __shfl(s_ao.y, owner), __shfl(s_ao.z, owner));
+                const f3 da = mk(__shfl(s_ad.x, owner), __shfl(s_ad.y, owner), __shfl(s_ad.z, owner));
                 const f3 ob = mk(__shfl(b_o.x, owner), __shfl(b_o.y, owner), __shfl(b_o.z, owner));
                 const f3 db = mk(__shfl(b_d.x, owner), __shfl(b_d.y, owner), __shfl(b_d.z, owner));
                 o = isA ? oa : ob;
@@ -1106,8 +1113,8 @@ __device__ __forceinline__ void path_body(
                     for (uint32_t i = 0; i < n; ++i) {
                         const TriRecord T = tile[i];
                         float tA, tB;
-                        if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
-                        if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
+                        if (tri_accept(T, s_ao, s_ad, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
+                        if (!SINGLE && tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
                     }
                 }
                 __syncthreads();
@@ -1118,12 +1125,16 @@ __device__ __forceinline__ void path_body(
                     const int ob = __shfl_xor(best, (int)off);
                     if (ot < bt || (ot == bt && ob > best)) { bt = ot; best = ob; }
                 }
-                const int srcA = hasA ? (int)(rank_in(mA) * R) : (int)lane;
-                const int srcB = hasB ? (int)((na + rank_in(mB)) * R) : (int)lane;
+                const int srcA = sA ? (int)(rank_in(mA) * R) : (int)lane;
+                const int srcB = sB ? (int)((na + rank_in(mB)) * R) : (int)lane;
                 const float tA_ = __shfl(bt, srcA), tB_ = __shfl(bt, srcB);
                 const int iA_ = __shfl(best, srcA), iB_ = __shfl(best, srcB);
-                if (hasA) { btA = tA_; bestA = iA_; }
-                if (hasB) { btB = tB_; bestB = iB_; }
+                if (sA) { btA = tA_; bestA = iA_; }
+                if (sB) { btB = tB_; bestB = iB_; }
+            }
+            if (SINGLE && !hasA) {      // the lane traced its path ray
+                btB = btA;
+                bestB = bestA;
             }
         } else if (BVH) {
             // ---- opt-in BVH: each lane traverses for its own rays ----
@@ -1195,7 +1206,8 @@ __device__ __forceinline__ void path_body(
             if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) col = add(col, nee_C);
         }
         // ---- resolve B: next bounce (:421-429) ----
-        if (hasB) {
+        const bool defer_B = SINGLE && hasA && hasB;    // B was not traced this iteration
+        if (hasB && !defer_B) {
             if (bestB < 0) {
                 col = add(col, mk(0.1f, 0.1f, 0.1f));
                 ended = true;
@@ -1210,11 +1222,11 @@ __device__ __forceinline__ void path_body(
                     surf_ev = true;
                 }
             }
-        } else if (hasA) {
+        } else if (hasA && !hasB) {
             ended = true;       // the path ended at its last surface event (RR / depth / att)
         }
         hasA = false;
-        hasB = false;
+        if (!defer_B) hasB = false;
     }
     flush_counters(counters, lane, trav, iters);
     if (A.timeline && lane == 0) {
@@ -1266,6 +1278,20 @@ __global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_k
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ TriRecord tile[kTile];
     path_body<true, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
+                           shade, tail_tab, tile);
+}
+
+// Variant 5: the LDS-tiled scan with one ray per lane per iteration (no empty ray slots).
+__global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_single_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    __shared__ TriRecord tile[kTile];
+    path_body<true, false, true>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
                            shade, tail_tab, tile);
 }
 
@@ -1593,6 +1619,10 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
         hipLaunchKernelGGL(rvcp::games101_bvh_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade, bvh_nodes, bvh_tris, bvh_ids);
+    else if (args->variant == 5)
+        hipLaunchKernelGGL(rvcp::games101_tiled_single_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+                           (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
+                           out_lin, counters, surf, shade);
     else if (args->variant == 4)
         hipLaunchKernelGGL(rvcp::games101_tiled_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
@@ -1632,8 +1662,10 @@ extern "C" int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n, 
 extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
 {
     int b = 0;
-    const hipError_t e = variant == 5
+    const hipError_t e = variant == rvcp::kOccupancyBvh
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_bvh_path_kernel, rvcp::kBlock, 0)
+        : variant == 5
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_single_kernel, rvcp::kBlock, 0)
         : variant == 4
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_kernel, rvcp::kBlock, 0)
         : variant == 3

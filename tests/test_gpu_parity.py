@@ -39,7 +39,7 @@ def _assert_same(gpu, orc):
     assert int(stats["traversals"]) == o_trav
 
 
-VARIANTS = [1, 2, 3, 4]    # kernel schedules (rvcp_config_t::kernel_variant); 0 = default
+VARIANTS = [1, 2, 3, 4, 5]    # kernel schedules (rvcp_config_t::kernel_variant); 0 = default
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -68,6 +68,15 @@ def test_variants_bitexact(cornell, variant, case):
         sc = rvcp_amd.scene.with_random_triangles(cornell, 200)
     cfg = rvcp_amd.abi.make_config(kernel_variant=variant, **kw)
     _assert_same(_gpu(sc, cfg, 40, 36), _oracle(sc, cfg, 40, 36))
+
+
+@pytest.mark.parametrize("variant", [4, 5])
+def test_multi_tile_bitexact(cornell, variant):
+    """LDS-tiled schedules over several triangle tiles (732 faces = 2 full tiles of 256 and a
+    partial one), nearest hits spread across tiles."""
+    sc = rvcp_amd.scene.with_random_triangles(cornell, 700)
+    cfg = rvcp_amd.abi.make_config(kernel_variant=variant, spp=2)
+    _assert_same(_gpu(sc, cfg, 48, 40), _oracle(sc, cfg, 48, 40))
 
 
 def test_bitexact_quirk_off(cornell):
