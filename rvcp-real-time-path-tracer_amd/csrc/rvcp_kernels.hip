@@ -927,6 +927,11 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 // ======================================================================================
 // Variant 4 is held to 4 waves per SIMD (128 VGPRs, a few spills around the tile loop): 5 %
 // faster on C5 than the 3 waves its natural 146-155 VGPRs give.
+// The BVH path kernel traces one ray per lane per iteration (the variant-5 form): C5 297 ->
+// 283 ms over the dual form, whose second traversal leaves the lanes without a path ray idle.
+#ifndef RVCP_BVH_SINGLE
+#define RVCP_BVH_SINGLE true
+#endif
 #ifndef RVCP_TILED_MIN_WAVES
 #define RVCP_TILED_MIN_WAVES 4
 #endif
@@ -1132,15 +1137,11 @@ __device__ __forceinline__ void path_body(
                 if (sA) { btA = tA_; bestA = iA_; }
                 if (sB) { btB = tB_; bestB = iB_; }
             }
-            if (SINGLE && !hasA) {      // the lane traced its path ray
-                btB = btA;
-                bestB = bestA;
-            }
         } else if (BVH) {
             // ---- opt-in BVH: each lane traverses for its own rays ----
             lds_i32 *stk = (lds_i32 *)bvh_stack;
-            if (hasA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, a_o, a_d, A.t_min, btA, bestA);
-            if (hasB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB);
+            if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA);
+            if (sB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB);
         } else if (tail) {
             // ---- tail: R lanes per ray, each scanning every R-th triangle ----
             // The frame queue is empty, so what is left are the serial sample chains of the
@@ -1196,6 +1197,16 @@ __device__ __forceinline__ void path_body(
                 if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
                 if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
             }
+        }
+
+        if (SINGLE && !hasA) {          // the lane traced its path ray
+            btB = btA;
+            bestB = bestA;
+        }
+
+        if (SINGLE && !hasA) {          // the lane traced its path ray
+            btB = btA;
+            bestB = bestA;
         }
 
         // ---- resolve A: visibility of the light sample (:447-459) ----
@@ -1263,7 +1274,7 @@ __global__ __launch_bounds__(kBlock, 4) void games101_bvh_path_kernel(
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ int32_t bvh_stack[kBvhStack * kBlock];     // traversal stacks, column per thread
-    path_body<false, true>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
+    path_body<false, true, RVCP_BVH_SINGLE>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
                            shade, tail_tab, nullptr, bvh_nodes, bvh_tris, bvh_ids,
                            bvh_stack + threadIdx.x);
 }
