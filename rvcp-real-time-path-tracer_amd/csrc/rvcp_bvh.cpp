@@ -195,4 +195,97 @@ int bvh_build(const float (*pos)[3][3], uint32_t n, std::vector<BvhNode> &nodes,
     return B.max_depth;     // the caller rejects max_depth >= kBvhStack
 }
 
+namespace {
+
+struct Collapser {
+    const std::vector<BvhNode> &n2;
+    std::vector<Bvh4Node> &out;
+    std::vector<int> height;        // binary height per node (a leaf child counts 0)
+
+    struct Child {
+        int32_t ref;
+        const float *box;           // lo xyz, hi xyz (already enlarged)
+    };
+
+    int h(int32_t ref) const { return ref < 0 ? 0 : height[ref]; }
+
+    int measure(int32_t ref) {
+        if (ref < 0) return 0;
+        const int a = measure(n2[ref].left), b = measure(n2[ref].right);
+        return height[ref] = 1 + std::max(a, b);
+    }
+
+    static float area(const float *b) {
+        const float x = b[3] - b[0], y = b[4] - b[1], z = b[5] - b[2];
+        return x * y + y * z + z * x;
+    }
+
+    // 4-wide node for binary node `ref`, whose traversal may use `budget` stack entries.
+    // Children are opened (largest box first) while (children - 1) plus the largest binary
+    // height among them fits the budget; an unopened binary subtree of height H never needs
+    // more than H entries, so every recursion stays feasible.
+    int32_t build(int32_t ref, int budget, int &need) {
+        const BvhNode &N = n2[ref];
+        std::vector<Child> c = {{N.left, N.lbox}, {N.right, N.rbox}};
+        while (c.size() < 4) {
+            int pick = -1;
+            float best = -1.0f;
+            for (size_t i = 0; i < c.size(); i++)
+                if (c[i].ref >= 0 && area(c[i].box) > best) { best = area(c[i].box); pick = (int)i; }
+            if (pick < 0) break;
+            const BvhNode &M = n2[c[pick].ref];
+            std::vector<Child> t = c;
+            t[pick] = {M.left, M.lbox};
+            t.push_back({M.right, M.rbox});
+            int hmax = 0;
+            for (const Child &x : t) hmax = std::max(hmax, h(x.ref));
+            if ((int)t.size() - 1 + hmax > budget) break;
+            c.swap(t);
+        }
+        const int32_t self = (int32_t)out.size();
+        out.emplace_back();
+        const int push = (int)c.size() - 1;
+        int sub = 0;
+        int32_t refs[4];
+        for (size_t i = 0; i < c.size(); i++) {
+            refs[i] = c[i].ref;
+            if (c[i].ref >= 0) {
+                int nd = 0;
+                refs[i] = build(c[i].ref, budget - push, nd);
+                sub = std::max(sub, nd);
+            }
+        }
+        Bvh4Node &Q = out[self];
+        for (int i = 0; i < 4; i++) {
+            const bool used = i < (int)c.size();
+            for (int k = 0; k < 3; k++) {
+                Q.lo[k][i] = used ? c[i].box[k] : 3e38f;
+                Q.hi[k][i] = used ? c[i].box[3 + k] : 3e38f;
+            }
+            Q.ref[i] = used ? refs[i] : ~0;
+            Q.pad[i] = 0;
+        }
+        need = push + sub;
+        return self;
+    }
+};
+
+}  // namespace
+
+int bvh4_collapse(const std::vector<BvhNode> &nodes, int32_t root, std::vector<Bvh4Node> &out,
+                  int32_t &root4)
+{
+    out.clear();
+    if (root < 0) {             // a single leaf: no inner node
+        root4 = root;
+        return 0;
+    }
+    Collapser C{nodes, out, std::vector<int>(nodes.size(), 0)};
+    C.measure(root);
+    out.reserve(nodes.size());
+    int need = 0;
+    root4 = C.build(root, kBvhStack, need);
+    return need;
+}
+
 }  // namespace rvcp

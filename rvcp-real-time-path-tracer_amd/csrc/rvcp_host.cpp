@@ -42,9 +42,8 @@ struct rvcp_ctx {
     rvcp_material_t *d_rawmats = nullptr;     // RVCP_INTEGRATOR_LEGACY: fuzz / ior needed
     rvcp_sphere_t *d_spheres = nullptr;
     // opt-in BVH (RVCP_ACCEL_BVH): nodes, leaf-ordered triangles and their face ids
-    BvhNode *d_bvh_nodes = nullptr;
+    Bvh4Node *d_bvh_nodes = nullptr;
     TriRecord *d_bvh_tris = nullptr;
-    uint32_t *d_bvh_ids = nullptr;
     int32_t bvh_root = 0;
     int bvh_depth = 0;
     float *d_gamma = nullptr;
@@ -168,7 +167,6 @@ void free_scene(rvcp_ctx *ctx)
     (void)hipFree(ctx->d_spheres); ctx->d_spheres = nullptr;
     (void)hipFree(ctx->d_bvh_nodes); ctx->d_bvh_nodes = nullptr;
     (void)hipFree(ctx->d_bvh_tris); ctx->d_bvh_tris = nullptr;
-    (void)hipFree(ctx->d_bvh_ids); ctx->d_bvh_ids = nullptr;
     ctx->has_scene = false;
 }
 
@@ -496,11 +494,14 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
             btri[j] = tri[order[j]];
             std::memcpy(&btri[j].pad[0], &order[j], 4);
         }
-        if ((rc = dev_upload<BvhNode>(ctx, &ctx->d_bvh_nodes, nodes.data(), nodes.size())) ||
-            (rc = dev_upload<TriRecord>(ctx, &ctx->d_bvh_tris, btri.data(), btri.size())) ||
-            (rc = dev_upload<uint32_t>(ctx, &ctx->d_bvh_ids, order.data(), order.size())))
+        std::vector<Bvh4Node> nodes4;
+        int32_t root4 = 0;
+        if (bvh4_collapse(nodes, root, nodes4, root4) > kBvhStack)
+            return fail(ctx, RVCP_E_UNSUPPORTED, "BVH traversal stack bound exceeded");
+        if ((rc = dev_upload<Bvh4Node>(ctx, &ctx->d_bvh_nodes, nodes4.data(), nodes4.size())) ||
+            (rc = dev_upload<TriRecord>(ctx, &ctx->d_bvh_tris, btri.data(), btri.size())))
             return rc;
-        ctx->bvh_root = root;
+        ctx->bvh_root = root4;
         ctx->bvh_depth = depth;
     }
     ctx->n_faces = n_faces;
@@ -685,7 +686,7 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
                                              ctx->d_mats, ctx->d_lights, ctx->d_gamma,
                                              (uint32_t *)d_rgba8, (float *)d_linear_rgb,
                                              ctx->d_counters, ctx->d_surf, ctx->d_shade,
-                                             ctx->d_bvh_nodes, ctx->d_bvh_tris, ctx->d_bvh_ids,
+                                             ctx->d_bvh_nodes, ctx->d_bvh_tris,
                                              blocks, s, ctx->evm);
             } else {
                 HIP_TRY(ctx, hipEventRecord(ctx->evm, s));

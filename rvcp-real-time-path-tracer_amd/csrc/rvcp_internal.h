@@ -101,11 +101,11 @@ struct alignas(16) MatRecord {
 };
 static_assert(sizeof(MatRecord) == 32, "MatRecord is 32 B");
 
-// Opt-in BVH (rvcp_config_t.accel = RVCP_ACCEL_BVH): a binary tree whose nodes hold both
-// children's boxes, so a traversal step tests two boxes and descends into the nearer child.
-// Child reference: >= 0 an internal node, < 0 a leaf ~ref = first << 3 | (count - 1) over
-// the leaf-ordered triangle arrays.  Boxes are enlarged at build time (bvh_build) so that a
-// triangle the exact test accepts is never culled by rounding in the box test.
+// Opt-in BVH (rvcp_config_t.accel = RVCP_ACCEL_BVH).  The builder makes a binary tree whose
+// nodes hold both children's boxes; child reference: >= 0 an internal node, < 0 a leaf
+// ~ref = first << 5 | (count - 1) over the leaf-ordered triangle array.  Boxes are enlarged at
+// build time (bvh_build) so that a triangle the exact test accepts is never culled by rounding
+// in the box test.  The device traverses the 4-wide tree bvh4_collapse makes of it.
 struct alignas(16) BvhNode {
     float lbox[6];      // left child: lo xyz, hi xyz
     float rbox[6];      // right child
@@ -114,7 +114,19 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
 constexpr int kBvhLeafMax = 4;
-constexpr int kBvhStack = 32;           // traversal stack entries per lane (tree depth bound)
+constexpr int kBvhStack = 32;           // traversal stack entries per lane
+
+// The traversed tree: up to 4 children per node, boxes stored per axis so one node is seven
+// 16-byte loads; a step tests the four boxes, pushes the hit children but the nearest (farthest
+// first) and descends into the nearest.  Unused child slots hold an unreachable box (a point
+// at 3e38) and the leaf reference ~0 (triangle 0 again: a repeated test never changes the hit).
+struct alignas(16) Bvh4Node {
+    float lo[3][4];     // lo[axis][child]
+    float hi[3][4];
+    int32_t ref[4];
+    int32_t pad[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node is 128 B");
 
 // Frame-constant parameters of one render launch.
 struct FrameArgs {
@@ -152,6 +164,10 @@ struct FrameArgs {
 // rvcp_bvh.cpp: build the BVH over n faces (three vertex positions each); returns the depth.
 int bvh_build(const float (*pos)[3][3], uint32_t n, std::vector<BvhNode> &nodes,
               std::vector<uint32_t> &order, int32_t &root);
+// Collapse the binary tree into the 4-wide one, keeping the traversal stack within
+// kBvhStack entries; returns that stack bound.
+int bvh4_collapse(const std::vector<BvhNode> &nodes, int32_t root, std::vector<Bvh4Node> &out,
+                  int32_t &root4);
 
 }  // namespace rvcp
 
@@ -167,9 +183,8 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *
                             const rvcp::LightRecord *lights, const float *gamma_t,
                             uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
                             rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
-                            const rvcp::BvhNode *bvh_nodes, const rvcp::TriRecord *bvh_tris,
-                            const uint32_t *bvh_ids, uint32_t grid_blocks, void *stream,
-                            void *main_event);
+                            const rvcp::Bvh4Node *bvh_nodes, const rvcp::TriRecord *bvh_tris,
+                            uint32_t grid_blocks, void *stream, void *main_event);
 // Integrator RVCP_INTEGRATOR_LEGACY (ray_tracer.comp): materials / spheres are the raw
 // rvcp_material_t / rvcp_sphere_t arrays, unorm_t the UNORM8 threshold table.
 int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,

@@ -192,11 +192,39 @@ __device__ __forceinline__ f3 slab_inv(f3 d) {
 
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 
-// LDS = true: the traversal stack is the caller's LDS column (stk[i * kBlock], one column per
-// thread, so the lanes of a wave hit distinct banks whatever their depths); LDS = false: a
-// private array (the pre-pass kernel, whose 1024-thread blocks would need 128 KiB of LDS).
+// 4-wide traversal (Bvh4Node, rvcp_bvh.cpp).  A step loads one node (seven 16-B loads in
+// flight together), tests its four boxes, sorts the children by entry distance (5-comparator
+// network, misses keyed +inf), pushes the hit ones but the nearest -- farthest first -- and
+// continues with the nearest.  Leaves are tested by bvh_leaf.  The slab test may cull only
+// boxes entered beyond the current nearest hit (tn > bt): the hit rule keeps a later face at
+// equal t, so a box entered exactly at bt must still be visited.
+// LDS = true: the stack is the caller's LDS column (stk[i * kBlock]; the lanes of a wave hit
+// distinct banks whatever their depths); LDS = false: a private array (the pre-pass kernel,
+// whose 1024-thread blocks would need 128 KiB of LDS).
+__device__ __forceinline__ void bvh4_box(float lx, float ly, float lz, float hx, float hy, float hz,
+                                         f3 o, f3 inv, float tmin, float bt, float &key) {
+    const float x0 = (lx - o.x) * inv.x, x1 = (hx - o.x) * inv.x;
+    const float y0 = (ly - o.y) * inv.y, y1 = (hy - o.y) * inv.y;
+    const float z0 = (lz - o.z) * inv.z, z1 = (hz - o.z) * inv.z;
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
+                                     __builtin_fmaxf(__builtin_fminf(z0, z1), tmin));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
+                                     __builtin_fminf(__builtin_fmaxf(z0, z1), bt));
+    key = tn <= tf ? tn : __builtin_inff();
+}
+
+__device__ __forceinline__ void bvh4_cas(float &ka, int32_t &ca, float &kb, int32_t &cb) {
+    const bool sw = kb < ka;
+    const float k = sw ? kb : ka;
+    const int32_t c = sw ? cb : ca;
+    kb = sw ? ka : kb;
+    cb = sw ? ca : cb;
+    ka = k;
+    ca = c;
+}
+
 template <bool LDS>
-__device__ __noinline__ void bvh_nearest(const BvhNode *__restrict__ nodes,
+__device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
                                          const TriRecord *__restrict__ btri, int32_t root,
                                          lds_i32 *stk, f3 o, f3 d, float tmin, float &bt,
                                          int &best) {
@@ -206,20 +234,25 @@ __device__ __noinline__ void bvh_nearest(const BvhNode *__restrict__ nodes,
     int32_t ref = root;
     for (;;) {
         if (ref >= 0) {
-            const BvhNode &N = nodes[ref];
-            float nl, nr;
-            const bool hl = slab(N.lbox, o, inv, tmin, bt, nl);
-            const bool hr = slab(N.rbox, o, inv, tmin, bt, nr);
-            if (hl && hr) {
-                const bool lfirst = nl <= nr;
-                const int32_t far = lfirst ? N.right : N.left;
-                if (LDS) stk[sp * kBlock] = far; else priv[sp] = far;
-                sp += 1;
-                ref = lfirst ? N.left : N.right;
-                continue;
-            }
-            if (hl) { ref = N.left; continue; }
-            if (hr) { ref = N.right; continue; }
+            const float4 *q = reinterpret_cast<const float4 *>(nodes + ref);
+            const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
+            const int4 r = reinterpret_cast<const int4 *>(nodes + ref)[6];
+            float k0, k1, k2, k3;
+            bvh4_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, o, inv, tmin, bt, k0);
+            bvh4_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, o, inv, tmin, bt, k1);
+            bvh4_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, o, inv, tmin, bt, k2);
+            bvh4_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, o, inv, tmin, bt, k3);
+            int32_t c0 = r.x, c1 = r.y, c2 = r.z, c3 = r.w;
+            bvh4_cas(k0, c0, k1, c1);
+            bvh4_cas(k2, c2, k3, c3);
+            bvh4_cas(k0, c0, k2, c2);
+            bvh4_cas(k1, c1, k3, c3);
+            bvh4_cas(k1, c1, k2, c2);
+            const float inf = __builtin_inff();
+            if (k3 < inf) { if (LDS) stk[sp * kBlock] = c3; else priv[sp] = c3; sp += 1; }
+            if (k2 < inf) { if (LDS) stk[sp * kBlock] = c2; else priv[sp] = c2; sp += 1; }
+            if (k1 < inf) { if (LDS) stk[sp * kBlock] = c1; else priv[sp] = c1; sp += 1; }
+            if (k0 < inf) { ref = c0; continue; }
         } else {
             bvh_leaf(btri, ref, o, d, tmin, bt, best);
         }
@@ -852,8 +885,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
     SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade,
-    const BvhNode *__restrict__ bvh_nodes, const TriRecord *__restrict__ bvh_tris,
-    const uint32_t *__restrict__ bvh_ids)
+    const Bvh4Node *__restrict__ bvh_nodes, const TriRecord *__restrict__ bvh_tris)
 {
     __shared__ uint32_t block_count, block_base;
     const uint32_t lane = lane_id();
@@ -945,8 +977,8 @@ __device__ __forceinline__ void path_body(
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
     unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
     const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile,
-    const BvhNode *__restrict__ bvh_nodes = nullptr, const TriRecord *__restrict__ bvh_tris = nullptr,
-    const uint32_t *__restrict__ bvh_ids = nullptr, int32_t *bvh_stack = nullptr)
+    const Bvh4Node *__restrict__ bvh_nodes = nullptr, const TriRecord *__restrict__ bvh_tris = nullptr,
+    int32_t *bvh_stack = nullptr)
 {
     const uint32_t lane = lane_id();
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1269,13 +1301,13 @@ __global__ __launch_bounds__(kBlock, 4) void games101_bvh_path_kernel(
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
     unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
-    const FaceShade *__restrict__ shade, const BvhNode *__restrict__ bvh_nodes,
-    const TriRecord *__restrict__ bvh_tris, const uint32_t *__restrict__ bvh_ids)
+    const FaceShade *__restrict__ shade, const Bvh4Node *__restrict__ bvh_nodes,
+    const TriRecord *__restrict__ bvh_tris)
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ int32_t bvh_stack[kBvhStack * kBlock];     // traversal stacks, column per thread
     path_body<false, true, RVCP_BVH_SINGLE>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
-                           shade, tail_tab, nullptr, bvh_nodes, bvh_tris, bvh_ids,
+                           shade, tail_tab, nullptr, bvh_nodes, bvh_tris,
                            bvh_stack + threadIdx.x);
 }
 
@@ -1614,8 +1646,8 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                                        uint32_t *out_rgba, float *out_lin,
                                        unsigned long long *counters, rvcp::SurfRecord *surf,
                                        const rvcp::FaceShade *shade,
-                                       const rvcp::BvhNode *bvh_nodes,
-                                       const rvcp::TriRecord *bvh_tris, const uint32_t *bvh_ids,
+                                       const rvcp::Bvh4Node *bvh_nodes,
+                                       const rvcp::TriRecord *bvh_tris,
                                        uint32_t grid_blocks, void *stream, void *main_event)
 {
     const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
@@ -1623,13 +1655,13 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
     hipLaunchKernelGGL(pre, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
                        (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
                        (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
-                       surf, shade, bvh_nodes, bvh_tris, bvh_ids);
+                       surf, shade, bvh_nodes, bvh_tris);
     if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
         return -2;
     if (args->accel)
         hipLaunchKernelGGL(rvcp::games101_bvh_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
-                           out_lin, counters, surf, shade, bvh_nodes, bvh_tris, bvh_ids);
+                           out_lin, counters, surf, shade, bvh_nodes, bvh_tris);
     else if (args->variant == 5)
         hipLaunchKernelGGL(rvcp::games101_tiled_single_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
