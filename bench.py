@@ -11,6 +11,8 @@ once, before timing (inputs resident in HBM).
 Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
   c3: Cornell 1024x1024 SPP=30.  For N>1 the frame grows with N at fixed SPP
       (side = round8(1024*sqrt(N))), so per-GPU work stays ~C3: "scaling": "weak".
+  c1: Cornell 128x128 SPP=1 (BASELINE configs[0], the CPU plumbing case; its cpu_baseline is
+      the whole frame).
   c2: Cornell 384x384 SPP=10 (README benchmark row).
   c4: Cornell 2048x2048 SPP=64, fixed frame sharded over N GPUs ("scaling": "strong").
   c5: Cornell + 100k random triangles, 1024x1024 SPP=30.
@@ -52,6 +54,9 @@ def workload(name, n_gpus):
         return dict(workload="cornell_1024sq_spp30" if n_gpus == 1 else
                     f"cornell_{side}sq_spp30_weak", W=side, H=side, spp=30, extra_tris=0,
                     scaling="weak")
+    if name == "c1":
+        return dict(workload="cornell_128sq_spp1", W=128, H=128, spp=1, extra_tris=0,
+                    scaling="strong")
     if name == "c2":
         return dict(workload="cornell_384sq_spp10", W=384, H=384, spp=10, extra_tris=0,
                     scaling="strong")
@@ -95,6 +100,17 @@ def load_traffic(workload_name, kernel_substr):
     return None, None
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(sc, cfg_kw, W, H, threads):
     """Time the CPU oracle (scalar C re-execution) on a bounded sample of the workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -115,14 +131,15 @@ def cpu_baseline(sc, cfg_kw, W, H, threads):
                  threads=threads, want_linear=False)
         dt = time.perf_counter() - t0
         return dict(value=128 * 128 / dt / 1e6, unit="Msamples/s", cores=threads, kind="port",
-                    sample="128x128 SPP=1 frame of the same scene", seconds=round(dt, 3))
+                    sample="128x128 SPP=1 frame of the same scene", seconds=round(dt, 3),
+                    cpu=cpu_model())
     # the whole frame on `threads` threads (a few seconds), then a single-thread figure on
     # every 64th row
     t0 = time.perf_counter()
     O.render(arrays, push, cfg, W, H, threads=threads, want_linear=False)
     dt = time.perf_counter() - t0
     samples = W * H * cfg_kw["spp"]
-    rows1 = list(range(0, H, 64))
+    rows1 = list(range(0, H, 64 if H >= 256 else 8))
     t1 = time.perf_counter()
     for y in rows1:
         O.render(arrays, push, cfg, W, H, rect=(0, y, W, 1), threads=1, want_linear=False)
@@ -131,8 +148,8 @@ def cpu_baseline(sc, cfg_kw, W, H, threads):
                 sample=f"the full {W}x{H} SPP={cfg_kw['spp']} frame on {threads} threads",
                 seconds=round(dt, 3),
                 single_thread_value=round(len(rows1) * W * cfg_kw["spp"] / dt1 / 1e6, 4),
-                single_thread_sample=f"every 64th row ({len(rows1)} rows), 1 thread",
-                single_thread_seconds=round(dt1, 3))
+                single_thread_sample=f"every {64 if H >= 256 else 8}th row ({len(rows1)} rows), 1 thread",
+                single_thread_seconds=round(dt1, 3), cpu=cpu_model())
 
 
 def main():
@@ -140,7 +157,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5", "spheres"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5", "spheres"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--save-frame", default="")
@@ -221,8 +238,11 @@ def main():
     torch.cuda.synchronize()
     kernel_ms, main_ms, trav, trav_exec = [], [], 0, 0
     t0 = time.perf_counter()
+    step_ms = []
     for _ in range(args.steps):
+        ts = time.perf_counter()
         st = step()
+        step_ms.append((time.perf_counter() - ts) * 1000.0)
         kernel_ms.append(float(st["kernel_ms"]))
         main_ms.append(float(st["main_kernel_ms"]))
         trav += int(st["traversals"])
@@ -281,6 +301,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(1000.0 / ms_per_step, 2),
+            "frame_ms_median": round(float(np.median(step_ms)), 4),
             "higher_is_better": True,
             "scaling": wl["scaling"],
             "vs_baseline": (round(value / REFERENCE_MSAMPLES[args.workload], 2)

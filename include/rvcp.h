@@ -294,6 +294,17 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
 /* Wait for the last async render of ctx and fetch its statistics. */
 int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats);
 
+/* The asynchronous pair of SURVEY.md §8(b) (the reference's per-image fences,
+ * vulkan.rs:367-369, 392-401): enqueue one full frame into DEVICE memory on `stream` (NULL:
+ * the context's own stream) and return; rvcp_wait blocks until it is done and fills stats.
+ * d_rgba8: W*H*4 bytes, d_linear_rgb (optional): W*H*3 floats, as rvcp_render.  Equivalent to
+ * rvcp_render_shard_async(..., 0, 1, ...) / rvcp_sync_stats.  One GPU: a context with
+ * n_gpus > 1 returns RVCP_E_UNSUPPORTED (use rvcp_render). */
+int rvcp_render_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
+                      uint32_t width, uint32_t height,
+                      void *d_rgba8, void *d_linear_rgb, void *stream);
+int rvcp_wait(rvcp_ctx_t *ctx, rvcp_stats_t *stats);
+
 /* Rows of an H-row frame owned by shard `shard_index` of `shard_count`. */
 uint32_t rvcp_shard_rows(uint32_t height, uint32_t shard_index, uint32_t shard_count);
 

@@ -38,7 +38,7 @@ RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E
 EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "rvcp_create",
             "rvcp_destroy", "rvcp_last_error", "rvcp_upload_scene", "rvcp_render", "rvcp_render_shard_async",
             "rvcp_sync_stats", "rvcp_shard_rows", "rvcp_assemble_frame_async",
-            "rvcp_upload_scene_file", "rvcp_mandelbrot"]
+            "rvcp_upload_scene_file", "rvcp_mandelbrot", "rvcp_render_async", "rvcp_wait"]
 
 
 # Integrator mode 2 (ray_tracer.comp ray_trace): its own #defines (ray_tracer.comp:5-13).
@@ -110,12 +110,15 @@ def load():
     L.rvcp_render.argtypes = [P, P, u32, u32, P, P, P]
     L.rvcp_render_shard_async.argtypes = [P, P, u32, u32, u32, u32, P, P, P]
     L.rvcp_sync_stats.argtypes = [P, P]
+    L.rvcp_render_async.argtypes = [P, P, u32, u32, P, P, P]
+    L.rvcp_wait.argtypes = [P, P]
     L.rvcp_shard_rows.argtypes = [u32, u32, u32]
     L.rvcp_shard_rows.restype = u32
     L.rvcp_assemble_frame_async.argtypes = [P, P, u32, u32, u32, u32, P, P]
     for name in ("rvcp_config_default", "rvcp_config_default_for", "rvcp_create", "rvcp_destroy", "rvcp_upload_scene",
                  "rvcp_render", "rvcp_render_shard_async", "rvcp_sync_stats",
-                 "rvcp_assemble_frame_async", "rvcp_upload_scene_file", "rvcp_mandelbrot"):
+                 "rvcp_assemble_frame_async", "rvcp_upload_scene_file", "rvcp_mandelbrot",
+                 "rvcp_render_async", "rvcp_wait"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -708,6 +708,20 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     return RVCP_OK;
 }
 
+int rvcp_render_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+                      uint32_t height, void *d_rgba8, void *d_linear_rgb, void *stream)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!ctx->subs.empty())
+        return fail(ctx, RVCP_E_UNSUPPORTED, "rvcp_render_async drives one GPU; use rvcp_render for n_gpus > 1");
+    return rvcp_render_shard_async(ctx, push, width, height, 0, 1, d_rgba8, d_linear_rgb, stream);
+}
+
+int rvcp_wait(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
+{
+    return rvcp_sync_stats(ctx, stats);
+}
+
 int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
 {
     if (!ctx) return RVCP_E_INVALID;
@@ -740,6 +754,7 @@ int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         }
         ctx->last_timeline_waves = 0;
     }
+    ctx->pending = false;           // a render is waited for once
     return RVCP_OK;
 }
 

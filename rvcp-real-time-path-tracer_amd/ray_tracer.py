@@ -148,6 +148,22 @@ class RayTracer:
             ctypes.c_void_p(d_rgba), ctypes.c_void_p(d_linear) if d_linear else None,
             ctypes.c_void_p(stream) if stream else None))
 
+    def render_async(self, push, width, height, d_rgba: int, d_linear: int = 0, stream: int = 0):
+        """rvcp_render_async: enqueue one full frame into device memory; see wait()."""
+        push = np.ascontiguousarray(push, dtype=PUSH_DTYPE)
+        self._push_keepalive = push
+        self._check(self._lib.rvcp_render_async(
+            self._ctx, abi.ptr(push), width, height, ctypes.c_void_p(d_rgba),
+            ctypes.c_void_p(d_linear) if d_linear else None,
+            ctypes.c_void_p(stream) if stream else None))
+
+    def wait(self):
+        """rvcp_wait: block until the last async render is done; returns its stats."""
+        stats = np.zeros((), dtype=abi.STATS_DTYPE)
+        self._check(self._lib.rvcp_wait(self._ctx, abi.ptr(stats)))
+        self.last_stats = stats
+        return stats
+
     def sync_stats(self):
         stats = np.zeros((), dtype=abi.STATS_DTYPE)
         self._check(self._lib.rvcp_sync_stats(self._ctx, abi.ptr(stats)))

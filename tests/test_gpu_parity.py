@@ -231,6 +231,32 @@ def test_shard_assembly_bitexact(cornell, n_shards):
     assert np.array_equal(got, full)
 
 
+def test_render_async_wait(cornell):
+    """rvcp_render_async / rvcp_wait (device output, caller's stream) == rvcp_render."""
+    torch = pytest.importorskip("torch")
+    W, H = 77, 45
+    cfg = rvcp_amd.abi.make_config(spp=3)
+    with rvcp_amd.RayTracer(cfg) as rt:
+        rt.upload_scene(cornell)
+        full, lin = rt.render(W, H, TIME, want_linear=True)
+        st_sync = rt.last_stats
+        d_rgba = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+        d_lin = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+        rt.render_async(cornell.push_constant(TIME), W, H, d_rgba.data_ptr(), d_lin.data_ptr(),
+                        stream=torch.cuda.current_stream().cuda_stream)
+        st = rt.wait()
+        with pytest.raises(rvcp_amd.abi.RvcpError):
+            rt.wait()                   # nothing in flight any more
+    assert np.array_equal(d_rgba.cpu().numpy().view(np.uint8).reshape(H, W, 4), full)
+    assert np.array_equal(d_lin.cpu().numpy().view(np.uint32), lin.view(np.uint32))
+    assert int(st["traversals"]) == int(st_sync["traversals"])
+    with rvcp_amd.RayTracer(rvcp_amd.abi.make_config(spp=1, n_gpus=2)) as rt:
+        rt.upload_scene(cornell)
+        with pytest.raises(rvcp_amd.abi.RvcpError) as e:
+            rt.render_async(cornell.push_constant(TIME), W, H, d_rgba.data_ptr())
+        assert e.value.code == rvcp_amd.abi.RVCP_E_UNSUPPORTED
+
+
 @pytest.mark.parametrize("n_gpus", [2, 3, 8])
 @pytest.mark.parametrize("W,H,spp", [(64, 64, 2), (37, 29, 3), (130, 3, 2), (256, 200, 1)])
 def test_single_process_multi_gpu(cornell, n_gpus, W, H, spp):
