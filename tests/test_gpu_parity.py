@@ -150,6 +150,21 @@ def test_upload_validation(cornell):
             rt.render_push(cornell.push_constant(TIME), 8, 8)   # no scene uploaded yet
 
 
+def test_frame_size_limits(cornell):
+    """W*H must be in [1, 2^31): rejected with RVCP_E_INVALID before any allocation; the
+    context stays usable."""
+    torch = pytest.importorskip("torch")
+    d = torch.zeros(16, dtype=torch.int32, device="cuda")
+    with rvcp_amd.RayTracer(spp=1) as rt:
+        rt.upload_scene(cornell)
+        push = cornell.push_constant(TIME)
+        for W, H in [(65536, 32768), (0, 16), (16, 0)]:
+            with pytest.raises(rvcp_amd.abi.RvcpError) as e:
+                rt.render_async(push, W, H, d.data_ptr())
+            assert e.value.code == rvcp_amd.abi.RVCP_E_INVALID
+        assert rt.render(4, 4, TIME).shape == (4, 4, 4)
+
+
 # ----------------------------------------------------------------------------------------
 # Full-size (C3: 1024^2, SPP=30) properties
 # ----------------------------------------------------------------------------------------
