@@ -9,7 +9,8 @@
  *
  * It is written independently of the HIP kernel: it follows the GLSL function by function
  * (each function cites the shader line it restates) and shares with the kernel only the
- * numeric contract of DESIGN.md §3 (float32 everywhere, no FMA contraction, IEEE
+ * numeric contract of DESIGN.md §3 (float32 everywhere, no implicit contraction, the
+ * builtins dot and cross as explicit fma chains, IEEE
  * correctly-rounded + - * / sqrt, the software sin below, the gamma threshold table).
  *
  * Parity pinning: the reference ships no tests and no golden vectors.  The
@@ -60,9 +61,12 @@ static inline v3 mulv(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); 
 static inline v3 muls(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 static inline v3 divs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 static inline v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
-static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* The builtins dot and cross are fused chains: GLSL leaves their internal
+ * rounding to the implementation; arithmetic the shader writes out stays unfused. */
+static inline float dot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 static inline v3 cross(v3 a, v3 b) {
-    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    return mk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)),
+              fmaf(a.x, b.y, -(a.y * b.x)));
 }
 static inline float length(v3 a) { return sqrtf(dot(a, a)); }
 /* GLSL normalize(v) restated as v * (1 / sqrt(dot(v, v))). */

@@ -110,8 +110,12 @@ inline h3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 inline h3 add(h3 a, h3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 inline h3 sub(h3 a, h3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 inline h3 muls(h3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
-inline float dot(h3 a, h3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-inline h3 cross(h3 a, h3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+// the shader builtins, fused as in DESIGN.md §3.1 (these restate shader code, not glam)
+inline float dot(h3 a, h3 b) { return std::fma(a.z, b.z, std::fma(a.y, b.y, a.x * b.x)); }
+inline h3 cross(h3 a, h3 b) {
+    return mk(std::fma(a.y, b.z, -(a.z * b.y)), std::fma(a.z, b.x, -(a.x * b.z)),
+              std::fma(a.x, b.y, -(a.y * b.x)));
+}
 inline float length(h3 a) { return std::sqrt(dot(a, a)); }
 inline h3 normalize(h3 a) { return muls(a, 1.0f / std::sqrt(dot(a, a))); }
 inline void st3(float *d, h3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; }

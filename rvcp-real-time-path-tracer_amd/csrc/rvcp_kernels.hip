@@ -20,8 +20,9 @@
 //  * The hit record (interpolated normal, material) is resolved once per traversal, for the
 //    nearest face only.
 //
-// Numerics: float32, no contraction (-ffp-contract=off), IEEE correctly
-// rounded division and sqrt, the software sin of the contract, so every pixel is
+// Numerics: float32, no implicit contraction (-ffp-contract=off; the
+// builtins dot/cross are explicit fma chains), IEEE correctly rounded division and sqrt,
+// the software sin of the contract, so every pixel is
 // bit-identical to oracle/rvcp_oracle.c whichever variant runs.
 #include <hip/hip_runtime.h>
 
@@ -42,9 +43,15 @@ __device__ __forceinline__ f3 mulv(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y,
 __device__ __forceinline__ f3 muls(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ f3 divs(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// The GLSL builtins dot and cross as fused chains: dot = fma(z, z',
+// fma(y, y', x*x')), cross_i = fma(a_j, b_k, -(a_k*b_j)).  Arithmetic written out in the
+// shader source stays unfused.
+__device__ __forceinline__ float dot(f3 a, f3 b) {
+    return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+}
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
-    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    return mk(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+              __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
 }
 __device__ __forceinline__ float len(f3 a) { return __builtin_sqrtf(dot(a, a)); }
 __device__ __forceinline__ f3 normalize(f3 a) { return muls(a, 1.0f / __builtin_sqrtf(dot(a, a))); }
@@ -126,20 +133,44 @@ __device__ __forceinline__ void store_pixel(uint32_t pix, f3 acc, const FrameArg
 }
 
 // One exact ray-triangle test (is_intersect_with_face, :238-260) with the nearest-hit rule
-// of get_intersection_with_scene (:291): accept iff the shader would replace the current
-// nearest hit whose time is `bt`.  5-compare form, DESIGN.md §3.5.
-__device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float tmin, float bt,
-                                           float &t_out) {
+// of get_intersection_with_scene (:291), in two stages.  Stage 1: the products that do not
+// need 1/den -- s = o - v0, s1 = d x e2, s2 = s x e1, den = s1.e1, n1 = s1.s, n2 = s2.d.
+struct TriPart {
+    f3 s2;
+    float den, n1, n2;
+};
+__device__ __forceinline__ TriPart tri_stage1(const TriRecord &T, f3 o, f3 d) {
     const f3 s = mk(o.x - T.v0[0], o.y - T.v0[1], o.z - T.v0[2]);
-    const f3 e1 = ld3(T.e1), e2 = ld3(T.e2);
-    const f3 s1 = cross(d, e2);
-    const f3 s2 = cross(s, e1);
-    const float f = rcp_ieee(dot(s1, e1));
-    const float t = f * dot(s2, e2);
-    const float b1 = f * dot(s1, s);
-    const float b2 = f * dot(s2, d);
+    const f3 e1 = ld3(T.e1);
+    const f3 s1 = cross(d, ld3(T.e2));
+    TriPart P;
+    P.s2 = cross(s, e1);
+    P.den = dot(s1, e1);
+    P.n1 = dot(s1, s);
+    P.n2 = dot(P.s2, d);
+    return P;
+}
+// Stage 2: f = 1/den, t = f (s2.e2), b1 = f n1, b2 = f n2 (:254-257); accept iff the shader
+// would replace the current nearest hit whose time is `bt`.  5-compare form, DESIGN.md §3.5.
+__device__ __forceinline__ bool tri_stage2(const TriRecord &T, const TriPart &P, float tmin,
+                                           float bt, float &t_out) {
+    const float f = rcp_ieee(P.den);
+    const float t = f * dot(P.s2, ld3(T.e2));
+    const float b1 = f * P.n1;
+    const float b2 = f * P.n2;
     t_out = t;
     return (b1 >= 0.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f) & (t >= tmin) & (t <= bt);
+}
+__device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float tmin, float bt,
+                                           float &t_out) {
+    return tri_stage2(T, tri_stage1(T, o, d), tmin, bt, t_out);
+}
+// A necessary condition for tri_stage2 to accept, from stage 1 alone: |n1| and |n2| at most
+// RN(|den| (1 + 2^-20)) (proof: DESIGN.md §4.2).  A wave skips stage 2 of a triangle when no
+// lane passes it; no result changes.
+__device__ __forceinline__ bool tri_maybe(const TriPart &P) {
+    const float m = __builtin_fabsf(P.den) * 1.00000095367431640625f;     // 1 + 2^-20
+    return (__builtin_fabsf(P.n1) <= m) & (__builtin_fabsf(P.n2) <= m);
 }
 
 // Opt-in BVH (RVCP_ACCEL_BVH): nearest hit of ray (o, d) over the tree, with the scan's exact
@@ -1144,14 +1175,23 @@ __device__ __forceinline__ void path_body(
                         }
                     }
                 } else if (wave_active) {
-                    // (a software-pipelined read of the next triangle costs 12 VGPRs and was
-                    // slower once the kernel is held to 4 waves/SIMD)
-#pragma unroll 2
+                    // Two-stage exact test: stage 2 (1/den, t, b1, b2, the
+                    // compares) only when some lane may accept.  (A software-pipelined read of
+                    // the next triangle costs 12 VGPRs and was slower at 4 waves/SIMD.)
                     for (uint32_t i = 0; i < n; ++i) {
                         const TriRecord T = tile[i];
-                        float tA, tB;
-                        if (tri_accept(T, s_ao, s_ad, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
-                        if (!SINGLE && tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
+                        const TriPart PA = tri_stage1(T, s_ao, s_ad);
+                        if (__any(sA && tri_maybe(PA))) {
+                            float tA;
+                            if (tri_stage2(T, PA, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
+                        }
+                        if (!SINGLE) {
+                            const TriPart PB = tri_stage1(T, b_o, b_d);
+                            if (__any(sB && tri_maybe(PB))) {
+                                float tB;
+                                if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
+                            }
+                        }
                     }
                 }
                 __syncthreads();
@@ -1229,11 +1269,6 @@ __device__ __forceinline__ void path_body(
                 if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
                 if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
             }
-        }
-
-        if (SINGLE && !hasA) {          // the lane traced its path ray
-            btB = btA;
-            bestB = bestA;
         }
 
         if (SINGLE && !hasA) {          // the lane traced its path ray

@@ -45,6 +45,27 @@ def f32_round(q: Fraction) -> np.float32:
 
 
 def fma(a, b, c) -> np.float32:
+    """float32 fma, one rounding.  a*b is exact in float64; the float64 sum's rounding error is
+    recovered exactly (TwoSum), which settles the one case double rounding can get wrong: a
+    float64 sum lying exactly on a float32 rounding midpoint."""
+    a, b, c = float(a), float(b), float(c)
+    p = a * b
+    s = p + c
+    r = F(s)
+    if not np.isfinite(s) or float(r) == s:
+        return r
+    bp = s - p
+    err = (p - (s - bp)) + (c - bp)
+    if err == 0.0:
+        return r
+    other = np.nextafter(r, F(np.inf) if s > float(r) else F(-np.inf))
+    if (float(r) + float(other)) * 0.5 == s:          # a midpoint: the lost error decides
+        return other if (err > 0.0) == (float(other) > float(r)) else r
+    return r
+
+
+def fma_exact(a, b, c) -> np.float32:
+    """fma by rational arithmetic (cross-check of fma above)."""
     return f32_round(Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c)))
 
 
@@ -93,12 +114,13 @@ def mul(a, b): return (F(a[0] * b[0]), F(a[1] * b[1]), F(a[2] * b[2]))
 def scale(a, s): return (F(a[0] * s), F(a[1] * s), F(a[2] * s))
 def div(a, s): return (F(a[0] / s), F(a[1] / s), F(a[2] / s))
 def neg(a): return (F(-a[0]), F(-a[1]), F(-a[2]))
-def dot(a, b): return F(F(F(a[0] * b[0]) + F(a[1] * b[1])) + F(a[2] * b[2]))
+# the builtins dot / cross as fused chains
+def dot(a, b): return fma(a[2], b[2], fma(a[1], b[1], F(a[0] * b[0])))
 
 
 def cross(a, b):
-    return (F(F(a[1] * b[2]) - F(a[2] * b[1])), F(F(a[2] * b[0]) - F(a[0] * b[2])),
-            F(F(a[0] * b[1]) - F(a[1] * b[0])))
+    return (fma(a[1], b[2], F(-F(a[2] * b[1]))), fma(a[2], b[0], F(-F(a[0] * b[2]))),
+            fma(a[0], b[1], F(-F(a[1] * b[0]))))
 
 
 def length(a): return F(np.sqrt(dot(a, a)))

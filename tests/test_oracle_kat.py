@@ -38,6 +38,27 @@ def test_sin_bitexact_vs_pyref():
         assert bits(O.sinf(float(x))) == bits(pyref.sinf(x)), x
 
 
+def test_pyref_fma_single_rounding():
+    """pyref's float64+TwoSum fma equals the rational-arithmetic fma, including inputs whose
+    float64 sum lands exactly on a float32 rounding midpoint."""
+    rng = np.random.default_rng(9)
+    cases = [tuple(F(x) for x in rng.uniform(-1e3, 1e3, 3)) for _ in range(3000)]
+    cases += [tuple(F(x) for x in rng.standard_normal(3) * 10.0 ** rng.integers(-20, 20, 3))
+              for _ in range(3000)]
+    # midpoint traps: a*b = 1 + 2^-24 + 2^-35 exactly; with c = -2^-35 +/- 2^-58 the exact sum is
+    # 1 + 2^-24 +/- 2^-58, whose float64 rounding is the float32 midpoint 1 + 2^-24
+    a, b = F(1.0 + 2.0 ** -12), F(1.0 - 2.0 ** -12 + 2.0 ** -23)
+    traps = [(a, b, F(-2.0 ** -35 + 2.0 ** -58)), (a, b, F(-2.0 ** -35 - 2.0 ** -58)),
+             (F(-a), b, F(2.0 ** -35 - 2.0 ** -58)), (a, b, F(-2.0 ** -35))]
+    assert float(pyref.fma(*traps[0])) == 1.0 + 2.0 ** -23
+    assert float(pyref.fma(*traps[1])) == 1.0
+    cases += traps
+    for a, b, c in cases:
+        assert bits(pyref.fma(a, b, c)) == bits(pyref.fma_exact(a, b, c)), (a, b, c)
+    assert np.isnan(pyref.fma(F(np.inf), F(0.0), F(1.0)))
+    assert pyref.fma(F(np.inf), F(2.0), F(1.0)) == np.inf
+
+
 def test_sin_special_values():
     assert math.isnan(O.sinf(float("inf"))) and math.isnan(O.sinf(float("nan")))
     assert O.sinf(0.0) == 0.0
