@@ -51,6 +51,7 @@ for s in $STEPS; do
         rehearse4) run rehearse4 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 4 --steps 3 --warmup 1 ;;
         rcp) run rcp_check 120 tools/build/rcp_check ;;
         rcp2) run rcp_check2 300 tools/build/rcp_check2 ;;
+        valu) run valu_rate 120 tools/build/valu_rate ;;
         pretest) run pretest_check 300 tools/build/pretest_check ;;
         split) run split 300 python tools/exp_split.py ;;
         split2) run split2 300 env RVCP_KERNEL_VARIANT=2 python tools/exp_split.py ;;

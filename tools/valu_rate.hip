@@ -1,0 +1,107 @@
+// valu_rate.hip -- issue rate of v_fma_f32 vs v_pk_fma_f32 (and v_pk_add/mul_f32) on gfx950,
+// all SIMDs busy, 8 waves per SIMD, 8 independent chains per lane.  Prints wave-instructions
+// per SIMD per clock (from the measured time and the shader clock read by s_memrealtime /
+// the kernel's wall time) and the lane-FLOP rate.
+//   make -C tools build/valu_rate && tools/build/valu_rate
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+constexpr int kIters = 4096;
+
+#define FMA8(op)                                                                          \
+    asm volatile(op " %0, %0, %8, %9\n\t" op " %1, %1, %8, %9\n\t" op " %2, %2, %8, %9\n\t"  \
+                 op " %3, %3, %8, %9\n\t" op " %4, %4, %8, %9\n\t" op " %5, %5, %8, %9\n\t"   \
+                 op " %6, %6, %8, %9\n\t" op " %7, %7, %8, %9"                                \
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6),    \
+                   "+v"(a7)                                                                   \
+                 : "v"(m), "v"(c))
+
+__global__ void k_fma(float *out, float seed) {
+    float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+          a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const float m = 0.999f, c = 1e-3f;
+    for (int i = 0; i < kIters; i++) { FMA8("v_fma_f32"); }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+__global__ void k_pkfma(float *out, float seed) {
+    v2f a0 = {seed + threadIdx.x, seed}, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+        a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const v2f m = {0.999f, 0.998f}, c = {1e-3f, 2e-3f};
+    for (int i = 0; i < kIters; i++) { FMA8("v_pk_fma_f32"); }
+    const v2f s = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s.x + s.y;
+}
+
+#define ADD8(op)                                                                          \
+    asm volatile(op " %0, %0, %8\n\t" op " %1, %1, %8\n\t" op " %2, %2, %8\n\t"              \
+                 op " %3, %3, %8\n\t" op " %4, %4, %8\n\t" op " %5, %5, %8\n\t"               \
+                 op " %6, %6, %8\n\t" op " %7, %7, %8"                                        \
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6),    \
+                   "+v"(a7)                                                                   \
+                 : "v"(m))
+
+__global__ void k_add(float *out, float seed) {
+    float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+          a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const float m = 1e-3f;
+    for (int i = 0; i < kIters; i++) { ADD8("v_add_f32"); }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
+__global__ void k_pkadd(float *out, float seed) {
+    v2f a0 = {seed + threadIdx.x, seed}, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+        a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const v2f m = {1e-3f, 2e-3f};
+    for (int i = 0; i < kIters; i++) { ADD8("v_pk_add_f32"); }
+    const v2f s = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s.x + s.y;
+}
+
+__global__ void k_pkmul(float *out, float seed) {
+    v2f a0 = {seed + threadIdx.x, seed}, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+        a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const v2f m = {0.999f, 0.998f};
+    for (int i = 0; i < kIters; i++) { ADD8("v_pk_mul_f32"); }
+    const v2f s = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s.x + s.y;
+}
+
+template <typename K>
+static void run(const char *name, K kern, int lanes_per_instr, int flops_per_lane, float *out,
+                int blocks, int threads) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, out, 1.0f);   // warm
+    (void)hipEventRecord(a);
+    for (int r = 0; r < 5; r++) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, out, 1.0f);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    const double s = ms * 1e-3 / 5;
+    const double waves = (double)blocks * threads / 64;
+    const double winstr = waves * kIters * 8;
+    const double simds = 256.0 * 4;
+    const double clk = 2.4e9;
+    std::printf("%-14s %8.3f ms  wave-instr/SIMD/clk(@2.4GHz) %.3f  cycles/instr %.2f  "
+                "TFLOP/s %.1f\n",
+                name, s * 1e3, winstr / simds / (s * clk), simds * s * clk / winstr,
+                winstr * 64 * lanes_per_instr * flops_per_lane / s * 1e-12);
+}
+
+int main() {
+    const int threads = 256, blocks = 256 * 8;   // 8 waves per SIMD
+    float *out = nullptr;
+    if (hipMalloc(&out, sizeof(float) * threads * blocks) != hipSuccess) return 2;
+    run("v_fma_f32", k_fma, 1, 2, out, blocks, threads);
+    run("v_pk_fma_f32", k_pkfma, 2, 2, out, blocks, threads);
+    run("v_add_f32", k_add, 1, 1, out, blocks, threads);
+    run("v_pk_add_f32", k_pkadd, 2, 1, out, blocks, threads);
+    run("v_pk_mul_f32", k_pkmul, 2, 1, out, blocks, threads);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 2;
+}
