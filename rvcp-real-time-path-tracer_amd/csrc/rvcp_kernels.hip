@@ -54,7 +54,9 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
               __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
 }
 __device__ __forceinline__ float len(f3 a) { return __builtin_sqrtf(dot(a, a)); }
-__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, 1.0f / __builtin_sqrtf(dot(a, a))); }
+// 1 / sqrt by rcp_ieee below (the IEEE quotient, fast path verified over all inputs)
+__device__ __forceinline__ float rcp_ieee(float den);
+__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, rcp_ieee(__builtin_sqrtf(dot(a, a)))); }
 __device__ __forceinline__ float fractf(float x) { return x - __builtin_floorf(x); }
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 
@@ -79,6 +81,27 @@ __device__ __forceinline__ float pt_sinf(float x) {
     return (j & 2) ? -v : v;
 }
 
+// pt_sinf for rand()'s arguments only: seed + index with seed in [0, 1] (a fract) and index a
+// float counter that stops growing at 2^24, so x lies in [1, 2^24 + 4]: finite and positive,
+// q = rint(x * 2/pi) < 2^24 is an exact integer, and (int)q & 3 equals q - 4 floor(q / 4).
+// The same arithmetic as pt_sinf without its range guard and with the integer quadrant
+// (6 fewer VALU instructions per rand()).
+__device__ __forceinline__ float pt_sinf_rand(float x) {
+    const float q = __builtin_rintf(x * 0.636619772367581343f);
+    float r = __builtin_fmaf(q, -1.57079637050628662109375f, x);
+    r = __builtin_fmaf(q, 4.37113900018624283e-8f, r);
+    const float z = r * r;
+    const float ps = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
+                                    -1.6666654611e-1f);
+    const float s = __builtin_fmaf(ps, z * r, r);
+    const float pc = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f),
+                                    z, 4.166664568298827e-2f);
+    const float c = __builtin_fmaf(pc, z * z, __builtin_fmaf(-0.5f, z, 1.0f));
+    const int j = (int)q;
+    const float v = (j & 1) ? c : s;
+    return (j & 2) ? -v : v;
+}
+
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
@@ -90,7 +113,7 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
 // rand(), :159-162: index += 1; fract(sin(seed + index) * 43758.5453)
 __device__ __forceinline__ float rnd(float seed, float &idx) {
     idx = idx + 1.0f;
-    return fractf(pt_sinf(seed + idx) * 43758.5453f);
+    return fractf(pt_sinf_rand(seed + idx) * 43758.5453f);
 }
 
 // 1 / den, IEEE round-to-nearest (the shader's `1.0 / dot(s1, e1)`, :254).
@@ -464,9 +487,9 @@ __device__ __forceinline__ void coop_unit_sphere(bool need, float seed, float &r
         const int owner = worker ? (int)tab[j] : (int)lane;
         const float s_seed = __shfl(seed, owner);
         const float base = __shfl(ridx, owner) + (float)(3u * c);
-        const float rx = fractf(pt_sinf(s_seed + (base + 1.0f)) * 43758.5453f);
-        const float ry = fractf(pt_sinf(s_seed + (base + 2.0f)) * 43758.5453f);
-        const float rz = fractf(pt_sinf(s_seed + (base + 3.0f)) * 43758.5453f);
+        const float rx = fractf(pt_sinf_rand(s_seed + (base + 1.0f)) * 43758.5453f);
+        const float ry = fractf(pt_sinf_rand(s_seed + (base + 2.0f)) * 43758.5453f);
+        const float rz = fractf(pt_sinf_rand(s_seed + (base + 3.0f)) * 43758.5453f);
         const f3 p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
         const uint64_t AM = __ballot(worker && !(dot(p, p) >= 1.0f));
         const uint64_t segmask = K >= 64u ? ~0ull : ((1ull << K) - 1ull);
