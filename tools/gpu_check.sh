@@ -71,6 +71,8 @@ for s in $STEPS; do
         c5var) run c5var 1100 bash -c 'for v in tools/build/var_*/librvcp.so; do echo "$v"; RVCP_LIB=$v python tools/frames.py --frames 2 --tris 100000 || exit 1; done' ;;
         benchc5bvh) run bench_c5_bvh 600 python bench.py --workload c5 --steps 3 --warmup 1 --accel bvh --no-cpu-baseline ;;
         benchc5) run bench_c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
+        benchc4) run bench_c4 300 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        c5pmcall) run c5pmcall 900 bash tools/c5_pmc.sh ;;
         benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 ;;
         profs) run profs 600 rocprofv3 --kernel-trace --stats -d "$OUT/profs_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 20 --warmup 2 --no-cpu-baseline ;;
         pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
