@@ -73,17 +73,18 @@ def workload(name, n_gpus):
 
 
 def load_valu_busy(workload_name, kernel_substr):
-    """VALU issue utilisation of the dominant kernel from the newest committed SQ PMC summary."""
+    """VALU issue utilisation of the dominant kernel from the newest committed SQ PMC summary:
+    (busy at 2 cycles per wave64 instruction, fraction of the measured issue peak)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_valu_{workload_name}.json")))
     if not files:
-        return None
+        return None, None
     with open(files[-1]) as f:
         d = json.load(f)
     for name, k in d.get("kernels", {}).items():
         if kernel_substr in name:
-            return k.get("valu_busy")
-    return None
+            return k.get("valu_busy"), k.get("issue_frac")
+    return None, None
 
 
 def load_traffic(workload_name, kernel_substr):
@@ -277,7 +278,7 @@ def main():
     kname = ("legacy_kernel" if legacy else "games101_bvh_path_kernel" if args.accel == "bvh"
              else "games101_tiled_single_kernel" if n_faces >= 256 else "games101_path_kernel")
     traffic, traffic_src = load_traffic(wl["workload"], kname)
-    valu_busy = load_valu_busy(wl["workload"], kname)
+    valu_busy, valu_issue_frac = load_valu_busy(wl["workload"], kname)
 
     frame_check = None
     if world > 1 and rank == 0:
@@ -332,6 +333,7 @@ def main():
                          "valu_tflops": round(tests_per_s * FLOP_PER_TEST / 1e12, 2),
                          "valu_frac": round(tests_per_s * FLOP_PER_TEST / 1e12 / FP32_PEAK_TFLOPS, 4),
                          "valu_busy_pmc": valu_busy,
+                         "valu_issue_frac_pmc": valu_issue_frac,
                          "executed_tests_per_s": round(exec_tests_per_s, 1)},
             "cpu_baseline": None,
         }

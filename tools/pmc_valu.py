@@ -4,8 +4,14 @@
   valu_busy = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction occupies a SIMD for two
               cycles on CDNA4, MI355X_MICROARCH.md) / (GRBM_GUI_ACTIVE per XCD x SIMDs)
 
+  issue_frac = (SQ_INSTS_VALU / (cycles x SIMDs)) / 0.35, the wave-instructions per SIMD per
+              clock the chip sustains on independent v_fma_f32 / v_add_f32 streams with every
+              SIMD full (tools/valu_rate.hip, profiles/r01_valu_rate.log): how close the kernel
+              is to the VALU issue rate actually reachable
+
 GRBM_GUI_ACTIVE is summed over the 8 XCDs by rocprofv3, so it is divided by 8 to get the
-kernel's cycles.  Writes the JSON bench.py reads into roofline.valu_busy.
+kernel's cycles.  Writes the JSON bench.py reads into roofline.valu_busy_pmc /
+roofline.valu_issue_frac_pmc.
 
   python tools/pmc_valu.py SQ.csv GRBM.csv OUT.json --workload NAME [--simds 1024 --xcds 8]
 """
@@ -33,17 +39,21 @@ def main():
     ap.add_argument("--workload", required=True)
     ap.add_argument("--simds", type=int, default=1024)
     ap.add_argument("--xcds", type=int, default=8)
+    ap.add_argument("--issue-peak", type=float, default=0.35)
     a = ap.parse_args()
     valu = per_kernel(a.sq_csv, "SQ_INSTS_VALU")
     grbm = per_kernel(a.grbm_csv, "GRBM_GUI_ACTIVE")
     out = {"workload": a.workload, "sources": [a.sq_csv, a.grbm_csv],
-           "method": "SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE / xcds x simds), per launch",
+           "method": "SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE / xcds x simds), per launch; "
+                     "issue_frac = SQ_INSTS_VALU / (cycles x simds) / measured issue peak",
+           "issue_peak_per_simd_clk": a.issue_peak,
            "kernels": {}}
     for k in sorted(set(valu) & set(grbm)):
         v = sum(valu[k]) / len(valu[k])
         g = sum(grbm[k]) / len(grbm[k]) / a.xcds
         out["kernels"][k] = {"valu_insts": v, "cycles": g,
-                             "valu_busy": round(2.0 * v / (g * a.simds), 4) if g else None}
+                             "valu_busy": round(2.0 * v / (g * a.simds), 4) if g else None,
+                             "issue_frac": round(v / (g * a.simds) / a.issue_peak, 4) if g else None}
     with open(a.out_json, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
