@@ -1285,12 +1285,19 @@ __device__ __forceinline__ void path_body(
             if (hasB) { btB = tB_; bestB = iB_; }
         } else {
             // ---- scan: both rays against every triangle (wave-uniform face index) ----
+            // (RVCP_EXP_SCAN_REPEAT > 1 re-runs the scan -- same result, since a repeat
+            // re-accepts exactly the kept face -- to measure the scan's share of the frame)
+#ifndef RVCP_EXP_SCAN_REPEAT
+#define RVCP_EXP_SCAN_REPEAT 1
+#endif
+            for (int rep = 0; rep < RVCP_EXP_SCAN_REPEAT; ++rep) {
 #pragma unroll 2
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
                 float tA, tB;
                 if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
                 if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
+            }
             }
         }
 
