@@ -52,7 +52,7 @@ def test_readme_blocks_full_resolution(cornell_arrays, cornell):
     _, rgba, trav = O.render(cornell_arrays, cornell.push_constant(TIME), cfg, 1024, 1024,
                              want_linear=False)
     rms, mean = _rms_vs_readme(rgba)
-    assert rms < 0.006, rms                  # measured 0.0031
+    assert rms < 0.006, rms                  # measured 0.0032 (quirk off: 0.027)
     # miss pixels outside the open box are exactly 64 in the screenshot and here
     assert (rgba[0, 0, :3] == 64).all() and (rgba[1023, 1023, :3] == 64).all()
     assert 4.85 < trav / (1024 * 1024 * 30) < 5.0
