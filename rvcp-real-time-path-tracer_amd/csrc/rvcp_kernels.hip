@@ -475,6 +475,22 @@ __device__ __forceinline__ void coop_unit_sphere(bool need, float seed, float &r
         const uint64_t M = __ballot(need);
         if (M == 0ull) break;
         const uint32_t n = (uint32_t)__builtin_popcountll(M);
+        if (n > kWave / 2) {
+            // K = 1: every lane still rejecting tests its own next candidate -- the same
+            // candidate the compacted form below would hand it, without the LDS round trips
+            const float rx = fractf(pt_sinf_rand(seed + (ridx + 1.0f)) * 43758.5453f);
+            const float ry = fractf(pt_sinf_rand(seed + (ridx + 2.0f)) * 43758.5453f);
+            const float rz = fractf(pt_sinf_rand(seed + (ridx + 3.0f)) * 43758.5453f);
+            const f3 p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
+            if (need) {
+                ridx = ridx + 3.0f;
+                if (!(dot(p, p) >= 1.0f)) {
+                    p_out = p;
+                    need = false;
+                }
+            }
+            continue;
+        }
         const uint32_t lgK = 31u - (uint32_t)__builtin_clz((uint32_t)kWave / n);   // floor(log2(64/n))
         const uint32_t K = 1u << lgK;
         const uint32_t r = rank_in(M);
