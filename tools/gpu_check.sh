@@ -36,6 +36,7 @@ for s in $STEPS; do
         newtests) run pytest_new 600 python -m pytest tests/test_golden_frames.py tests/test_interactive.py tests/test_scene_io.py tests/test_mandelbrot.py -m gpu -x -q ;;
         headless) run headless 300 python tools/headless.py --frames 120 --size 384 --spp 10 --dump gpurun_out/headless --format png --script walk ;;
         timeline) run timeline 300 bash -c "rm -f /tmp/tl.bin && RVCP_DEBUG_TIMELINE=/tmp/tl.bin python tools/frames.py --frames 3 && python tools/timeline.py /tmp/tl.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl.bin\")//96)')" ;;
+        timelinec2) run timelinec2 300 bash -c "rm -f /tmp/tl2.bin && RVCP_DEBUG_TIMELINE=/tmp/tl2.bin python tools/frames.py --frames 3 --size 384 --spp 10 && python tools/timeline.py /tmp/tl2.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl2.bin\")//96)')" ;;
         timeline5) run timeline5 300 bash -c "rm -f /tmp/tl5.bin && RVCP_DEBUG_TIMELINE=/tmp/tl5.bin python tools/frames.py --variant 5 --frames 3 && python tools/timeline.py /tmp/tl5.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl5.bin\")//96)')" ;;
         chunks) run chunks 500 bash -c "echo c3; python tools/frames.py --frames 10 || exit 1; echo c2; python tools/frames.py --frames 10 --size 384 --spp 10 || exit 1; echo sph; python tools/frames.py --integrator 1 --scene spheres --frames 10 --spp 5 || exit 1; echo small128; python tools/frames.py --frames 10 --size 128 --spp 30 || exit 1" ;;
         c5t) run c5t 400 bash -c "echo c5-512-v4; python tools/frames.py --variant 4 --frames 3 --tris 100000 --size 512 --spp 4 || exit 1; echo c5-512-v3; python tools/frames.py --variant 3 --frames 2 --tris 100000 --size 512 --spp 4" ;;
