@@ -1048,7 +1048,7 @@ __device__ __forceinline__ void path_body(
     unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
     const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile,
     const Bvh4Node *__restrict__ bvh_nodes = nullptr, const TriRecord *__restrict__ bvh_tris = nullptr,
-    int32_t *bvh_stack = nullptr)
+    int32_t *bvh_stack = nullptr, float4 *compact_lds = nullptr)
 {
     const uint32_t lane = lane_id();
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1299,6 +1299,54 @@ __device__ __forceinline__ void path_body(
             const int iA_ = __shfl(best, srcA), iB_ = __shfl(best, srcB);
             if (hasA) { btA = tA_; bestA = iA_; }
             if (hasB) { btB = tB_; bestB = iB_; }
+        } else if (!TILED && wave_active && nr <= (uint32_t)kWave) {
+            // ---- compact: at most 64 rays, one per lane, one slot instead of two ----
+            // Ray j (A rays of the lanes in lane order, then B rays) goes to lane j through
+            // this wave's LDS rows, lane j tests it against every triangle, and the nearest hits
+            // go back the same way.  Each ray meets the same triangles in the same order, so
+            // every nearest hit is unchanged.
+            float4 *rows = compact_lds + (threadIdx.x / kWave) * (2 * kWave);
+            if (hasA) {
+                const uint32_t j = rank_in(mA);
+                rows[2 * j] = make_float4(a_o.x, a_o.y, a_o.z, 0.0f);
+                rows[2 * j + 1] = make_float4(a_d.x, a_d.y, a_d.z, 0.0f);
+            }
+            if (hasB) {
+                const uint32_t j = na + rank_in(mB);
+                rows[2 * j] = make_float4(b_o.x, b_o.y, b_o.z, 0.0f);
+                rows[2 * j + 1] = make_float4(b_d.x, b_d.y, b_d.z, 0.0f);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const float4 ro = rows[2 * lane], rd = rows[2 * lane + 1];
+            const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
+            float bt = A.t_max;
+            int best = -1;
+#pragma unroll 2
+            for (uint32_t i = 0; i < A.n_faces; ++i) {
+                const TriRecord T = tri[i];
+                float t;
+                if (tri_accept(T, o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
+            }
+            // lanes >= nr traced stale rows; their results are never read
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            rows[2 * lane] = make_float4(bt, __int_as_float(best), 0.0f, 0.0f);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (hasA) {
+                const float4 r = rows[2 * rank_in(mA)];
+                btA = r.x;
+                bestA = __float_as_int(r.y);
+            }
+            if (hasB) {
+                const float4 r = rows[2 * (na + rank_in(mB))];
+                btB = r.x;
+                bestB = __float_as_int(r.y);
+            }
         } else {
             // ---- scan: both rays against every triangle (wave-uniform face index) ----
             // (RVCP_EXP_SCAN_REPEAT > 1 re-runs the scan -- same result, since a repeat
@@ -1371,8 +1419,9 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
     const FaceShade *__restrict__ shade)
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];   // tail: ray rank -> owner lane
+    __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];  // compact scan: rays, then hits
     path_body<false, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
-                            shade, tail_tab, nullptr);
+                            shade, tail_tab, nullptr, nullptr, nullptr, nullptr, compact_lds);
 }
 
 // Opt-in BVH (RVCP_ACCEL_BVH): the variant-3 machine with per-lane BVH traversal in place of
