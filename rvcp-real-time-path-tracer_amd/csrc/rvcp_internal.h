@@ -67,14 +67,17 @@ struct alignas(16) LightRecord {
 static_assert(sizeof(LightRecord) == 96, "LightRecord is 96 B");
 
 // A pixel whose primary ray hit a non-emissive surface, as the primary pre-pass hands it to
-// the path kernel (variant 3): the cached primary hit record (:421-431 at depth 0).
+// the path kernel (variant 3): the cached primary hit record (:421-431 at depth 0) and the
+// pixel's RNG seed.
 struct alignas(16) SurfRecord {
     float pos[3];
-    uint32_t mat;
-    float nrm[3];
     uint32_t pix;
+    float nrm[3];
+    float seed;         // srand's seed of the pixel (:153-155), computed once by the pre-pass
+    float alb_pi[3];    // albedo / pi of the hit material
+    uint32_t mat;
 };
-static_assert(sizeof(SurfRecord) == 32, "SurfRecord is 32 B");
+static_assert(sizeof(SurfRecord) == 48, "SurfRecord is 48 B");
 
 // Per-face shading data, gathered by index once per traversal for the nearest face only:
 // the three vertex normals (interpolated at :262-266), the face material (:272) with its type

@@ -964,10 +964,11 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     if (threadIdx.x == 0) block_count = 0;
     __syncthreads();
     bool is_surf = false;
-    f3 hpos = mk(0, 0, 0), hn = mk(0, 0, 0);
+    f3 hpos = mk(0, 0, 0), hn = mk(0, 0, 0), halb = mk(0, 0, 0);
     uint32_t hmat = 0;
+    float u_ = 0.0f, v_ = 0.0f;
     if (live) {
-        float u_, v_, tmin, tmax;
+        float tmin, tmax;
         f3 o, d;
         pixel_uv(A, pix, u_, v_);
         primary_ray(A, u_, v_, o, d, tmin, tmax);
@@ -984,7 +985,11 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
         }
         FaceShade fs;
         fs.ty = 0;
-        if (best >= 0) { hit_shade(tri, shade, best, o, d, bt, hpos, hn, fs); hmat = fs.mat; }
+        if (best >= 0) {
+            hit_shade(tri, shade, best, o, d, bt, hpos, hn, fs);
+            hmat = fs.mat;
+            halb = ld3(fs.alb_pi);
+        }
         const bool miss = best < 0;
         const bool is_light = !miss && fs.ty == kLight;
         if (miss || is_light) {
@@ -1011,8 +1016,9 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     __syncthreads();
     if (is_surf) {
         SurfRecord r;
-        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.mat = hmat;
-        r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.pix = pix;
+        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.pix = pix;
+        r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.seed = pixel_seed(A, u_, v_);
+        r.alb_pi[0] = halb.x; r.alb_pi[1] = halb.y; r.alb_pi[2] = halb.z; r.mat = hmat;
         surf[block_base + wave_off + rank_in(m)] = r;
     }
 }
@@ -1102,10 +1108,8 @@ __device__ __forceinline__ void path_body(
                 if (got) {
                     const SurfRecord r = surf[slot];
                     pix = r.pix;
-                    P_pos = ld3(r.pos); P_nrm = ld3(r.nrm); P_alb = ld3(mats[r.mat].alb_pi);
-                    float u_, v_;
-                    pixel_uv(A, pix, u_, v_);
-                    seed = pixel_seed(A, u_, v_);
+                    P_pos = ld3(r.pos); P_nrm = ld3(r.nrm); P_alb = ld3(r.alb_pi);
+                    seed = r.seed;
                     ridx = 0.0f;
                     k = 0;
                     acc = mk(0, 0, 0);
