@@ -1127,6 +1127,15 @@ __device__ __forceinline__ void path_body(
             if (surf_ev) {                                          // :431-462
                 surf_ev = false;
                 f3 ws;
+#if RVCP_EXP_REPEAT_NEE
+                {
+                    float sd = seed, ri = ridx, dd;
+                    f3 cc, ww, ps = S_pos;
+                    asm volatile("" : "+v"(sd), "+v"(ri), "+v"(ps.x));
+                    const bool ok = nee_sample(A, lights, S_alb, ps, S_nrm, att, sd, ri, cc, dd, ww);
+                    asm volatile("" :: "v"(cc.x), "v"(cc.y), "v"(cc.z), "v"(dd), "v"(ww.x), "v"(ri), "v"(ok ? 1 : 0));
+                }
+#endif
                 if (nee_sample(A, lights, S_alb, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist,
                                ws)) {
                     a_o = add(S_pos, muls(ws, A.eps));
@@ -1138,8 +1147,25 @@ __device__ __forceinline__ void path_body(
                 if (!need_dir && !hasA) ended = true;
             }
             f3 p = mk(0, 0, 0);
+#if RVCP_EXP_REPEAT_COOP
+            {
+                float sd = seed, ri = ridx;
+                f3 pp = mk(0, 0, 0);
+                asm volatile("" : "+v"(sd), "+v"(ri));
+                coop_unit_sphere(need_dir, sd, ri, pp, lane, tail_tab[threadIdx.x / kWave]);
+                asm volatile("" :: "v"(pp.x), "v"(pp.y), "v"(pp.z), "v"(ri));
+            }
+#endif
             coop_unit_sphere(need_dir, seed, ridx, p, lane, tail_tab[threadIdx.x / kWave]);
             if (need_dir) {                                         // :464-478
+#if RVCP_EXP_REPEAT_BRDF
+                {
+                    f3 at2 = att, wi2, p2 = p;
+                    asm volatile("" : "+v"(p2.x), "+v"(at2.x));
+                    brdf_finish(A, S_alb, S_nrm, p2, at2, wi2);
+                    asm volatile("" :: "v"(at2.x), "v"(at2.y), "v"(at2.z), "v"(wi2.x), "v"(wi2.y), "v"(wi2.z));
+                }
+#endif
                 f3 wi;
                 brdf_finish(A, S_alb, S_nrm, p, att, wi);
                 depth += 1;
@@ -1390,6 +1416,15 @@ __device__ __forceinline__ void path_body(
             } else {
                 f3 hpos, hn;
                 FaceShade fs;
+#if RVCP_EXP_REPEAT_HIT
+                {
+                    f3 hp2, hn2, bo2 = b_o;
+                    FaceShade fs2;
+                    asm volatile("" : "+v"(bo2.x));
+                    hit_shade(tri, shade, bestB, bo2, b_d, btB, hp2, hn2, fs2);
+                    asm volatile("" :: "v"(hp2.x), "v"(hn2.x), "v"(hn2.y), "v"(hn2.z), "v"(fs2.ty));
+                }
+#endif
                 hit_shade(tri, shade, bestB, b_o, b_d, btB, hpos, hn, fs);
                 if (fs.ty == kLight) {
                     ended = true;       // depth >= 1: no emission term (:426)
