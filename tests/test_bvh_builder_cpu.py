@@ -47,3 +47,31 @@ def test_bvh4_tiny_mesh(checker, tmp_path):
     r = subprocess.run([checker, mesh, "100"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "nodes4=0" in r.stdout
+
+
+def test_bvh4_builder_sanitized(tmp_path):
+    """The builder + collapse under AddressSanitizer / UBSan (host code only), on a degenerate,
+    a tiny and a random mesh: no report, and the same answers."""
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "bvh4_asan")
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-ffp-contract=off",
+                        "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                        "-I", CSRC, os.path.join(ROOT, "tools", "bvh4_check.cpp"),
+                        os.path.join(CSRC, "rvcp_bvh.cpp"), "-o", exe],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("sanitizer runtime unavailable: " + r.stderr[-200:])
+    sc = rvcp_amd.scene.with_random_triangles(rvcp_amd.Scene.default(), 3000)
+    v = sc.mesh.aligned_vertices()
+    f = sc.mesh.aligned_faces()
+    meshes = {"random": v["position"][:, :3][f["vertices"]].astype(np.float32),
+              "degenerate": np.zeros((5, 3, 3), np.float32),
+              "tiny": np.array([[[0, 0, 0], [1, 0, 0], [0, 1, 0]]], np.float32)}
+    for name, tris in meshes.items():
+        path = str(tmp_path / f"{name}.bin")
+        tris.tofile(path)
+        r = subprocess.run([exe, path, "200"], capture_output=True, text=True)
+        assert r.returncode == 0, (name, r.stdout[-500:], r.stderr[-2000:])
+        assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr
+        assert "mismatches 0 of 200" in r.stdout, (name, r.stdout)
