@@ -1,0 +1,69 @@
+/* rvcp_render.c -- a host program over the C-ABI alone (no Python, no torch): what the
+ * reference's Rust main loop becomes once its Vulkano pipeline is swapped for librvcp
+ * (INTEGRATION.md).  Loads a .rvcpscn scene (the reference's upload arrays + camera), renders
+ * `frames` frames with the reference's push constant {camera, time}, writes the last frame as
+ * a binary PPM and prints one JSON line of stats per frame.
+ *
+ *   make -C examples            # gcc, links ../rvcp-real-time-path-tracer_amd/csrc/build/librvcp.so
+ *   examples/build/rvcp_render scene.rvcpscn W H SPP TIME FRAMES out.ppm
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "rvcp.h"
+
+static int die(rvcp_ctx_t *ctx, const char *what, int rc)
+{
+    fprintf(stderr, "%s failed (%d): %s\n", what, rc, ctx ? rvcp_last_error(ctx) : "");
+    if (ctx) rvcp_destroy(ctx);
+    return 1;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc != 8) {
+        fprintf(stderr, "usage: %s scene.rvcpscn W H SPP TIME FRAMES out.ppm\n", argv[0]);
+        return 2;
+    }
+    const uint32_t W = (uint32_t)strtoul(argv[2], NULL, 10);
+    const uint32_t H = (uint32_t)strtoul(argv[3], NULL, 10);
+    const uint32_t spp = (uint32_t)strtoul(argv[4], NULL, 10);
+    const float time = strtof(argv[5], NULL);
+    const int frames = atoi(argv[6]);
+    if (W == 0 || H == 0 || spp == 0 || frames < 1) return 2;
+
+    rvcp_config_t cfg;
+    int rc = rvcp_config_default(&cfg);      /* the shader's #defines */
+    if (rc) return die(NULL, "rvcp_config_default", rc);
+    cfg.spp = spp;
+    rvcp_ctx_t *ctx = NULL;
+    rc = rvcp_create(&cfg, &ctx);             /* == create_compute_pipeline (vulkan.rs:576) */
+    if (rc) return die(ctx, "rvcp_create", rc);
+
+    rvcp_push_constant_t push;
+    memset(&push, 0, sizeof(push));
+    rc = rvcp_upload_scene_file(ctx, argv[1], &push.camera);   /* == descriptor set 0 */
+    if (rc) return die(ctx, "rvcp_upload_scene_file", rc);
+    push.time = time;
+
+    uint8_t *rgba = (uint8_t *)malloc((size_t)W * H * 4);
+    if (!rgba) return die(ctx, "malloc", -1);
+    for (int f = 0; f < frames; f++) {
+        rvcp_stats_t st;
+        rc = rvcp_render(ctx, &push, W, H, rgba, NULL, &st);  /* push constants + dispatch */
+        if (rc) { free(rgba); return die(ctx, "rvcp_render", rc); }
+        printf("{\"frame\": %d, \"kernel_ms\": %.4f, \"traversals\": %llu, \"samples\": %llu}\n",
+               f, st.kernel_ms, (unsigned long long)st.traversals,
+               (unsigned long long)st.samples);
+    }
+
+    FILE *out = fopen(argv[7], "wb");
+    if (!out) { free(rgba); return die(ctx, "fopen", -1); }
+    fprintf(out, "P6\n%u %u\n255\n", W, H);
+    for (size_t i = 0; i < (size_t)W * H; i++) fwrite(rgba + 4 * i, 1, 3, out);
+    fclose(out);
+    free(rgba);
+    rc = rvcp_destroy(ctx);
+    return rc ? 1 : 0;
+}
