@@ -1043,8 +1043,14 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_TILED_MIN_WAVES
 #define RVCP_TILED_MIN_WAVES 4
 #endif
+// The variant-3 path kernel is held to 5 waves per SIMD (96 VGPRs, ~13 spilled around cold
+// code) with the scan loop not unrolled: C3 5.93 -> 5.78 ms, C4 44.2 -> 41.4 ms, C2 unchanged,
+// over its natural 105 VGPRs / 4 waves (tools/ab.sh; 6 waves spill 54 and run 1.8x slower).
+#ifndef RVCP_SCAN_UNROLL
+#define RVCP_SCAN_UNROLL 1
+#endif
 #ifndef RVCP_PATH_MIN_WAVES
-#define RVCP_PATH_MIN_WAVES 1
+#define RVCP_PATH_MIN_WAVES 5
 #endif
 template <bool TILED, bool BVH, bool SINGLE = false>
 __device__ __forceinline__ void path_body(
@@ -1353,7 +1359,7 @@ __device__ __forceinline__ void path_body(
             const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
             float bt = A.t_max;
             int best = -1;
-#pragma unroll 2
+#pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
                 float t;
@@ -1385,7 +1391,7 @@ __device__ __forceinline__ void path_body(
 #define RVCP_EXP_SCAN_REPEAT 1
 #endif
             for (int rep = 0; rep < RVCP_EXP_SCAN_REPEAT; ++rep) {
-#pragma unroll 2
+#pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
                 float tA, tB;
