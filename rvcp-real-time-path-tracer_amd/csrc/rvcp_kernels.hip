@@ -1043,9 +1043,10 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_TILED_MIN_WAVES
 #define RVCP_TILED_MIN_WAVES 4
 #endif
-// The variant-3 path kernel is held to 5 waves per SIMD (96 VGPRs, ~13 spilled around cold
-// code) with the scan loop not unrolled: C3 5.93 -> 5.78 ms, C4 44.2 -> 41.4 ms, C2 unchanged,
-// over its natural 105 VGPRs / 4 waves (tools/ab.sh; 6 waves spill 54 and run 1.8x slower).
+// The variant-3 path kernel runs 5 waves per SIMD: 95 VGPRs without spills once the scan loop
+// is not unrolled and the pixel's surface record is re-read per sample instead of held in
+// registers (C3 5.93 -> 5.73 ms, C4 44.2 -> 41.3 ms, C2 unchanged, over 105 VGPRs / 4 waves;
+// tools/ab.sh).  Forcing 6 waves spills 26 VGPRs and is slower.
 #ifndef RVCP_SCAN_UNROLL
 #define RVCP_SCAN_UNROLL 1
 #endif
@@ -1078,10 +1079,11 @@ __device__ __forceinline__ void path_body(
     const float sppf = (float)A.spp;
 
     bool need_pixel = true, done = false, ended = false, surf_ev = false;
-    uint32_t pix = 0, k = 0, depth = 0, trav = 0, iters = 0;
+    // the pixel's surface record (cached primary hit, pixel index) is re-read from the list at
+    // each sample start instead of being held in 10 VGPRs for the whole pixel
+    uint32_t pslot = 0, k = 0, depth = 0, trav = 0, iters = 0;
     float seed = 0.0f, ridx = 0.0f;
     f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
-    f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0), P_alb = mk(0, 0, 0);
     f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0), S_alb = mk(0, 0, 0);
     bool hasA = false;
     f3 a_o = mk(0, 0, 0), a_d = mk(0, 0, 1), a_p = mk(0, 0, 0), nee_C = mk(0, 0, 0);
@@ -1097,13 +1099,14 @@ __device__ __forceinline__ void path_body(
                 acc = add(acc, divs(col, sppf));
                 k += 1;
                 if (k >= A.spp) {
-                    store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
+                    store_pixel(surf[pslot].pix, acc, A, gamma_t, out_rgba, out_lin);
                     need_pixel = true;
                 } else {
                     depth = 0;
                     att = mk(1, 1, 1);
                     col = mk(0, 0, 0);
-                    S_pos = P_pos; S_nrm = P_nrm; S_alb = P_alb;
+                    const SurfRecord r = surf[pslot];
+                    S_pos = ld3(r.pos); S_nrm = ld3(r.nrm); S_alb = ld3(r.alb_pi);
                     surf_ev = true;
                 }
             }
@@ -1113,8 +1116,7 @@ __device__ __forceinline__ void path_body(
                 queue_take(q, __ballot(need_pixel && !done), lane, Q, counters, got, slot);
                 if (got) {
                     const SurfRecord r = surf[slot];
-                    pix = r.pix;
-                    P_pos = ld3(r.pos); P_nrm = ld3(r.nrm); P_alb = ld3(r.alb_pi);
+                    pslot = slot;
                     seed = r.seed;
                     ridx = 0.0f;
                     k = 0;
@@ -1122,7 +1124,7 @@ __device__ __forceinline__ void path_body(
                     depth = 0;
                     att = mk(1, 1, 1);
                     col = mk(0, 0, 0);
-                    S_pos = P_pos; S_nrm = P_nrm; S_alb = P_alb;
+                    S_pos = ld3(r.pos); S_nrm = ld3(r.nrm); S_alb = ld3(r.alb_pi);
                     need_pixel = false;
                     surf_ev = true;
                 } else if (need_pixel && q.exhausted) {
