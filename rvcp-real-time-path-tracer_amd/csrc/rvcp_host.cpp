@@ -618,7 +618,8 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     A.light_pdf = ctx->light_pdf;
     A.want_linear = d_linear_rgb ? 1u : 0u;
     A.variant = ctx->cfg.kernel_variant != 0 ? ctx->cfg.kernel_variant
-              : (ctx->n_faces >= kTiledMinFaces ? 5 : kDefaultVariant);
+              : ctx->n_faces >= kTiledMinFaces ? 5
+              : (uint64_t)A.n_pixels * A.spp >= kWideMinSamples ? 6 : kDefaultVariant;
     A.accel = (ctx->cfg.accel == RVCP_ACCEL_BVH && ctx->n_faces > 0) ? RVCP_ACCEL_BVH : RVCP_ACCEL_NONE;
     if (A.accel == RVCP_ACCEL_BVH) A.variant = 3;    // the BVH traversal lives in the v3 kernels
     A.bvh_root = ctx->bvh_root;

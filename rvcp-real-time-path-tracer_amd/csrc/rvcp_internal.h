@@ -30,8 +30,12 @@ constexpr uint32_t kChunkWindow = 10000;    // 100 us
 // (selectable; variant 5 is the automatic choice for meshes of kTiledMinFaces faces or more).
 // 5 = variant 4 with one ray per lane per iteration (the shadow ray, then the path ray), so no
 // ray slot is empty; for scan-bound meshes.
+// 6 = variant 3 compiled for 6 waves per SIMD instead of 5 (80 VGPRs, a few spills): faster
+// once the frame is large enough that latency hiding beats the spills (automatic from
+// kWideMinSamples pixel-samples per frame).
 constexpr int kDefaultVariant = 3;
-constexpr int kMaxVariant = 5;
+constexpr int kMaxVariant = 6;
+constexpr uint64_t kWideMinSamples = 8ull << 20;   // auto: variant 6 from 8 Msamples per frame
 constexpr int kOccupancyBvh = 100;          // rvcp_games101_occupancy code of the BVH kernel
 #ifndef RVCP_TILE
 #define RVCP_TILE 256

@@ -1053,7 +1053,10 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_PATH_MIN_WAVES
 #define RVCP_PATH_MIN_WAVES 5
 #endif
-template <bool TILED, bool BVH, bool SINGLE = false>
+// LDS_STATE: the light sample's pending state (a_p, nee_C, nee_dist: written at the surface
+// event, read when the shadow ray resolves) and the pixel's running sum `acc` live in this
+// lane's column of an LDS block (SoA, stride kBlock) instead of 10 VGPRs across the scan.
+template <bool TILED, bool BVH, bool SINGLE = false, bool LDS_STATE = false>
 __device__ __forceinline__ void path_body(
     const FrameArgs &A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
@@ -1061,8 +1064,11 @@ __device__ __forceinline__ void path_body(
     unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
     const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile,
     const Bvh4Node *__restrict__ bvh_nodes = nullptr, const TriRecord *__restrict__ bvh_tris = nullptr,
-    int32_t *bvh_stack = nullptr, float4 *compact_lds = nullptr)
+    int32_t *bvh_stack = nullptr, float4 *compact_lds = nullptr, float *state_lds = nullptr)
 {
+    float *const st = LDS_STATE ? state_lds + threadIdx.x : nullptr;   // st[f * kBlock]
+    auto st_put3 = [&](int f, f3 v) { st[f * kBlock] = v.x; st[(f + 1) * kBlock] = v.y; st[(f + 2) * kBlock] = v.z; };
+    auto st_get3 = [&](int f) { return mk(st[f * kBlock], st[(f + 1) * kBlock], st[(f + 2) * kBlock]); };
     const uint32_t lane = lane_id();
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     unsigned long long t_exhausted = 0ull;
@@ -1096,7 +1102,9 @@ __device__ __forceinline__ void path_body(
         for (;;) {
             if (ended) {                                            // color += L / SPP (:495)
                 ended = false;
+                if (LDS_STATE) acc = st_get3(7);
                 acc = add(acc, divs(col, sppf));
+                if (LDS_STATE) st_put3(7, acc);
                 k += 1;
                 if (k >= A.spp) {
                     store_pixel(surf[pslot].pix, acc, A, gamma_t, out_rgba, out_lin);
@@ -1121,6 +1129,7 @@ __device__ __forceinline__ void path_body(
                     ridx = 0.0f;
                     k = 0;
                     acc = mk(0, 0, 0);
+                    if (LDS_STATE) st_put3(7, acc);
                     depth = 0;
                     att = mk(1, 1, 1);
                     col = mk(0, 0, 0);
@@ -1150,6 +1159,11 @@ __device__ __forceinline__ void path_body(
                     a_d = ws;
                     a_p = S_pos;
                     hasA = true;
+                    if (LDS_STATE) {
+                        st_put3(0, a_p);
+                        st_put3(3, nee_C);
+                        st[6 * kBlock] = nee_dist;
+                    }
                 }
                 need_dir = !(rnd(seed, ridx) > A.rr);               // Russian roulette :462
                 if (!need_dir && !hasA) ended = true;
@@ -1410,6 +1424,11 @@ __device__ __forceinline__ void path_body(
 
         // ---- resolve A: visibility of the light sample (:447-459) ----
         if (hasA) {
+            if (LDS_STATE) {
+                a_p = st_get3(0);
+                nee_C = st_get3(3);
+                nee_dist = st[6 * kBlock];
+            }
             const f3 hp = bestA >= 0 ? add(a_o, muls(a_d, btA))
                                      : mk(__builtin_inff(), __builtin_inff(), __builtin_inff());
             const float dist_blocked = len(sub(hp, a_p));
@@ -1458,7 +1477,8 @@ __device__ __forceinline__ void path_body(
     }
 }
 
-__global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_kernel(
+template <int MIN_WAVES>
+__global__ __launch_bounds__(kBlock, MIN_WAVES) void games101_path_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
@@ -1467,8 +1487,13 @@ __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void games101_path_ker
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];   // tail: ray rank -> owner lane
     __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];  // compact scan: rays, then hits
-    path_body<false, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
-                            shade, tail_tab, nullptr, nullptr, nullptr, nullptr, compact_lds);
+#ifndef RVCP_STATE_LDS
+#define RVCP_STATE_LDS 1
+#endif
+    __shared__ float state_lds[RVCP_STATE_LDS ? 10 * kBlock : 1];   // LDS_STATE columns
+    path_body<false, false, false, RVCP_STATE_LDS != 0>(
+        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
+        nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
 }
 
 // Opt-in BVH (RVCP_ACCEL_BVH): the variant-3 machine with per-lane BVH traversal in place of
@@ -1848,7 +1873,9 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade);
     else
-        hipLaunchKernelGGL(rvcp::games101_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+        hipLaunchKernelGGL(args->variant == 6 ? rvcp::games101_path_kernel<6>
+                                              : rvcp::games101_path_kernel<RVCP_PATH_MIN_WAVES>,
+                           dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade);
     return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -1888,8 +1915,10 @@ extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_single_kernel, rvcp::kBlock, 0)
         : variant == 4
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_kernel, rvcp::kBlock, 0)
+        : variant == 6
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel<6>, rvcp::kBlock, 0)
         : variant == 3
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel, rvcp::kBlock, 0)
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel<RVCP_PATH_MIN_WAVES>, rvcp::kBlock, 0)
         : variant == 2
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_dual_kernel, rvcp::kBlock, 0)
         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_kernel, rvcp::kBlock, 0);
