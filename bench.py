@@ -25,7 +25,10 @@ Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the path-tr
 traversals not attributed to it) over its HIP-event time (rvcp_stats_t.main_kernel_ms,
 events on the launch stream).  `traffic` is the same kernel's measured HBM bytes per launch
 from the rocprofv3 PMC summary committed under profiles/ (tools/pmc_traffic.py), when one
-exists for the workload.  `cpu_baseline` times the scalar C oracle (oracle/rvcp_oracle.c, the
+exists for the workload; `valu_busy_pmc` / `valu_issue_frac_pmc` are that kernel's VALU issue
+utilisation from the committed SQ counter passes (tools/pmc_valu.py: at 2 cycles per wave64
+instruction, and as a fraction of the issue rate tools/valu_rate.hip measures) -- the bound
+that actually limits this FP32 kernel.  `cpu_baseline` times the scalar C oracle (oracle/rvcp_oracle.c, the
 CPU re-execution of the same kernel) on a bounded sample of the workload, rank 0 at N=1 only.
 """
 import argparse
