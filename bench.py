@@ -9,27 +9,31 @@ One step = one frame: every rank renders its 8-row stripes of the frame with the
 once, before timing (inputs resident in HBM).
 
 Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
-  c3: Cornell 1024x1024 SPP=30.  For N>1 the frame grows with N at fixed SPP
-      (side = round8(1024*sqrt(N))), so per-GPU work stays ~C3: "scaling": "weak".
+  c3: Cornell 1024x1024 SPP=30 (the N=1 default).  With --workload c3 at N>1 the frame
+      grows with N at fixed SPP (side = round8(1024*sqrt(N))): "scaling": "weak".
   c1: Cornell 128x128 SPP=1 (BASELINE configs[0], the CPU plumbing case; its cpu_baseline is
       the whole frame).
   c2: Cornell 384x384 SPP=10 (README benchmark row).
-  c4: Cornell 2048x2048 SPP=64, fixed frame sharded over N GPUs ("scaling": "strong").
+  c4: Cornell 2048x2048 SPP=64, fixed frame sharded over N GPUs ("scaling": "strong"): the
+      BASELINE.json 8-GPU config and the default for N>1.  Rank 0 also renders the same frame
+      alone after the timed region (bit-exactness check, and `one_gpu_ms` for the speedup).
   c5: Cornell + 100k random triangles, 1024x1024 SPP=30.
   spheres: integrator mode 2 (ray_tracer.comp) on the deprecated host's sphere room,
       1024x1024 at its SPP=5 (not a BASELINE config; reported for coverage).
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the path-tracing kernel,
->99% of the frame's GPU time): algorithmic bytes = its reference-algorithm traversals x F x
-36 B per launch (the primary rays the pre-pass traces once are the only
-traversals not attributed to it) over its HIP-event time (rvcp_stats_t.main_kernel_ms,
-events on the launch stream).  `traffic` is the same kernel's measured HBM bytes per launch
-from the rocprofv3 PMC summary committed under profiles/ (tools/pmc_traffic.py), when one
-exists for the workload; `valu_busy_pmc` / `valu_issue_frac_pmc` are that kernel's VALU issue
-utilisation from the committed SQ counter passes (tools/pmc_valu.py: at 2 cycles per wave64
-instruction, and as a fraction of the issue rate tools/valu_rate.hip measures) -- the bound
-that actually limits this FP32 kernel.  `cpu_baseline` times the scalar C oracle (oracle/rvcp_oracle.c, the
-CPU re-execution of the same kernel) on a bounded sample of the workload, rank 0 at N=1 only.
+>99% of the frame's GPU time), whose bound is FP32 VALU issue: `achieved` =
+useful FLOP per launch (52 per reference-algorithm ray-triangle test, 25 per ray-sphere test,
+SURVEY.md §8(d)) / that kernel's HIP-event time on its launch stream
+(rvcp_stats_t.main_kernel_ms), `peak` = 157.3 TFLOP/s FP32 vector.  `traffic` is the same
+kernel's measured HBM bytes per launch from the rocprofv3 PMC summary committed under
+profiles/ (tools/pmc_traffic.py), when one exists for the workload and kernel schedule;
+`hbm_algorithmic` is SURVEY.md §8(d)'s HBM-read figure (36 algorithmic bytes per triangle
+test), which exceeds the HBM peak because the scene is served on-chip.  `valu_busy_pmc` /
+`valu_issue_frac_pmc` come from the committed SQ counter passes (tools/pmc_valu.py).
+`cpu_baseline` times the scalar C oracle (oracle/rvcp_oracle.c, the CPU re-execution of the
+same kernel) on the box's CPU share (OMP_NUM_THREADS threads, 16 per GPU on the GPU box), rank
+0 at N=1 only.
 """
 import argparse
 import json
@@ -44,6 +48,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FLOP_PER_SPHERE_TEST = 25      # ray_tracer.comp:300-321
 # the reference's published C3 row (README.md:26, 3 fps on an RTX 3060) and
 # C2 row (README.md:22, 51 fps), as Msamples/s
 REFERENCE_MSAMPLES = {"c3": 94.4, "c2": 75.2}
@@ -75,7 +80,7 @@ def workload(name, n_gpus):
     raise SystemExit(f"unknown workload {name}")
 
 
-def load_valu_busy(workload_name, kernel_substr):
+def load_valu_busy(workload_name, kernel_name):
     """VALU issue utilisation of the dominant kernel from the newest committed SQ PMC summary:
     (busy at 2 cycles per wave64 instruction, fraction of the measured issue peak)."""
     import glob
@@ -85,12 +90,12 @@ def load_valu_busy(workload_name, kernel_substr):
     with open(files[-1]) as f:
         d = json.load(f)
     for name, k in d.get("kernels", {}).items():
-        if kernel_substr in name:
+        if kernel_name in name:
             return k.get("valu_busy"), k.get("issue_frac")
     return None, None
 
 
-def load_traffic(workload_name, kernel_substr):
+def load_traffic(workload_name, kernel_name):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{workload_name}.json")))
@@ -99,7 +104,7 @@ def load_traffic(workload_name, kernel_substr):
     with open(files[-1]) as f:
         d = json.load(f)
     for name, k in d.get("kernels", {}).items():
-        if kernel_substr in name and k.get("bytes"):
+        if kernel_name in name and k.get("bytes"):
             return float(k["bytes"]), os.path.relpath(files[-1], ROOT)
     return None, None
 
@@ -161,9 +166,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5", "spheres"])
+    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "spheres"],
+                    help="default: c3 at N=1 (headline), c4 at N>1 (BASELINE's 8-GPU config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads for cpu_baseline (default: OMP_NUM_THREADS, else the "
+                         "CPUs this process may use)")
     ap.add_argument("--save-frame", default="")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
@@ -179,19 +187,20 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
-    # Rehearsal (RVCP_BENCH_REHEARSAL=1): every rank on device 0 and a gloo gather through host
-    # memory, to exercise the N>1 code path on a 1-GPU box.  Never used for reported numbers.
+    # Rehearsal (RVCP_BENCH_REHEARSAL=1): every rank on device 0 and the gather through host
+    # memory over gloo (RCCL refuses two ranks on one GPU), to exercise the N>1 code path on
+    # a 1-GPU box.  Never used for reported numbers.
     rehearsal = os.environ.get("RVCP_BENCH_REHEARSAL") == "1"
     if rehearsal:
         local_rank = 0
     torch.cuda.set_device(local_rank)
     if world > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # control plane only (barriers, the max-over-ranks time, the RCCL id); the frame
+        # itself moves over RCCL inside librvcp (rvcp_gather_frame_async)
+        dist.init_process_group("gloo")
 
-    wl = workload(args.workload, world)
+    wname = args.workload or ("c3" if world == 1 else "c4")
+    wl = workload(wname, world)
     W, H, spp = wl["W"], wl["H"], wl["spp"]
     legacy = wl.get("integrator", 0) == 1
     sc = rvcp_amd.scene.sphere_scene() if legacy else rvcp_amd.Scene.default()
@@ -207,9 +216,13 @@ def main():
     push = sc.push_constant(123.0)
     n_faces = len(sc.mesh.aligned_faces())
     n_spheres = len(sc.spheres) if legacy else 0
+    if world > 1 and not rehearsal:
+        uid = [rvcp_amd.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        rt.rccl_init(uid[0], world, rank)
 
     rows = rvcp_amd.shard_rows(H, rank, world)
-    slot = max(rvcp_amd.shard_rows(H, k, world) for k in range(world))
+    slot = rvcp_amd.shard_rows(H, 0, world)          # shard 0 has the most rows
     dev = torch.device("cuda", local_rank)
     shard_buf = torch.zeros((slot, W), dtype=torch.int32, device=dev)
     frame = torch.zeros((H, W), dtype=torch.int32, device=dev) if rank == 0 else None
@@ -219,20 +232,21 @@ def main():
     def step():
         if world == 1:
             rt.render_shard_async(push, W, H, 0, 1, frame.data_ptr(), stream=stream)
-            st = rt.sync_stats()
-            return st
+            return rt.sync_stats()
         rt.render_shard_async(push, W, H, rank, world, shard_buf.data_ptr(), stream=stream)
-        st = rt.sync_stats()
         if rehearsal:
+            st = rt.sync_stats()
             got = rvcp_amd.frame.gather_shards(shard_buf.cpu(), rank, world, dst=0)
             if rank == 0:
                 gat_flat.copy_(torch.stack(got))
-        else:
-            rvcp_amd.frame.gather_shards(shard_buf, rank, world, dst=0, out=gat_flat)   # RCCL
-        if rank == 0:
-            rt.assemble_frame_async(gat_flat.data_ptr(), slot, W, H, world, frame.data_ptr(),
-                                    stream=stream)
-        return st
+                rt.assemble_frame_async(gat_flat.data_ptr(), slot, W, H, world, frame.data_ptr(),
+                                        stream=stream)
+            return st
+        # RCCL gather + device assembly, enqueued behind the render without a host sync
+        rt.gather_frame_async(shard_buf.data_ptr(), W, H,
+                              gat_flat.data_ptr() if rank == 0 else 0,
+                              frame.data_ptr() if rank == 0 else 0, stream=stream)
+        return rt.sync_stats()
 
     for _ in range(args.warmup):
         step()
@@ -240,7 +254,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, main_ms, trav, trav_exec = [], [], 0, 0
+    kernel_ms, main_ms, trav, trav_exec, variant = [], [], 0, 0, 0
     t0 = time.perf_counter()
     step_ms = []
     for _ in range(args.steps):
@@ -251,13 +265,14 @@ def main():
         main_ms.append(float(st["main_kernel_ms"]))
         trav += int(st["traversals"])
         trav_exec += int(st["traversals_executed"])
+        variant = int(st["kernel_variant"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -265,7 +280,7 @@ def main():
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed * 1000.0 / args.steps
 
-    # roofline for the dominant kernel (this rank's launches).  The pre-pass (variants 3/4,
+    # roofline of the dominant kernel (this rank's launches).  The pre-pass (schedules 3-6,
     # games101 only) traces each pixel's primary ray once; every other reference-algorithm
     # traversal -- including the reused primary hits of samples 2..SPP -- belongs to the
     # path kernel.
@@ -273,24 +288,34 @@ def main():
     avg_kernel_s = (sum(main_ms) / len(main_ms)) / 1000.0
     prepass = 0 if legacy else rows * W
     units = trav / args.steps - prepass                     # traversals per path-kernel launch
-    # a traversal tests F triangles (36 B each) and, in mode 2, S spheres (16 B each)
+    tri_tests = units * n_faces
+    flop_per_launch = tri_tests * FLOP_PER_TEST + units * n_spheres * FLOP_PER_SPHERE_TEST
+    achieved_tflops = flop_per_launch / avg_kernel_s / 1e12
+    # 36 algorithmic bytes per triangle test (16 per sphere test)
     bytes_per_launch = units * (n_faces * 36 + n_spheres * 16)
-    achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
-    tests_per_s = units * (n_faces + n_spheres) / avg_kernel_s
+    algo_gbs = bytes_per_launch / avg_kernel_s / 1e9
     exec_tests_per_s = (trav_exec / args.steps - prepass) * (n_faces + n_spheres) / avg_kernel_s
-    kname = ("legacy_kernel" if legacy else "games101_bvh_path_kernel" if args.accel == "bvh"
-             else "games101_tiled_single_kernel" if n_faces >= 256 else "games101_path_kernel")
+    kname = rvcp_amd.abi.KERNEL_NAMES.get(variant, "?")
     traffic, traffic_src = load_traffic(wl["workload"], kname)
     valu_busy, valu_issue_frac = load_valu_busy(wl["workload"], kname)
 
-    frame_check = None
+    frame_check, one_gpu_ms = None, None
     if world > 1 and rank == 0:
-        # the assembled N-rank frame must be bit-identical to a 1-rank render (outside timing)
+        # the assembled N-rank frame must be bit-identical to a 1-rank render of the same frame
+        # (outside timing); its time is the same-frame single-GPU reference for the speedup
         single = torch.zeros((H, W), dtype=torch.int32, device=dev)
-        rt.render_shard_async(push, W, H, 0, 1, single.data_ptr(), stream=stream)
-        rt.sync_stats()
-        torch.cuda.synchronize()
+        times = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            ts = time.perf_counter()
+            rt.render_shard_async(push, W, H, 0, 1, single.data_ptr(), stream=stream)
+            rt.sync_stats()
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - ts) * 1000.0)
+        one_gpu_ms = float(np.median(times))
         frame_check = bool(torch.equal(single, frame))
+    if world > 1:
+        dist.barrier()
 
     if args.save_frame and rank == 0:
         np.save(args.save_frame, frame.cpu().numpy().view(np.uint8).reshape(H, W, 4))
@@ -308,42 +333,59 @@ def main():
             "frame_ms_median": round(float(np.median(step_ms)), 4),
             "higher_is_better": True,
             "scaling": wl["scaling"],
-            "vs_baseline": (round(value / REFERENCE_MSAMPLES[args.workload], 2)
-                            if args.workload in REFERENCE_MSAMPLES else None),
+            # the reference's published rows are single-GPU (RTX 3060) C3 / C2 frames
+            "vs_baseline": (round(value / REFERENCE_MSAMPLES[wname], 2)
+                            if world == 1 and wname in REFERENCE_MSAMPLES else None),
             "dtype": "f32",
             "data": ("synthetic (the reference's deprecated sphere-room scene, integrator mode 2, "
                      "fixed time seed 123.0)" if legacy else
                      "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)"),
             "config": {"workload": wl["workload"], "width": W, "height": H, "spp": spp,
                        "faces": n_faces, "parallelism": f"pixel-stripes x{world}",
-                       "accel": args.accel,
-                       "gather": ("gloo-rehearsal" if rehearsal else "rccl") if world > 1 else "none"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                       "accel": args.accel, "kernel_schedule": variant,
+                       "gather": ("gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
+                                  "rccl ncclGather via rvcp_gather_frame_async") if world > 1 else "none"},
+            "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 2),
+                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
+                         "traffic_hbm_frac": None if traffic is None else
+                         round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 5),
                          "kernel": kname,
                          "kernel_ms": round(avg_kernel_s * 1000.0, 4),
                          "frame_kernels_ms": round(avg_frame_s * 1000.0, 4),
-                         "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                         "definition": "reference-algorithm traversals of the path kernel x "
-                                       "(F x 36 B + S x 16 B) per launch / its HIP-event time "
-                                       "(SURVEY.md §8(d))",
+                         "definition": f"useful FP32 FLOP per launch ({FLOP_PER_TEST} per reference-"
+                                       f"algorithm ray-triangle test, {FLOP_PER_SPHERE_TEST} per "
+                                       "ray-sphere test) / the dominant kernel's HIP-event time"
+                                       + (" (BVH: brute-force-equivalent tests; work avoided)"
+                                          if args.accel == "bvh" else ""),
+                         "tests_per_launch": round(tri_tests),
+                         "hbm_algorithmic": {
+                             "bytes_per_launch": round(bytes_per_launch),
+                             "achieved_gbs": round(algo_gbs, 1),
+                             "frac_of_peak": round(algo_gbs / HBM_PEAK_GBS, 4),
+                             "definition": "SURVEY.md §8(d): reference-algorithm traversals x "
+                                           "(F x 36 B + S x 16 B) per launch / kernel time; > 1 "
+                                           "= on-chip reuse (scene in scalar cache / LDS)"},
                          "traversals_per_sample": round(trav / args.steps / (W * H * spp / world), 4)
                          if world == 1 else None,
                          "executed_traversal_frac": round(trav_exec / max(trav, 1), 4),
-                         "valu_tflops": round(tests_per_s * FLOP_PER_TEST / 1e12, 2),
-                         "valu_frac": round(tests_per_s * FLOP_PER_TEST / 1e12 / FP32_PEAK_TFLOPS, 4),
+                         "executed_tests_per_s": round(exec_tests_per_s, 1),
                          "valu_busy_pmc": valu_busy,
-                         "valu_issue_frac_pmc": valu_issue_frac,
-                         "executed_tests_per_s": round(exec_tests_per_s, 1)},
+                         "valu_issue_frac_pmc": valu_issue_frac},
             "cpu_baseline": None,
         }
         if frame_check is not None:
             out["config"]["assembled_frame_bitexact_vs_1gpu"] = frame_check
+            out["config"]["one_gpu_ms"] = round(one_gpu_ms, 4)
+            out["config"]["speedup_vs_one_gpu_same_frame"] = round(one_gpu_ms / ms_per_step, 3)
+            if rehearsal:
+                out["config"]["physical_gpus"] = 1
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            threads = args.cpu_threads or O.default_threads()
             out["cpu_baseline"] = cpu_baseline(sc, cfg_kw, W, H, threads)
         print(json.dumps(out), flush=True)
 

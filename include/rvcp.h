@@ -12,6 +12,10 @@
  *   - All functions return 0 (RVCP_OK) on success and a negative RVCP_E_* code on failure.
  *     Nothing aborts or throws across the ABI; `rvcp_last_error(ctx)` returns a message.
  *   - A context is not thread-safe: use one context per host thread.
+ *   - One frame in flight per context: a render, upload or Mandelbrot call while an async
+ *     frame is pending (rvcp_render_async / rvcp_render_shard_async not yet waited for with
+ *     rvcp_wait / rvcp_sync_stats) fails with RVCP_E_INVALID.  Use one context per frame in
+ *     flight.
  *   - Host pointers stay owned by the caller; the library copies what it needs.
  *   - Pointers named `d_*` are HIP device pointers; `stream` is a `hipStream_t` (NULL = the
  *     legacy default stream).
@@ -169,7 +173,9 @@ typedef struct rvcp_stats {
                                          are reused across a pixel's samples) */
     uint64_t samples;                 /* pixels * spp */
     uint32_t faces;                   /* F, triangles tested per traversal */
-    uint32_t _reserved;
+    int32_t kernel_variant;           /* the kernel schedule that ran (rvcp_config_t::
+                                         kernel_variant resolved; 7 = BVH path kernel,
+                                         8 = RVCP_INTEGRATOR_LEGACY kernel, 0 = none) */
     uint64_t wave_iterations;         /* wave-level trace iterations; lane utilisation of the
                                          scan = traversals_executed / (64 * wave_iterations) */
     double main_kernel_ms;            /* device time of the dominant (path-tracing) kernel
@@ -207,7 +213,8 @@ typedef struct rvcp_ctx rvcp_ctx_t;
 #define RVCP_E_HIP          (-2)   /* HIP runtime error */
 #define RVCP_E_NO_SCENE     (-3)   /* render before upload */
 #define RVCP_E_UNSUPPORTED  (-4)
-#define RVCP_E_NOMEM        (-5)
+#define RVCP_E_NOMEM        (-5)   /* host or device allocation failed */
+#define RVCP_E_INTERNAL     (-6)   /* unexpected internal error (caught at the ABI boundary) */
 
 /* ---------------------------------------------------------------------------------------
  * Entry points
@@ -315,6 +322,41 @@ uint32_t rvcp_shard_rows(uint32_t height, uint32_t shard_index, uint32_t shard_c
 int rvcp_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t slot_rows,
                               uint32_t width, uint32_t height, uint32_t shard_count,
                               void *d_frame, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * One process per GPU: every rank renders its stripes with
+ * rvcp_render_shard_async(ctx, ..., rank, world, d_shard, ...) into a shard buffer of
+ * rvcp_shard_rows(H, 0, world) rows (shard 0 has the most rows; shorter shards send padding),
+ * then rvcp_gather_frame_async gathers the shards to rank 0 with one RCCL ncclGather over
+ * xGMI and assembles the frame there on the device.  The reference is single-device
+ * (src/ray_tracer/vulkan.rs:145-193 picks one physical device); this replaces nothing in it
+ * and adds the multi-GPU form north_star asks for.  RCCL is loaded at run time
+ * (librccl.so.1: the copy the process already holds, e.g. PyTorch-ROCm's, else the system
+ * one); without it these return RVCP_E_UNSUPPORTED.
+ * ------------------------------------------------------------------------------------- */
+#define RVCP_RCCL_ID_BYTES 128     /* sizeof(ncclUniqueId) */
+
+/* Rank 0: create the communicator id (ncclGetUniqueId) to hand to every rank by any
+ * out-of-band channel (MPI, a TCP store, torch.distributed's broadcast). */
+int rvcp_rccl_unique_id(uint8_t out_id[RVCP_RCCL_ID_BYTES]);
+
+/* Every rank, collectively: create ctx's communicator (ncclCommInitRank on ctx's device).
+ * Blocks until all `world` ranks have joined.  Destroyed with the context. */
+int rvcp_rccl_init(rvcp_ctx_t *ctx, const uint8_t id[RVCP_RCCL_ID_BYTES], uint32_t world,
+                   uint32_t rank);
+
+/* Use the caller's existing communicator (an ncclComm_t over ctx's device, rank `rank` of
+ * `world`) instead; the caller keeps ownership. */
+int rvcp_rccl_attach(rvcp_ctx_t *ctx, void *nccl_comm, uint32_t world, uint32_t rank);
+
+/* Every rank, collectively, after its rvcp_render_shard_async on the same stream: gather the
+ * shards to rank 0 (ncclGather, root 0, shard k at slot k of d_gathered) and, on rank 0,
+ * assemble the W x H RGBA8 frame into d_frame.  d_shard_rgba8: rvcp_shard_rows(H, 0, world)
+ * * W * 4 bytes on every rank; d_gathered (world times that) and d_frame (W*H*4 bytes) are
+ * needed on rank 0 only (NULL elsewhere).  Enqueued on `stream` (NULL: ctx's stream); the
+ * frame is bit-identical to a single-GPU render. */
+int rvcp_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, uint32_t width,
+                            uint32_t height, void *d_gathered, void *d_frame, void *stream);
 
 #ifdef __cplusplus
 }

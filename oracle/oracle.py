@@ -94,13 +94,25 @@ def sample_ray(push, W, H, x, y) -> np.ndarray:
     return out
 
 
+def default_threads() -> int:
+    """Worker threads for the oracle: OMP_NUM_THREADS when set (the GPU box sets it to its CPU
+    share, 16 per GPU), else the CPUs this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0)) or 1
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def render(scene_arrays: dict, push, cfg, W, H, rect=None, threads=None, want_linear=True):
     """Render with the oracle.  scene_arrays: materials/vertices/faces/lum_face_ids numpy
     record arrays (scene.py dtypes); push: PUSH_DTYPE record; cfg: rvcp_config_t bytes
     (numpy record of CONFIG_DTYPE).  Returns (linear [th,tw,3] f32 | None, rgba [th,tw,4] u8,
     traversals)."""
     x0, y0, tw, th = rect if rect is not None else (0, 0, W, H)
-    threads = threads or os.cpu_count() or 1
+    threads = threads or default_threads()
     mats = np.ascontiguousarray(scene_arrays["materials"])
     verts = np.ascontiguousarray(scene_arrays["vertices"])
     faces = np.ascontiguousarray(scene_arrays["faces"])

@@ -7,12 +7,12 @@ repository root (``import rvcp_amd``), which loads this package under the name `
 from . import abi, scene
 from .scene import (Camera, Face, Material, MaterialType, Mesh, Scene, Sphere, Vertex,
                     cornell_box, push_constant)
-from .ray_tracer import RayTracer, shard_row_ids, shard_rows
+from .ray_tracer import RayTracer, rccl_unique_id, shard_row_ids, shard_rows
 from . import frame
 from . import interactive
 from . import scene_io
 from . import mandelbrot
 
 __all__ = ["abi", "scene", "frame", "interactive", "scene_io", "mandelbrot", "Camera", "Face", "Material", "MaterialType", "Mesh", "Scene",
-           "Sphere", "Vertex", "cornell_box", "push_constant", "RayTracer", "shard_rows",
-           "shard_row_ids"]
+           "Sphere", "Vertex", "cornell_box", "push_constant", "RayTracer", "rccl_unique_id",
+           "shard_rows", "shard_row_ids"]

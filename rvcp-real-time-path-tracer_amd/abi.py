@@ -22,9 +22,13 @@ CONFIG_DTYPE = np.dtype([("device", "<i4"), ("integrator", "<i4"), ("spp", "<u4"
                          ("accel", "<i4"), ("n_gpus", "<i4"), ("_reserved", "<u4", 3)])
 STATS_DTYPE = np.dtype([("kernel_ms", "<f8"), ("traversals", "<u8"),
                         ("traversals_executed", "<u8"), ("samples", "<u8"), ("faces", "<u4"),
-                        ("_reserved", "<u4"), ("wave_iterations", "<u8"),
+                        ("kernel_variant", "<i4"), ("wave_iterations", "<u8"),
                         ("main_kernel_ms", "<f8")])
 assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 56
+# rvcp_stats_t.kernel_variant -> the dominant kernel's name as rocprofv3 reports it
+KERNEL_NAMES = {1: "games101_kernel", 2: "games101_dual_kernel", 3: "games101_path_kernel<5>",
+                4: "games101_tiled_kernel", 5: "games101_tiled_single_kernel",
+                6: "games101_path_kernel<6>", 7: "games101_bvh_path_kernel", 8: "legacy_kernel"}
 
 # Defaults == the shader's #defines (ray_tracer_games101_branch.comp:5-13).
 DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop_eps=0.05,
@@ -32,13 +36,15 @@ DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop
                 lum_id_std140_quirk=1, kernel_variant=0, accel=0, n_gpus=1)
 
 # Error codes
-RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E_NOMEM = \
-    0, -1, -2, -3, -4, -5
+RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E_NOMEM, \
+    RVCP_E_INTERNAL = 0, -1, -2, -3, -4, -5, -6
+RCCL_ID_BYTES = 128
 
 EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "rvcp_create",
             "rvcp_destroy", "rvcp_last_error", "rvcp_upload_scene", "rvcp_render", "rvcp_render_shard_async",
             "rvcp_sync_stats", "rvcp_shard_rows", "rvcp_assemble_frame_async",
-            "rvcp_upload_scene_file", "rvcp_mandelbrot", "rvcp_render_async", "rvcp_wait"]
+            "rvcp_upload_scene_file", "rvcp_mandelbrot", "rvcp_render_async", "rvcp_wait",
+            "rvcp_rccl_unique_id", "rvcp_rccl_init", "rvcp_rccl_attach", "rvcp_gather_frame_async"]
 
 
 # Integrator mode 2 (ray_tracer.comp ray_trace): its own #defines (ray_tracer.comp:5-13).
@@ -80,6 +86,9 @@ def _share_torch_hip_runtime():
     spec = importlib.util.find_spec("torch")
     if spec is None or not spec.submodule_search_locations:
         return
+    # (RCCL is not preloaded: librvcp dlopen()s "librccl.so.1" when a gather needs it, which
+    # resolves by soname to the copy `import torch` already loaded.  Preloading torch's
+    # librccl.so before torch itself aborts the interpreter at exit.)
     for d in spec.submodule_search_locations:
         for name in ("libhsa-runtime64.so", "libamdhip64.so"):
             f = os.path.join(d, "lib", name)
@@ -115,10 +124,15 @@ def load():
     L.rvcp_shard_rows.argtypes = [u32, u32, u32]
     L.rvcp_shard_rows.restype = u32
     L.rvcp_assemble_frame_async.argtypes = [P, P, u32, u32, u32, u32, P, P]
+    L.rvcp_rccl_unique_id.argtypes = [P]
+    L.rvcp_rccl_init.argtypes = [P, P, u32, u32]
+    L.rvcp_rccl_attach.argtypes = [P, P, u32, u32]
+    L.rvcp_gather_frame_async.argtypes = [P, P, u32, u32, P, P, P]
     for name in ("rvcp_config_default", "rvcp_config_default_for", "rvcp_create", "rvcp_destroy", "rvcp_upload_scene",
                  "rvcp_render", "rvcp_render_shard_async", "rvcp_sync_stats",
                  "rvcp_assemble_frame_async", "rvcp_upload_scene_file", "rvcp_mandelbrot",
-                 "rvcp_render_async", "rvcp_wait"):
+                 "rvcp_render_async", "rvcp_wait", "rvcp_rccl_unique_id", "rvcp_rccl_init",
+                 "rvcp_rccl_attach", "rvcp_gather_frame_async"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

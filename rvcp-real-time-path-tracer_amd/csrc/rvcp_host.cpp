@@ -7,18 +7,23 @@
 // Compiled with hipcc -ffp-contract=off: the frame constants it derives (camera basis,
 // light-area prefix sums, gamma thresholds) use the same float operations as the shader, so
 // the kernel's results stay bit-identical to the CPU oracle.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
 
 #include "../../include/rvcp.h"
 #include "rvcp_internal.h"
+#include "rvcp_scene_prep.h"
 
 using namespace rvcp;
 
@@ -76,9 +81,16 @@ struct rvcp_ctx {
     std::vector<float *> shard_lin;
     std::vector<size_t> shard_cap;
 
+    // one process per GPU: the RCCL communicator of rvcp_gather_frame_async (rank `comm_rank`
+    // of `comm_world`; created by rvcp_rccl_init, or the caller's by rvcp_rccl_attach)
+    ncclComm_t comm = nullptr;
+    bool comm_owned = false;
+    uint32_t comm_world = 0, comm_rank = 0;
+
     // last launch
     bool pending = false;
     bool last_trivial = false;
+    int32_t last_variant = 0;
     uint64_t last_pixels = 0;
     uint32_t last_spp = 0;
 
@@ -96,6 +108,68 @@ int fail(rvcp_ctx *ctx, int code, const std::string &msg)
     return code;
 }
 
+// RCCL, resolved at run time: dlopen("librccl.so.1") returns the copy the process already
+// holds (PyTorch-ROCm's, soname librccl.so.1, or the host's own) and otherwise the system one,
+// so librvcp needs no RCCL to load and shares one RCCL with its host.
+struct RcclApi {
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*gather)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t,
+                           hipStream_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+    bool ok = false;
+    std::string why;
+};
+
+const RcclApi &rccl_api()
+{
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char *e = dlerror();
+            api.why = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+            return;
+        }
+        api.get_unique_id = (decltype(api.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
+        api.gather = (decltype(api.gather))dlsym(h, "ncclGather");
+        api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
+        api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.gather &&
+                 api.error_string;
+        if (!api.ok) api.why = "librccl.so.1 lacks ncclGather / ncclCommInitRank";
+    });
+    return api;
+}
+
+// Report an error without allocating on the failure path that may itself be out of memory.
+int fail_noexcept(rvcp_ctx *ctx, int code, const char *msg) noexcept
+{
+    try {
+        if (ctx) ctx->err = msg;
+        else g_create_error = msg;
+    } catch (...) {
+    }
+    return code;
+}
+
+template <typename F>
+int barrier(rvcp_ctx *ctx, F &&f) noexcept
+{
+    try {
+        return f();
+    } catch (const std::bad_alloc &) {
+        return fail_noexcept(ctx, RVCP_E_NOMEM, "out of host memory");
+    } catch (const std::exception &e) {
+        return fail_noexcept(ctx, RVCP_E_INTERNAL, e.what());
+    } catch (...) {
+        return fail_noexcept(ctx, RVCP_E_INTERNAL, "unknown C++ exception");
+    }
+}
+
 #define HIP_TRY(ctx, expr)                                                                  \
     do {                                                                                    \
         hipError_t e_ = (expr);                                                             \
@@ -103,36 +177,11 @@ int fail(rvcp_ctx *ctx, int code, const std::string &msg)
             return fail((ctx), RVCP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-// ---- host-side vec3 with the shader's evaluation order ----
-struct h3 { float x, y, z; };
-inline h3 mk(float x, float y, float z) { return h3{x, y, z}; }
-inline h3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
-inline h3 add(h3 a, h3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-inline h3 sub(h3 a, h3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-inline h3 muls(h3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
-// the shader builtins, fused as in DESIGN.md §3.1 (these restate shader code, not glam)
-inline float dot(h3 a, h3 b) { return std::fma(a.z, b.z, std::fma(a.y, b.y, a.x * b.x)); }
-inline h3 cross(h3 a, h3 b) {
-    return mk(std::fma(a.y, b.z, -(a.z * b.y)), std::fma(a.z, b.x, -(a.x * b.z)),
-              std::fma(a.x, b.y, -(a.y * b.x)));
-}
-inline float length(h3 a) { return std::sqrt(dot(a, a)); }
-inline h3 normalize(h3 a) { return muls(a, 1.0f / std::sqrt(dot(a, a))); }
-inline void st3(float *d, h3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; }
-
-// get_face_area, ray_tracer_games101_branch.comp:302-307
-float face_area(const rvcp_vertex_t *v, const rvcp_face_t &f)
-{
-    h3 v0 = ld3(v[f.vertices[0]].position), v1 = ld3(v[f.vertices[1]].position);
-    h3 v2 = ld3(v[f.vertices[2]].position);
-    return 0.5f * length(cross(sub(v1, v0), sub(v2, v0)));
-}
-
 // sample_ray's frame constants, :217-227
 void camera_constants(const rvcp_push_constant_t &pc, uint32_t W, uint32_t H, FrameArgs &A)
 {
     const float PI = 3.1415926f;
-    h3 cpos = ld3(pc.camera.position), up = ld3(pc.camera.up), fwd = ld3(pc.camera.forward);
+    h3 cpos = ld3h(pc.camera.position), up = ld3h(pc.camera.up), fwd = ld3h(pc.camera.forward);
     const float rad = pc.camera.vertical_fov / 2.0f * PI / 180.0f;   // degree_to_radian :141
     const float h = 2.0f * pc.camera.t_near * std::tan(rad);
     const float w = h * (float)W / (float)H;
@@ -180,7 +229,7 @@ extern "C" {
 
 const char *rvcp_version(void) { return "rvcp-mi355x 0.1.0 (gfx950)"; }
 
-int rvcp_config_default_for(int32_t integrator, rvcp_config_t *cfg)
+static int impl_config_default_for(int32_t integrator, rvcp_config_t *cfg)
 {
     if (!cfg) return RVCP_E_INVALID;
     if (integrator == RVCP_INTEGRATOR_GAMES101) return rvcp_config_default(cfg);
@@ -199,7 +248,7 @@ int rvcp_config_default_for(int32_t integrator, rvcp_config_t *cfg)
     return RVCP_OK;
 }
 
-int rvcp_config_default(rvcp_config_t *cfg)
+static int impl_config_default(rvcp_config_t *cfg)
 {
     if (!cfg) return RVCP_E_INVALID;
     std::memset(cfg, 0, sizeof(*cfg));
@@ -222,7 +271,7 @@ const char *rvcp_last_error(const rvcp_ctx_t *ctx)
     return ctx ? ctx->err.c_str() : g_create_error.c_str();
 }
 
-int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
+static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
 {
     if (!cfg || !out_ctx) return fail(nullptr, RVCP_E_INVALID, "null argument");
     *out_ctx = nullptr;
@@ -247,6 +296,7 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
 
     rvcp_ctx *ctx = new (std::nothrow) rvcp_ctx();
     if (!ctx) return fail(nullptr, RVCP_E_NOMEM, "out of memory");
+    try {
     ctx->cfg = *cfg;
     ctx->device = cfg->device;
     auto bail = [&](int rc) {
@@ -323,11 +373,15 @@ int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         }
         (void)hipSetDevice(cfg->device);
     }
+    } catch (...) {     // the exception barrier reports it; free what was built
+        rvcp_destroy(ctx);
+        throw;
+    }
     *out_ctx = ctx;
     return RVCP_OK;
 }
 
-int rvcp_destroy(rvcp_ctx_t *ctx)
+static int impl_destroy(rvcp_ctx_t *ctx)
 {
     if (!ctx) return RVCP_OK;
     for (size_t i = 0; i < ctx->subs.size(); i++) {
@@ -339,7 +393,11 @@ int rvcp_destroy(rvcp_ctx_t *ctx)
     }
     ctx->subs.clear();
     (void)hipSetDevice(ctx->device);
+    // a frame still in flight (possibly on the caller's stream) reads the buffers freed below
+    if (ctx->pending && ctx->ev1) (void)hipEventSynchronize(ctx->ev1);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm && ctx->comm_owned) (void)rccl_api().comm_destroy(ctx->comm);
+    ctx->comm = nullptr;
     free_scene(ctx);
     (void)hipFree(ctx->d_gamma);
     (void)hipFree(ctx->d_unorm);
@@ -365,7 +423,7 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
                       const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
                       const uint32_t *lum_sphere_ids, uint32_t n_lum_sphere_ids);
 
-int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_t n_materials,
+static int impl_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_t n_materials,
                       const rvcp_vertex_t *vertices, uint32_t n_vertices,
                       const rvcp_face_t *faces, uint32_t n_faces,
                       const rvcp_sphere_t *spheres, uint32_t n_spheres,
@@ -396,88 +454,30 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
 {
     (void)lum_sphere_ids; (void)n_lum_sphere_ids;
     if (!ctx) return RVCP_E_INVALID;
-    if (!materials || n_materials == 0) return fail(ctx, RVCP_E_INVALID, "need >= 1 material");
-    if ((n_vertices && !vertices) || (n_faces && !faces) || (n_lum_face_ids && !lum_face_ids) ||
-        (n_spheres && !spheres))
-        return fail(ctx, RVCP_E_INVALID, "null array with nonzero length");
-    for (uint32_t i = 0; i < n_spheres; i++)
-        if (spheres[i].material_id >= n_materials)
-            return fail(ctx, RVCP_E_INVALID, "sphere " + std::to_string(i) + " material out of range");
-    for (uint32_t i = 0; i < n_faces; i++) {
-        for (int k = 0; k < 3; k++)
-            if (faces[i].vertices[k] >= n_vertices)
-                return fail(ctx, RVCP_E_INVALID, "face " + std::to_string(i) + " vertex index out of range");
-        if (faces[i].material_id >= n_materials)
-            return fail(ctx, RVCP_E_INVALID, "face " + std::to_string(i) + " material out of range");
-    }
-    for (uint32_t i = 0; i < n_lum_face_ids; i++)
-        if (lum_face_ids[i] >= n_faces)
-            return fail(ctx, RVCP_E_INVALID, "luminous face id out of range");
+    if (ctx->pending)
+        return fail(ctx, RVCP_E_INVALID, "a frame is in flight on this context (rvcp_wait first)");
+    SceneInput in;
+    in.materials = materials; in.n_materials = n_materials;
+    in.vertices = vertices; in.n_vertices = n_vertices;
+    in.faces = faces; in.n_faces = n_faces;
+    in.spheres = spheres; in.n_spheres = n_spheres;
+    in.lum_face_ids = lum_face_ids; in.n_lum_face_ids = n_lum_face_ids;
+    SceneTables tab;
+    std::string err;
+    if (prepare_scene(in, ctx->cfg.lum_id_std140_quirk != 0, tab, err) != RVCP_OK)
+        return fail(ctx, RVCP_E_INVALID, err);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-
-    // triangles: v0, e1 = v1 - v0, e2 = v2 - v0 (:243-248)
-    std::vector<TriRecord> tri(n_faces);
-    for (uint32_t i = 0; i < n_faces; i++) {
-        h3 v0 = ld3(vertices[faces[i].vertices[0]].position);
-        h3 v1 = ld3(vertices[faces[i].vertices[1]].position);
-        h3 v2 = ld3(vertices[faces[i].vertices[2]].position);
-        std::memset(&tri[i], 0, sizeof(TriRecord));
-        st3(tri[i].v0, v0);
-        st3(tri[i].e1, sub(v1, v0));
-        st3(tri[i].e2, sub(v2, v0));
-    }
-    std::vector<MatRecord> mats(n_materials);
-    for (uint32_t i = 0; i < n_materials; i++) {
-        std::memcpy(mats[i].albedo, materials[i].albedo, sizeof(float) * 3);
-        mats[i].ty = materials[i].ty;
-        for (int c = 0; c < 3; c++) mats[i].alb_pi[c] = materials[i].albedo[c] / 3.1415926f;
-        mats[i].pad = 0;
-    }
-    std::vector<FaceShade> shade(n_faces);
-    for (uint32_t i = 0; i < n_faces; i++) {
-        FaceShade &fs = shade[i];
-        std::memset(&fs, 0, sizeof(fs));
-        std::memcpy(fs.n0, vertices[faces[i].vertices[0]].normal, 12);
-        std::memcpy(fs.n1, vertices[faces[i].vertices[1]].normal, 12);
-        std::memcpy(fs.n2, vertices[faces[i].vertices[2]].normal, 12);
-        fs.mat = faces[i].material_id;
-        fs.ty = mats[fs.mat].ty;
-        std::memcpy(fs.alb_pi, mats[fs.mat].alb_pi, 12);
-    }
-    // light table (sample_light_games101, :384-404) with the std140 id quirk (:109-111)
-    const bool quirk = ctx->cfg.lum_id_std140_quirk != 0;
-    std::vector<LightRecord> lights(n_lum_face_ids ? n_lum_face_ids : 1);
-    float total = 0.0f;
-    for (uint32_t i = 0; i < n_lum_face_ids; i++) {
-        const uint32_t id = quirk ? ((4u * i < n_lum_face_ids) ? lum_face_ids[4u * i] : 0u)
-                                  : lum_face_ids[i];
-        total += face_area(vertices, faces[id]);
-    }
-    float run = 0.0f;
-    for (uint32_t i = 0; i < n_lum_face_ids; i++) {
-        const uint32_t id = quirk ? ((4u * i < n_lum_face_ids) ? lum_face_ids[4u * i] : 0u)
-                                  : lum_face_ids[i];
-        const rvcp_face_t &f = faces[id];
-        run += face_area(vertices, f);
-        LightRecord &L = lights[i];
-        std::memset(&L, 0, sizeof(L));
-        L.cum = run;
-        L.face = id;
-        std::memcpy(L.v0, vertices[f.vertices[0]].position, 12);
-        std::memcpy(L.v1, vertices[f.vertices[1]].position, 12);
-        std::memcpy(L.v2, vertices[f.vertices[2]].position, 12);
-        st3(L.n, normalize(ld3(vertices[f.vertices[0]].normal)));
-        std::memcpy(L.le, materials[f.material_id].albedo, 12);
-    }
+    const std::vector<TriRecord> &tri = tab.tri;
+    const float total = tab.light_total;
 
     free_scene(ctx);
     int rc;
     if ((rc = dev_upload<TriRecord>(ctx, &ctx->d_tri, tri.data(), n_faces)) ||
         (rc = dev_upload<rvcp_face_t>(ctx, &ctx->d_faces, faces, n_faces)) ||
         (rc = dev_upload<rvcp_vertex_t>(ctx, &ctx->d_verts, vertices, n_vertices)) ||
-        (rc = dev_upload<MatRecord>(ctx, &ctx->d_mats, mats.data(), n_materials)) ||
-        (rc = dev_upload<FaceShade>(ctx, &ctx->d_shade, shade.data(), n_faces)) ||
-        (rc = dev_upload<LightRecord>(ctx, &ctx->d_lights, lights.data(), n_lum_face_ids)) ||
+        (rc = dev_upload<MatRecord>(ctx, &ctx->d_mats, tab.mats.data(), n_materials)) ||
+        (rc = dev_upload<FaceShade>(ctx, &ctx->d_shade, tab.shade.data(), n_faces)) ||
+        (rc = dev_upload<LightRecord>(ctx, &ctx->d_lights, tab.lights.data(), n_lum_face_ids)) ||
         (rc = dev_upload<rvcp_material_t>(ctx, &ctx->d_rawmats, materials, n_materials)) ||
         (rc = dev_upload<rvcp_sphere_t>(ctx, &ctx->d_spheres, spheres, n_spheres)))
         return rc;
@@ -518,57 +518,18 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     return RVCP_OK;
 }
 
-int rvcp_upload_scene_file(rvcp_ctx_t *ctx, const char *path, rvcp_camera_t *out_camera)
+static int impl_upload_scene_file(rvcp_ctx_t *ctx, const char *path, rvcp_camera_t *out_camera)
 {
     if (!ctx) return RVCP_E_INVALID;
-    if (!path) return fail(ctx, RVCP_E_INVALID, "null path");
-    FILE *f = std::fopen(path, "rb");
-    if (!f) return fail(ctx, RVCP_E_INVALID, std::string("cannot open scene file ") + path);
-    std::vector<unsigned char> data;
-    unsigned char buf[1 << 16];
-    size_t got;
-    while ((got = std::fread(buf, 1, sizeof(buf), f)) > 0) data.insert(data.end(), buf, buf + got);
-    const bool read_error = std::ferror(f) != 0;
-    std::fclose(f);
-    if (read_error) return fail(ctx, RVCP_E_INVALID, "error reading scene file");
-    constexpr size_t kHeader = 128;
-    if (data.size() < kHeader || std::memcmp(data.data(), "RVCPSCN1", 8) != 0)
-        return fail(ctx, RVCP_E_INVALID, "not an RVCPSCN1 scene file");
-    uint32_t version, header_bytes;
-    rvcp_lengths_t L;
-    std::memcpy(&version, data.data() + 8, 4);
-    std::memcpy(&header_bytes, data.data() + 12, 4);
-    std::memcpy(&L, data.data() + 16, sizeof(L));
-    if (version != 1 || header_bytes != kHeader)
-        return fail(ctx, RVCP_E_INVALID, "unsupported scene file version");
-    const uint64_t need = kHeader + 32ull * L.materials_len + 32ull * L.spheres_len +
-                          32ull * L.vertices_len + 16ull * L.faces_len +
-                          4ull * L.luminous_sphere_id_len + 4ull * L.luminous_face_id_len;
-    if (need != data.size())
-        return fail(ctx, RVCP_E_INVALID, "scene file size does not match its lengths");
-    // copy each array into storage of its own type (the byte buffer has no alignment promise)
-    size_t off = kHeader;
-    auto take = [&](auto &vec, uint32_t n) {
-        vec.resize(n);
-        if (n) std::memcpy(vec.data(), data.data() + off, n * sizeof(vec[0]));
-        off += (size_t)n * sizeof(vec[0]);
-    };
-    std::vector<rvcp_material_t> mats;
-    std::vector<rvcp_sphere_t> sph;
-    std::vector<rvcp_vertex_t> verts;
-    std::vector<rvcp_face_t> faces;
-    std::vector<uint32_t> lsph, lface;
-    take(mats, L.materials_len);
-    take(sph, L.spheres_len);
-    take(verts, L.vertices_len);
-    take(faces, L.faces_len);
-    take(lsph, L.luminous_sphere_id_len);
-    take(lface, L.luminous_face_id_len);
-    const int rc = rvcp_upload_scene(ctx, mats.data(), L.materials_len, verts.data(),
-                                     L.vertices_len, faces.data(), L.faces_len, sph.data(),
-                                     L.spheres_len, lface.data(), L.luminous_face_id_len,
-                                     lsph.data(), L.luminous_sphere_id_len);
-    if (rc == RVCP_OK && out_camera) std::memcpy(out_camera, data.data() + 40, sizeof(*out_camera));
+    SceneFile sf;
+    std::string err;
+    if (read_scene_file(path, sf, err) != RVCP_OK) return fail(ctx, RVCP_E_INVALID, err);
+    const rvcp_lengths_t &L = sf.lengths;
+    const int rc = rvcp_upload_scene(ctx, sf.materials.data(), L.materials_len, sf.vertices.data(),
+                                     L.vertices_len, sf.faces.data(), L.faces_len, sf.spheres.data(),
+                                     L.spheres_len, sf.lum_face_ids.data(), L.luminous_face_id_len,
+                                     sf.lum_sphere_ids.data(), L.luminous_sphere_id_len);
+    if (rc == RVCP_OK && out_camera) *out_camera = sf.camera;
     return rc;
 }
 
@@ -582,7 +543,7 @@ uint32_t rvcp_shard_rows(uint32_t height, uint32_t shard_index, uint32_t shard_c
     return rows;
 }
 
-int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
                             uint32_t height, uint32_t shard_index, uint32_t shard_count,
                             void *d_rgba8, void *d_linear_rgb, void *stream)
 {
@@ -593,6 +554,9 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     if ((uint64_t)width * height >= (1ull << 31))
         return fail(ctx, RVCP_E_INVALID, "frame too large (W*H must be < 2^31)");
     if (!ctx->has_scene) return fail(ctx, RVCP_E_NO_SCENE, "render before rvcp_upload_scene");
+    // one frame in flight per context: its surface list, counters and events are the frame's
+    if (ctx->pending)
+        return fail(ctx, RVCP_E_INVALID, "a frame is in flight on this context (rvcp_wait first)");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
 
@@ -708,12 +672,13 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
     ctx->pending = true;
     ctx->last_trivial = trivial;
+    ctx->last_variant = (trivial || A.n_pixels == 0) ? 0 : legacy ? 8 : A.accel ? 7 : A.variant;
     ctx->last_pixels = A.n_pixels;
     ctx->last_spp = A.spp;
     return RVCP_OK;
 }
 
-int rvcp_render_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+static int impl_render_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
                       uint32_t height, void *d_rgba8, void *d_linear_rgb, void *stream)
 {
     if (!ctx) return RVCP_E_INVALID;
@@ -722,12 +687,12 @@ int rvcp_render_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_
     return rvcp_render_shard_async(ctx, push, width, height, 0, 1, d_rgba8, d_linear_rgb, stream);
 }
 
-int rvcp_wait(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
+static int impl_wait(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
 {
     return rvcp_sync_stats(ctx, stats);
 }
 
-int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
+static int impl_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
 {
     if (!ctx) return RVCP_E_INVALID;
     if (!ctx->pending) return fail(ctx, RVCP_E_INVALID, "no render in flight");
@@ -748,6 +713,7 @@ int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         stats->traversals = ctx->last_trivial ? 0 : c[0] + ctx->last_pixels * (ctx->last_spp - 1);
         stats->samples = ctx->last_pixels * ctx->last_spp;
         stats->faces = ctx->n_faces;
+        stats->kernel_variant = ctx->last_variant;
         stats->wave_iterations = c[2];
     }
     if (ctx->last_timeline_waves) {
@@ -830,6 +796,7 @@ static int render_multi(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint3
         total.samples += st.samples;
         total.wave_iterations += st.wave_iterations;
         total.faces = st.faces;
+        total.kernel_variant = st.kernel_variant;
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         const uint32_t stripes = (H + 7) / 8;
         const uint32_t full = H / 8;                       // stripes with 8 rows
@@ -859,11 +826,13 @@ static int render_multi(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint3
     return RVCP_OK;
 }
 
-int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+static int impl_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
                 uint32_t height, uint8_t *out_rgba8, float *out_linear_rgb, rvcp_stats_t *stats)
 {
     if (!ctx) return RVCP_E_INVALID;
     if (!out_rgba8) return fail(ctx, RVCP_E_INVALID, "out_rgba8 is required");
+    if (ctx->pending)
+        return fail(ctx, RVCP_E_INVALID, "a frame is in flight on this context (rvcp_wait first)");
     if (width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 31))
         return fail(ctx, RVCP_E_INVALID, "invalid frame size");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -896,12 +865,14 @@ int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t widt
     return RVCP_OK;
 }
 
-int rvcp_mandelbrot(rvcp_ctx_t *ctx, const rvcp_mandelbrot_push_t *push, uint32_t width,
+static int impl_mandelbrot(rvcp_ctx_t *ctx, const rvcp_mandelbrot_push_t *push, uint32_t width,
                     uint32_t height, uint8_t *out_rgba8, float *out_value, rvcp_stats_t *stats)
 {
     if (!ctx) return RVCP_E_INVALID;
     if (!push || !out_rgba8 || width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 31))
         return fail(ctx, RVCP_E_INVALID, "invalid mandelbrot arguments");
+    if (ctx->pending)
+        return fail(ctx, RVCP_E_INVALID, "a frame is in flight on this context (rvcp_wait first)");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const size_t npx = (size_t)width * height;
     if (ctx->cap_rgba < npx) {
@@ -938,7 +909,7 @@ int rvcp_mandelbrot(rvcp_ctx_t *ctx, const rvcp_mandelbrot_push_t *push, uint32_
     return RVCP_OK;
 }
 
-int rvcp_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t slot_rows,
+static int impl_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t slot_rows,
                               uint32_t width, uint32_t height, uint32_t shard_count,
                               void *d_frame, void *stream)
 {
@@ -954,6 +925,191 @@ int rvcp_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t 
                              (uint32_t *)d_frame, s) != 0)
         return fail(ctx, RVCP_E_HIP, "assemble launch failed");
     return RVCP_OK;
+}
+
+
+// ---- one process per GPU: the frame gather over RCCL ----
+static int impl_rccl_unique_id(uint8_t *out_id)
+{
+    if (!out_id) return fail(nullptr, RVCP_E_INVALID, "null id buffer");
+    const RcclApi &R = rccl_api();
+    if (!R.ok) return fail(nullptr, RVCP_E_UNSUPPORTED, R.why);
+    static_assert(sizeof(ncclUniqueId) == RVCP_RCCL_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    const ncclResult_t r = R.get_unique_id(&id);
+    if (r != ncclSuccess) return fail(nullptr, RVCP_E_HIP, std::string("ncclGetUniqueId: ") + R.error_string(r));
+    std::memcpy(out_id, &id, sizeof(id));
+    return RVCP_OK;
+}
+
+static int impl_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, uint32_t rank)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!id || world == 0 || rank >= world || world > 4096)
+        return fail(ctx, RVCP_E_INVALID, "invalid RCCL rank / world");
+    if (ctx->comm) return fail(ctx, RVCP_E_INVALID, "context already has a communicator");
+    const RcclApi &R = rccl_api();
+    if (!R.ok) return fail(ctx, RVCP_E_UNSUPPORTED, R.why);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = R.comm_init_rank(&comm, (int)world, uid, (int)rank);
+    if (r != ncclSuccess) return fail(ctx, RVCP_E_HIP, std::string("ncclCommInitRank: ") + R.error_string(r));
+    ctx->comm = comm;
+    ctx->comm_owned = true;
+    ctx->comm_world = world;
+    ctx->comm_rank = rank;
+    return RVCP_OK;
+}
+
+static int impl_rccl_attach(rvcp_ctx_t *ctx, void *nccl_comm, uint32_t world, uint32_t rank)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!nccl_comm || world == 0 || rank >= world)
+        return fail(ctx, RVCP_E_INVALID, "invalid communicator / rank / world");
+    if (ctx->comm) return fail(ctx, RVCP_E_INVALID, "context already has a communicator");
+    if (!rccl_api().ok) return fail(ctx, RVCP_E_UNSUPPORTED, rccl_api().why);
+    ctx->comm = (ncclComm_t)nccl_comm;
+    ctx->comm_owned = false;
+    ctx->comm_world = world;
+    ctx->comm_rank = rank;
+    return RVCP_OK;
+}
+
+static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, uint32_t width,
+                                   uint32_t height, void *d_gathered, void *d_frame, void *stream)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!ctx->comm) return fail(ctx, RVCP_E_INVALID, "no communicator (rvcp_rccl_init first)");
+    const bool root = ctx->comm_rank == 0;
+    if (!d_shard_rgba8 || width == 0 || height == 0 || (root && (!d_gathered || !d_frame)))
+        return fail(ctx, RVCP_E_INVALID, "invalid gather arguments");
+    if ((uint64_t)width * height >= (1ull << 31))
+        return fail(ctx, RVCP_E_INVALID, "frame too large (W*H must be < 2^31)");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    const uint32_t N = ctx->comm_world;
+    const uint32_t slot = rvcp_shard_rows(height, 0, N);      // shard 0 has the most rows
+    const ncclResult_t r = rccl_api().gather(d_shard_rgba8, root ? d_gathered : nullptr,
+                                             (size_t)slot * width, ncclUint32, 0, ctx->comm, s);
+    if (r != ncclSuccess) return fail(ctx, RVCP_E_HIP, std::string("ncclGather: ") + rccl_api().error_string(r));
+    if (root && rvcp_launch_assemble((const uint32_t *)d_gathered, slot, width, height, N,
+                                     (uint32_t *)d_frame, s) != 0)
+        return fail(ctx, RVCP_E_HIP, "assemble launch failed");
+    return RVCP_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Exception barrier: every int-returning entry point runs its implementation inside
+// `barrier`, so no C++ exception (std::bad_alloc from a host vector or string, anything a
+// runtime library throws) crosses the C-ABI (rvcp.h conventions).
+// ---------------------------------------------------------------------------------------
+
+int rvcp_config_default_for(int32_t integrator, rvcp_config_t *cfg)
+{
+    return barrier(nullptr, [&] { return impl_config_default_for(integrator, cfg); });
+}
+
+int rvcp_config_default(rvcp_config_t *cfg)
+{
+    return barrier(nullptr, [&] { return impl_config_default(cfg); });
+}
+
+int rvcp_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
+{
+    return barrier(nullptr, [&] { return impl_create(cfg, out_ctx); });
+}
+
+int rvcp_destroy(rvcp_ctx_t *ctx)
+{
+    return barrier(nullptr, [&] { return impl_destroy(ctx); });
+}
+
+int rvcp_upload_scene(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_t n_materials,
+                      const rvcp_vertex_t *vertices, uint32_t n_vertices,
+                      const rvcp_face_t *faces, uint32_t n_faces,
+                      const rvcp_sphere_t *spheres, uint32_t n_spheres,
+                      const uint32_t *lum_face_ids, uint32_t n_lum_face_ids,
+                      const uint32_t *lum_sphere_ids, uint32_t n_lum_sphere_ids)
+{
+    return barrier(ctx, [&] { return impl_upload_scene(ctx, materials, n_materials, vertices,
+        n_vertices, faces, n_faces, spheres, n_spheres, lum_face_ids, n_lum_face_ids,
+        lum_sphere_ids, n_lum_sphere_ids); });
+}
+
+int rvcp_upload_scene_file(rvcp_ctx_t *ctx, const char *path, rvcp_camera_t *out_camera)
+{
+    return barrier(ctx, [&] { return impl_upload_scene_file(ctx, path, out_camera); });
+}
+
+int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+                            uint32_t height, uint32_t shard_index, uint32_t shard_count,
+                            void *d_rgba8, void *d_linear_rgb, void *stream)
+{
+    return barrier(ctx, [&] { return impl_render_shard_async(ctx, push, width, height,
+        shard_index, shard_count, d_rgba8, d_linear_rgb, stream); });
+}
+
+int rvcp_render_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+                      uint32_t height, void *d_rgba8, void *d_linear_rgb, void *stream)
+{
+    return barrier(ctx, [&] { return impl_render_async(ctx, push, width, height, d_rgba8,
+        d_linear_rgb, stream); });
+}
+
+int rvcp_wait(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
+{
+    return barrier(ctx, [&] { return impl_wait(ctx, stats); });
+}
+
+int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
+{
+    return barrier(ctx, [&] { return impl_sync_stats(ctx, stats); });
+}
+
+int rvcp_render(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+                uint32_t height, uint8_t *out_rgba8, float *out_linear_rgb, rvcp_stats_t *stats)
+{
+    return barrier(ctx, [&] { return impl_render(ctx, push, width, height, out_rgba8,
+        out_linear_rgb, stats); });
+}
+
+int rvcp_mandelbrot(rvcp_ctx_t *ctx, const rvcp_mandelbrot_push_t *push, uint32_t width,
+                    uint32_t height, uint8_t *out_rgba8, float *out_value, rvcp_stats_t *stats)
+{
+    return barrier(ctx, [&] { return impl_mandelbrot(ctx, push, width, height, out_rgba8,
+        out_value, stats); });
+}
+
+int rvcp_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t slot_rows,
+                              uint32_t width, uint32_t height, uint32_t shard_count,
+                              void *d_frame, void *stream)
+{
+    return barrier(ctx, [&] { return impl_assemble_frame_async(ctx, d_gathered, slot_rows,
+        width, height, shard_count, d_frame, stream); });
+}
+
+int rvcp_rccl_unique_id(uint8_t *out_id)
+{
+    return barrier(nullptr, [&] { return impl_rccl_unique_id(out_id); });
+}
+
+int rvcp_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, uint32_t rank)
+{
+    return barrier(ctx, [&] { return impl_rccl_init(ctx, id, world, rank); });
+}
+
+int rvcp_rccl_attach(rvcp_ctx_t *ctx, void *nccl_comm, uint32_t world, uint32_t rank)
+{
+    return barrier(ctx, [&] { return impl_rccl_attach(ctx, nccl_comm, world, rank); });
+}
+
+int rvcp_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, uint32_t width,
+                            uint32_t height, void *d_gathered, void *d_frame, void *stream)
+{
+    return barrier(ctx, [&] { return impl_gather_frame_async(ctx, d_shard_rgba8, width, height,
+        d_gathered, d_frame, stream); });
 }
 
 }  // extern "C"

@@ -176,6 +176,35 @@ class RayTracer:
             self._ctx, ctypes.c_void_p(d_gathered), slot_rows, width, height, shard_count,
             ctypes.c_void_p(d_frame), ctypes.c_void_p(stream) if stream else None))
 
+    # ------------------------------------------------------------------ one process per GPU
+    def rccl_init(self, unique_id: bytes, world: int, rank: int):
+        """rvcp_rccl_init: join the frame-gather communicator (collective over `world` ranks;
+        `unique_id` from rccl_unique_id() on rank 0, shared out of band)."""
+        if len(unique_id) != abi.RCCL_ID_BYTES:
+            raise ValueError("unique_id must be 128 bytes")
+        buf = (ctypes.c_uint8 * abi.RCCL_ID_BYTES).from_buffer_copy(unique_id)
+        self._check(self._lib.rvcp_rccl_init(self._ctx, ctypes.cast(buf, ctypes.c_void_p), world, rank))
+
+    def gather_frame_async(self, d_shard: int, width: int, height: int, d_gathered: int = 0,
+                           d_frame: int = 0, stream: int = 0):
+        """rvcp_gather_frame_async: RCCL gather of the shards to rank 0 + device assembly
+        there (d_gathered / d_frame only on rank 0)."""
+        self._check(self._lib.rvcp_gather_frame_async(
+            self._ctx, ctypes.c_void_p(d_shard), width, height,
+            ctypes.c_void_p(d_gathered) if d_gathered else None,
+            ctypes.c_void_p(d_frame) if d_frame else None,
+            ctypes.c_void_p(stream) if stream else None))
+
+
+def rccl_unique_id() -> bytes:
+    """rvcp_rccl_unique_id (rank 0): the 128-byte RCCL communicator id."""
+    L = abi.load()
+    buf = (ctypes.c_uint8 * abi.RCCL_ID_BYTES)()
+    rc = L.rvcp_rccl_unique_id(ctypes.cast(buf, ctypes.c_void_p))
+    if rc != abi.RVCP_OK:
+        raise abi.RvcpError(rc, L.rvcp_last_error(None).decode())
+    return bytes(buf)
+
 
 def shard_rows(height: int, shard_index: int, shard_count: int) -> int:
     """Rows of shard `shard_index` (8-row stripes dealt round-robin).  Pure-Python twin of

@@ -1,0 +1,111 @@
+"""C-ABI contract on the GPU: one frame in flight per context, and the one-process-per-GPU
+RCCL gather (rvcp_rccl_init / rvcp_gather_frame_async) at world size 1 -- the form every
+rank of the multi-GPU bench runs (include/rvcp.h)."""
+import numpy as np
+import pytest
+
+import rvcp_amd
+
+pytestmark = pytest.mark.gpu
+TIME = 123.0
+
+
+def test_one_frame_in_flight(cornell):
+    """A second async frame, an upload or a Mandelbrot call while a frame is pending on the
+    context is rejected (RVCP_E_INVALID) instead of overwriting the pending frame's surface
+    list, counters and events; after rvcp_wait the context renders again, and both frames
+    equal the synchronous render."""
+    torch = pytest.importorskip("torch")
+    W, H = 96, 64
+    with rvcp_amd.RayTracer(spp=3) as rt:
+        rt.upload_scene(cornell)
+        ref = rt.render(W, H, TIME)
+        push = cornell.push_constant(TIME)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        a = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+        b = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+        rt.render_async(push, W, H, a.data_ptr(), stream=s1.cuda_stream)
+        for call in (lambda: rt.render_async(push, W, H, b.data_ptr(), stream=s2.cuda_stream),
+                     lambda: rt.render_shard_async(push, W, H, 0, 2, b.data_ptr(), stream=s2.cuda_stream),
+                     lambda: rt.render(W, H, TIME),
+                     lambda: rt.upload_scene(cornell),
+                     lambda: rt.mandelbrot(rvcp_amd.mandelbrot.Config().push_constant(), 16, 16)):
+            with pytest.raises(rvcp_amd.abi.RvcpError) as e:
+                call()
+            assert e.value.code == rvcp_amd.abi.RVCP_E_INVALID
+            assert "in flight" in str(e.value)
+        st = rt.wait()
+        rt.render_async(push, W, H, b.data_ptr(), stream=s2.cuda_stream)
+        st2 = rt.wait()
+        torch.cuda.synchronize()
+    for t in (a, b):
+        assert np.array_equal(t.cpu().numpy().view(np.uint8).reshape(H, W, 4), ref)
+    assert int(st["traversals"]) == int(st2["traversals"])
+
+
+def test_destroy_with_frame_pending(cornell):
+    """rvcp_destroy waits for a frame still in flight on the caller's stream before it frees
+    the buffers that frame reads."""
+    torch = pytest.importorskip("torch")
+    W, H = 256, 256
+    a = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    rt = rvcp_amd.RayTracer(spp=8)
+    rt.upload_scene(cornell)
+    rt.render_async(cornell.push_constant(TIME), W, H, a.data_ptr(), stream=s.cuda_stream)
+    rt.close()
+    torch.cuda.synchronize()
+    with rvcp_amd.RayTracer(spp=8) as rt2:
+        rt2.upload_scene(cornell)
+        ref = rt2.render(W, H, TIME)
+    assert np.array_equal(a.cpu().numpy().view(np.uint8).reshape(H, W, 4), ref)
+
+
+@pytest.mark.parametrize("W,H", [(128, 96), (77, 45)])
+def test_rccl_gather_world1(cornell, W, H):
+    """rvcp_rccl_init + rvcp_render_shard_async + rvcp_gather_frame_async (ncclGather to
+    rank 0 and device assembly) with one rank == the direct render."""
+    torch = pytest.importorskip("torch")
+    uid = rvcp_amd.rccl_unique_id()
+    assert len(uid) == 128
+    stream = torch.cuda.current_stream().cuda_stream
+    with rvcp_amd.RayTracer(spp=2) as rt:
+        rt.upload_scene(cornell)
+        ref = rt.render(W, H, TIME)
+        rt.rccl_init(uid, 1, 0)
+        slot = rvcp_amd.shard_rows(H, 0, 1)
+        shard = torch.zeros((slot, W), dtype=torch.int32, device="cuda")
+        gathered = torch.zeros((1, slot, W), dtype=torch.int32, device="cuda")
+        frame = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+        for _ in range(2):
+            rt.render_shard_async(cornell.push_constant(TIME), W, H, 0, 1, shard.data_ptr(), stream=stream)
+            rt.gather_frame_async(shard.data_ptr(), W, H, gathered.data_ptr(), frame.data_ptr(), stream=stream)
+            rt.sync_stats()
+        torch.cuda.synchronize()
+        with pytest.raises(rvcp_amd.abi.RvcpError):
+            rt.rccl_init(uid, 1, 0)                     # one communicator per context
+    assert np.array_equal(frame.cpu().numpy().view(np.uint8).reshape(H, W, 4), ref)
+
+
+def test_gather_without_communicator(cornell):
+    torch = pytest.importorskip("torch")
+    d = torch.zeros(64, dtype=torch.int32, device="cuda")
+    with rvcp_amd.RayTracer(spp=1) as rt:
+        with pytest.raises(rvcp_amd.abi.RvcpError) as e:
+            rt.gather_frame_async(d.data_ptr(), 8, 8, d.data_ptr(), d.data_ptr())
+        assert e.value.code == rvcp_amd.abi.RVCP_E_INVALID
+
+
+def test_stats_report_schedule(cornell):
+    """rvcp_stats_t.kernel_variant names the schedule that ran (bench.py picks the rocprof
+    kernel name from it)."""
+    with rvcp_amd.RayTracer(spp=30) as rt:
+        rt.upload_scene(cornell)
+        rt.render(1024, 1024, TIME)
+        assert int(rt.last_stats["kernel_variant"]) == 6
+        rt.render(64, 64, TIME)
+        assert int(rt.last_stats["kernel_variant"]) == 3
+    with rvcp_amd.RayTracer(spp=1) as rt:
+        rt.upload_scene(rvcp_amd.scene.with_random_triangles(cornell, 300))
+        rt.render(32, 32, TIME)
+        assert int(rt.last_stats["kernel_variant"]) == 5

@@ -76,6 +76,12 @@ for s in $STEPS; do
         c5pmcall) run c5pmcall 900 bash tools/c5_pmc.sh ;;
         benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 ;;
         profs) run profs 600 rocprofv3 --kernel-trace --stats -d "$OUT/profs_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 20 --warmup 2 --no-cpu-baseline ;;
+        abi) run pytest_abi 300 python -u -m pytest tests/test_gpu_abi.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+        rehearse8c4) run rehearse8c4 400 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 --workload c4 --steps 5 --warmup 1 ;;
+        rehearse2c4) run rehearse2c4 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 ;;
+        abpk) run abpk 600 bash -c 'bash tools/ab.sh "" packed scalar && bash tools/ab.sh "--size 384 --spp 10" packed scalar && bash tools/ab.sh "--size 2048 --spp 64 --frames 6" packed scalar' ;;
+        configs) run pytest_configs 900 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+        valupmc) run valu_rate_wall 120 tools/build/valu_rate && run valupmc 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/valupmc_$TAG" -o run --output-format csv -- tools/build/valu_rate ;;
         pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     esac
 done

@@ -1,13 +1,16 @@
 // valu_rate.hip -- issue rate of v_fma_f32 vs v_pk_fma_f32 (and v_pk_add/mul_f32) on gfx950,
-// all SIMDs busy, 8 waves per SIMD, 8 independent chains per lane.  Prints wave-instructions
-// per SIMD per clock (from the measured time and the shader clock read by s_memrealtime /
-// the kernel's wall time) and the lane-FLOP rate.
-//   make -C tools build/valu_rate && tools/build/valu_rate
+// all SIMDs busy, 8 waves per SIMD, 8 independent chains per lane.  Prints the wall time,
+// wave-instructions per SIMD per clock AT AN ASSUMED 2.4 GHz and the lane-FLOP rate.  The
+// clock-independent figure comes from running it under rocprofv3 --pmc SQ_INSTS_VALU
+// GRBM_GUI_ACTIVE (tools/pmc_valu.py): wave-instructions / (GRBM cycles per XCD x 1024 SIMDs).
+// Each launch runs `iters` x 8 instructions per lane (default 65536: ~5 ms, long enough for
+// the GRBM clock quotient, MI355X_MICROARCH.md "DVFS give-back").
+//   make -C tools build/valu_rate && tools/build/valu_rate [iters]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 
-constexpr int kIters = 4096;
 
 #define FMA8(op)                                                                          \
     asm volatile(op " %0, %0, %8, %9\n\t" op " %1, %1, %8, %9\n\t" op " %2, %2, %8, %9\n\t"  \
@@ -17,7 +20,7 @@ constexpr int kIters = 4096;
                    "+v"(a7)                                                                   \
                  : "v"(m), "v"(c))
 
-__global__ void k_fma(float *out, float seed) {
+__global__ void k_fma(float *out, float seed, int kIters) {
     float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
           a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     const float m = 0.999f, c = 1e-3f;
@@ -25,9 +28,60 @@ __global__ void k_fma(float *out, float seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
 }
 
+// The same v_fma_f32 streams with inline-constant operands (one VGPR read per instruction)
+// and with 16 independent chains: whether operand reads, not the issue slot, set the rate.
+#define FMA8IC                                                                              \
+    asm volatile("v_fma_f32 %0, %0, 0.5, 1.0\n\tv_fma_f32 %1, %1, 0.5, 1.0\n\t"           \
+                 "v_fma_f32 %2, %2, 0.5, 1.0\n\tv_fma_f32 %3, %3, 0.5, 1.0\n\t"           \
+                 "v_fma_f32 %4, %4, 0.5, 1.0\n\tv_fma_f32 %5, %5, 0.5, 1.0\n\t"           \
+                 "v_fma_f32 %6, %6, 0.5, 1.0\n\tv_fma_f32 %7, %7, 0.5, 1.0"                 \
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6),    \
+                   "+v"(a7))
+
+__global__ void k_fma_ic(float *out, float seed, int kIters) {
+    float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+          a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    for (int i = 0; i < kIters; i++) { FMA8IC; }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
+__global__ void k_fma16(float *out, float seed, int kIters) {
+    float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+          a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    float b0 = a0 + 8, b1 = a0 + 9, b2 = a0 + 10, b3 = a0 + 11, b4 = a0 + 12, b5 = a0 + 13,
+          b6 = a0 + 14, b7 = a0 + 15;
+    const float m = 0.999f, c = 1e-3f;
+    for (int i = 0; i < kIters / 2; i++) {
+        FMA8("v_fma_f32");
+        asm volatile("v_fma_f32 %0, %0, %8, %9\n\tv_fma_f32 %1, %1, %8, %9\n\t"
+                     "v_fma_f32 %2, %2, %8, %9\n\tv_fma_f32 %3, %3, %8, %9\n\t"
+                     "v_fma_f32 %4, %4, %8, %9\n\tv_fma_f32 %5, %5, %8, %9\n\t"
+                     "v_fma_f32 %6, %6, %8, %9\n\tv_fma_f32 %7, %7, %8, %9"
+                     : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3), "+v"(b4), "+v"(b5), "+v"(b6), "+v"(b7)
+                     : "v"(m), "v"(c));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] =
+        a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + b0 + b1 + b2 + b3 + b4 + b5 + b6 + b7;
+}
+
+// v_mov_b32 (no arithmetic): the bare issue rate of a one-operand VALU instruction
+__global__ void k_mov(float *out, float seed, int kIters) {
+    float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+          a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const float m = 1.0f;
+    for (int i = 0; i < kIters; i++) {
+        asm volatile("v_mov_b32 %0, %8\n\tv_mov_b32 %1, %8\n\tv_mov_b32 %2, %8\n\t"
+                     "v_mov_b32 %3, %8\n\tv_mov_b32 %4, %8\n\tv_mov_b32 %5, %8\n\t"
+                     "v_mov_b32 %6, %8\n\tv_mov_b32 %7, %8"
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                     : "v"(m));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
 typedef float v2f __attribute__((ext_vector_type(2)));
 
-__global__ void k_pkfma(float *out, float seed) {
+__global__ void k_pkfma(float *out, float seed, int kIters) {
     v2f a0 = {seed + threadIdx.x, seed}, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
         a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     const v2f m = {0.999f, 0.998f}, c = {1e-3f, 2e-3f};
@@ -44,7 +98,7 @@ __global__ void k_pkfma(float *out, float seed) {
                    "+v"(a7)                                                                   \
                  : "v"(m))
 
-__global__ void k_add(float *out, float seed) {
+__global__ void k_add(float *out, float seed, int kIters) {
     float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
           a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     const float m = 1e-3f;
@@ -52,7 +106,7 @@ __global__ void k_add(float *out, float seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
 }
 
-__global__ void k_pkadd(float *out, float seed) {
+__global__ void k_pkadd(float *out, float seed, int kIters) {
     v2f a0 = {seed + threadIdx.x, seed}, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
         a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     const v2f m = {1e-3f, 2e-3f};
@@ -61,7 +115,7 @@ __global__ void k_pkadd(float *out, float seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = s.x + s.y;
 }
 
-__global__ void k_pkmul(float *out, float seed) {
+__global__ void k_pkmul(float *out, float seed, int kIters) {
     v2f a0 = {seed + threadIdx.x, seed}, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
         a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     const v2f m = {0.999f, 0.998f};
@@ -72,13 +126,13 @@ __global__ void k_pkmul(float *out, float seed) {
 
 template <typename K>
 static void run(const char *name, K kern, int lanes_per_instr, int flops_per_lane, float *out,
-                int blocks, int threads) {
+                int blocks, int threads, int kIters) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, out, 1.0f);   // warm
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, out, 1.0f, kIters);   // warm
     (void)hipEventRecord(a);
-    for (int r = 0; r < 5; r++) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, out, 1.0f);
+    for (int r = 0; r < 5; r++) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, out, 1.0f, kIters);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     float ms = 0;
@@ -94,14 +148,18 @@ static void run(const char *name, K kern, int lanes_per_instr, int flops_per_lan
                 winstr * 64 * lanes_per_instr * flops_per_lane / s * 1e-12);
 }
 
-int main() {
+int main(int argc, char **argv) {
+    const int iters = argc > 1 ? std::atoi(argv[1]) : 65536;
     const int threads = 256, blocks = 256 * 8;   // 8 waves per SIMD
     float *out = nullptr;
     if (hipMalloc(&out, sizeof(float) * threads * blocks) != hipSuccess) return 2;
-    run("v_fma_f32", k_fma, 1, 2, out, blocks, threads);
-    run("v_pk_fma_f32", k_pkfma, 2, 2, out, blocks, threads);
-    run("v_add_f32", k_add, 1, 1, out, blocks, threads);
-    run("v_pk_add_f32", k_pkadd, 2, 1, out, blocks, threads);
-    run("v_pk_mul_f32", k_pkmul, 2, 1, out, blocks, threads);
+    run("v_fma_f32", k_fma, 1, 2, out, blocks, threads, iters);
+    run("v_pk_fma_f32", k_pkfma, 2, 2, out, blocks, threads, iters);
+    run("v_add_f32", k_add, 1, 1, out, blocks, threads, iters);
+    run("v_pk_add_f32", k_pkadd, 2, 1, out, blocks, threads, iters);
+    run("v_pk_mul_f32", k_pkmul, 2, 1, out, blocks, threads, iters);
+    run("v_fma_f32 ic", k_fma_ic, 1, 2, out, blocks, threads, iters);
+    run("v_fma_f32 x16", k_fma16, 1, 2, out, blocks, threads, iters);
+    run("v_mov_b32", k_mov, 1, 0, out, blocks, threads, iters);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 2;
 }
