@@ -32,8 +32,8 @@ profiles/ (tools/pmc_traffic.py), when one exists for the workload and kernel sc
 test), which exceeds the HBM peak because the scene is served on-chip.  `valu_busy_pmc` /
 `valu_issue_frac_pmc` come from the committed SQ counter passes (tools/pmc_valu.py).
 `cpu_baseline` times the scalar C oracle (oracle/rvcp_oracle.c, the CPU re-execution of the
-same kernel) on the box's CPU share (OMP_NUM_THREADS threads, 16 per GPU on the GPU box), rank
-0 at N=1 only.
+same kernel) on every hardware thread of the host (`cores`), with the box's CPU share
+(OMP_NUM_THREADS, 16 per GPU) and one thread timed beside it, rank 0 at N=1 only.
 """
 import argparse
 import json
@@ -120,8 +120,28 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(sc, cfg_kw, W, H, threads):
-    """Time the CPU oracle (scalar C re-execution) on a bounded sample of the workload."""
+def host_threads():
+    """Hardware threads this process may run on (the whole host, not OMP_NUM_THREADS)."""
+    try:
+        return len(os.sched_getaffinity(0)) or 1
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 quota (cpu.max), or None when unlimited/unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(sc, cfg_kw, W, H, threads, share_threads=0):
+    """Time the CPU oracle (scalar C re-execution) on a bounded sample of the workload:
+    `threads` (default: every hardware thread of the host) on the whole frame, the box's CPU
+    share (`share_threads`, OMP_NUM_THREADS) on the same frame, and 1 thread on a row sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     import rvcp_amd
@@ -148,6 +168,13 @@ def cpu_baseline(sc, cfg_kw, W, H, threads):
     O.render(arrays, push, cfg, W, H, threads=threads, want_linear=False)
     dt = time.perf_counter() - t0
     samples = W * H * cfg_kw["spp"]
+    share = {}
+    if share_threads and share_threads != threads:
+        t2 = time.perf_counter()
+        O.render(arrays, push, cfg, W, H, threads=share_threads, want_linear=False)
+        dt2 = time.perf_counter() - t2
+        share = dict(share_threads=share_threads, share_value=round(samples / dt2 / 1e6, 4),
+                     share_seconds=round(dt2, 3))
     rows1 = list(range(0, H, 64 if H >= 256 else 8))
     t1 = time.perf_counter()
     for y in rows1:
@@ -158,7 +185,8 @@ def cpu_baseline(sc, cfg_kw, W, H, threads):
                 seconds=round(dt, 3),
                 single_thread_value=round(len(rows1) * W * cfg_kw["spp"] / dt1 / 1e6, 4),
                 single_thread_sample=f"every {64 if H >= 256 else 8}th row ({len(rows1)} rows), 1 thread",
-                single_thread_seconds=round(dt1, 3), cpu=cpu_model())
+                single_thread_seconds=round(dt1, 3), cpu=cpu_model(),
+                cgroup_cpu_quota=cgroup_cpu_quota(), **share)
 
 
 def main():
@@ -170,8 +198,8 @@ def main():
                     help="default: c3 at N=1 (headline), c4 at N>1 (BASELINE's 8-GPU config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="oracle threads for cpu_baseline (default: OMP_NUM_THREADS, else the "
-                         "CPUs this process may use)")
+                    help="oracle threads for cpu_baseline (default: every hardware thread "
+                         "this process may use; the OMP_NUM_THREADS share is timed beside it)")
     ap.add_argument("--save-frame", default="")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
@@ -385,8 +413,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O
-            threads = args.cpu_threads or O.default_threads()
-            out["cpu_baseline"] = cpu_baseline(sc, cfg_kw, W, H, threads)
+            threads = args.cpu_threads or host_threads()
+            out["cpu_baseline"] = cpu_baseline(sc, cfg_kw, W, H, threads,
+                                               share_threads=O.default_threads())
         print(json.dumps(out), flush=True)
 
     rt.close()

@@ -32,7 +32,7 @@ lscpu > "$OUT/lscpu.txt" 2>&1 || true
 for s in $STEPS; do
     case $s in
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
         newtests) run pytest_new 600 python -m pytest tests/test_golden_frames.py tests/test_interactive.py tests/test_scene_io.py tests/test_mandelbrot.py -m gpu -x -q ;;
         headless) run headless 300 python tools/headless.py --frames 120 --size 384 --spp 10 --dump gpurun_out/headless --format png --script walk ;;
         timeline) run timeline 300 bash -c "rm -f /tmp/tl.bin && RVCP_DEBUG_TIMELINE=/tmp/tl.bin python tools/frames.py --frames 3 && python tools/timeline.py /tmp/tl.bin --waves \$(python -c 'import os;print(os.path.getsize(\"/tmp/tl.bin\")//96)')" ;;
