@@ -123,6 +123,11 @@ enum {
     RVCP_ACCEL_BVH = 1,               /* opt-in BVH (README.md:28-32 TODO "BVH") */
 };
 
+enum {
+    RVCP_UNORM_DRIVER = 0,            /* the reference driver's 12-bit fixed-point conversion */
+    RVCP_UNORM_NEAREST = 1,           /* round-to-nearest */
+};
+
 typedef struct rvcp_config {
     int32_t device;                   /* HIP device ordinal */
     int32_t integrator;               /* RVCP_INTEGRATOR_* */
@@ -161,7 +166,14 @@ typedef struct rvcp_config {
      * a 1-GPU render.  The single-process form of SURVEY.md §8(e); one process per GPU with
      * rvcp_render_shard_async + an RCCL gather (bench.py) is the other. */
     int32_t n_gpus;
-    uint32_t _reserved[3];
+    /* Float -> UNORM8 conversion of the stored colour (imageStore to the R8G8B8A8/B8G8R8A8
+     * UNORM image, ray_tracer_games101_branch.comp:500, ray_tracer.comp:822,
+     * mandelbrot.comp:33).  RVCP_UNORM_DRIVER (0, default): the conversion the reference's
+     * driver performed, measured on its own render Notes/README/fractal.png (every one of its
+     * 1,048,576 pixels reproduced): u8 = (floor(4096 x) * 255 + 2048) >> 12.
+     * RVCP_UNORM_NEAREST (1): round-to-nearest, u8 = floor(255 x + 1/2). */
+    int32_t unorm_rule;
+    uint32_t _reserved[2];
 } rvcp_config_t;
 
 /* Per-render statistics (all optional). */

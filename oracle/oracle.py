@@ -49,8 +49,13 @@ def lib():
                                          u32, u32, u32, u32, u32, u32, P, P, P, ctypes.c_int]
         L.rvcp_oracle_unorm_u8.argtypes = [ctypes.c_float]
         L.rvcp_oracle_unorm_u8.restype = ctypes.c_uint8
+        for f in ("rvcp_oracle_unorm_u8_rule", "rvcp_oracle_gamma_u8_rule"):
+            getattr(L, f).argtypes = [ctypes.c_float, ctypes.c_int]
+            getattr(L, f).restype = ctypes.c_uint8
+        L.rvcp_oracle_gamma_threshold_rule.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.rvcp_oracle_gamma_threshold_rule.restype = ctypes.c_float
         L.rvcp_oracle_render.restype = ctypes.c_int
-        L.rvcp_oracle_mandelbrot.argtypes = [P, u32, u32, P, P]
+        L.rvcp_oracle_mandelbrot.argtypes = [P, u32, u32, ctypes.c_int, P, P]
         L.rvcp_oracle_mandelbrot.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -64,12 +69,18 @@ def sinf(x: float) -> float:
     return float(lib().rvcp_oracle_sinf(ctypes.c_float(x)))
 
 
-def gamma_u8(c: float) -> int:
-    return int(lib().rvcp_oracle_gamma_u8(ctypes.c_float(c)))
+def gamma_u8(c: float, unorm_rule: int = 0) -> int:
+    """pow(clamp(c), 0.6) stored as UNORM8 under rvcp_config_t.unorm_rule (0 driver, 1 nearest)."""
+    return int(lib().rvcp_oracle_gamma_u8_rule(ctypes.c_float(c), int(unorm_rule)))
 
 
-def unorm_u8(c: float) -> int:
-    return int(lib().rvcp_oracle_unorm_u8(ctypes.c_float(c)))
+def unorm_u8(c: float, unorm_rule: int = 0) -> int:
+    """clamp(c) stored as UNORM8 under rvcp_config_t.unorm_rule (0 driver, 1 nearest)."""
+    return int(lib().rvcp_oracle_unorm_u8_rule(ctypes.c_float(c), int(unorm_rule)))
+
+
+def gamma_threshold(k: int, unorm_rule: int = 0) -> float:
+    return float(lib().rvcp_oracle_gamma_threshold_rule(int(k), int(unorm_rule)))
 
 
 def rand_sequence(time: float, u: float, v: float, n: int) -> np.ndarray:
@@ -134,13 +145,13 @@ def render(scene_arrays: dict, push, cfg, W, H, rect=None, threads=None, want_li
     return lin, rgba, int(trav[0])
 
 
-def mandelbrot(push, W, H):
+def mandelbrot(push, W, H, unorm_rule=0):
     """The Mandelbrot operator (mandelbrot.comp): returns (rgba [H,W,4] u8, i [H,W] f32).
-    push: a MANDELBROT_PUSH_DTYPE record (position[2], scale)."""
+    push: a MANDELBROT_PUSH_DTYPE record (position[2], scale); unorm_rule: rvcp_config_t's."""
     push = np.ascontiguousarray(push)
     rgba = np.zeros((H, W, 4), dtype=np.uint8)
     val = np.zeros((H, W), dtype=np.float32)
-    rc = lib().rvcp_oracle_mandelbrot(_ptr(push), W, H, _ptr(rgba), _ptr(val))
+    rc = lib().rvcp_oracle_mandelbrot(_ptr(push), W, H, int(unorm_rule), _ptr(rgba), _ptr(val))
     if rc != 0:
         raise ValueError(f"rvcp_oracle_mandelbrot failed: {rc}")
     return rgba, val

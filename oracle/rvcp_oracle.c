@@ -47,6 +47,7 @@ typedef struct {
     float att_stop, t_min, t_max, rr, eps;
     int quirk;
     int integrator;          /* 0 = games101 (dispatched), 1 = ray_tracer.comp ray_trace */
+    int unorm_rule;          /* rvcp_config_t.unorm_rule */
 } params_t;
 
 /* ------------------------------------------------------------------------------------- */
@@ -467,23 +468,38 @@ static v3 ray_trace_legacy(const scene_t *sc, const params_t *P, rng_t *g, ray_t
     return color;
 }
 
-/* UNORM8 store without gamma (ray_tracer.comp:820-822): u8 = #{k : c >= U[k]},
- * U[k] = float((k - 0.5) / 255). */
-static float g_unorm_T[256];
+/* Float -> UNORM8 conversion of the stored value x in [0, 1], two rules
+ * (rvcp_config_t.unorm_rule):
+ *   0 RVCP_UNORM_DRIVER  -- the reference driver's: q = floor(4096 x), u8 = (255 q + 2048) >> 12,
+ *                           fitted to the reference's own render Notes/README/fractal.png
+ *                           (tests/test_mandelbrot.py pins it on every pixel);
+ *   1 RVCP_UNORM_NEAREST -- u8 = floor(255 x + 1/2).
+ * Both are applied as a count of thresholds: u8 = #{k in 1..255 : x >= G[k]}, with
+ * G[k] = ceil((4096 k - 2048) / 255) / 4096 (driver) or (k - 1/2) / 255 (nearest). */
+static double unorm_G(int rule, int k)
+{
+    return rule == 1 ? (k - 0.5) / 255.0 : ceil((4096.0 * k - 2048.0) / 255.0) / 4096.0;
+}
+static float g_unorm_T[2][256];
 static pthread_once_t g_unorm_once = PTHREAD_ONCE_INIT;
 static void unorm_init(void)
 {
-    g_unorm_T[0] = 0.0f;
-    for (int k = 1; k < 256; k++) g_unorm_T[k] = (float)((k - 0.5) / 255.0);
+    for (int r = 0; r < 2; r++) {
+        g_unorm_T[r][0] = 0.0f;
+        for (int k = 1; k < 256; k++) g_unorm_T[r][k] = (float)unorm_G(r, k);
+    }
 }
-uint8_t rvcp_oracle_unorm_u8(float c)
+static int rule_index(int rule) { return rule == 1 ? 1 : 0; }
+uint8_t rvcp_oracle_unorm_u8_rule(float c, int rule)
 {
     pthread_once(&g_unorm_once, unorm_init);
+    const float *T = g_unorm_T[rule_index(rule)];
     float x = (c > 0.0f) ? ((c < 1.0f) ? c : 1.0f) : 0.0f;
     int n = 0;
-    for (int k = 1; k < 256; k++) n += (x >= g_unorm_T[k]);
+    for (int k = 1; k < 256; k++) n += (x >= T[k]);
     return (uint8_t)n;
 }
+uint8_t rvcp_oracle_unorm_u8(float c) { return rvcp_oracle_unorm_u8_rule(c, 0); }
 
 /* ------------------------------------------------------------------------------------- */
 /* Camera: sample_ray, :217-235                                                            */
@@ -518,28 +534,33 @@ static ray_t sample_ray(const cam_t *c, float u_, float v_, float W, float H)
 
 /* ------------------------------------------------------------------------------------- */
 /* Tone map: pow(clamp(c, 0, 1), 0.6) (:498) then UNORM8 store (:500).                     */
-/* u8 = #{k in 1..255 : c >= T[k]}, T[k] = float(((k-0.5)/255)^(1/0.6)).   */
+/* u8 = #{k in 1..255 : c >= T[k]}, T[k] = float(G[k]^(1/0.6)) (G above).   */
 /* ------------------------------------------------------------------------------------- */
-static float g_gamma_T[256];
+static float g_gamma_T[2][256];
 static pthread_once_t g_gamma_once = PTHREAD_ONCE_INIT;
 static void gamma_init(void)
 {
-    g_gamma_T[0] = 0.0f;
-    for (int k = 1; k < 256; k++) g_gamma_T[k] = (float)pow((k - 0.5) / 255.0, 1.0 / 0.6);
+    for (int r = 0; r < 2; r++) {
+        g_gamma_T[r][0] = 0.0f;
+        for (int k = 1; k < 256; k++) g_gamma_T[r][k] = (float)pow(unorm_G(r, k), 1.0 / 0.6);
+    }
 }
-uint8_t rvcp_oracle_gamma_u8(float c)
+uint8_t rvcp_oracle_gamma_u8_rule(float c, int rule)
 {
     pthread_once(&g_gamma_once, gamma_init);
+    const float *T = g_gamma_T[rule_index(rule)];
     float x = (c > 0.0f) ? ((c < 1.0f) ? c : 1.0f) : 0.0f;     /* clamp, NaN -> 0 */
     int n = 0;
-    for (int k = 1; k < 256; k++) n += (x >= g_gamma_T[k]);
+    for (int k = 1; k < 256; k++) n += (x >= T[k]);
     return (uint8_t)n;
 }
-float rvcp_oracle_gamma_threshold(int k)
+uint8_t rvcp_oracle_gamma_u8(float c) { return rvcp_oracle_gamma_u8_rule(c, 0); }
+float rvcp_oracle_gamma_threshold_rule(int k, int rule)
 {
     pthread_once(&g_gamma_once, gamma_init);
-    return (k >= 0 && k < 256) ? g_gamma_T[k] : 0.0f;
+    return (k >= 0 && k < 256) ? g_gamma_T[rule_index(rule)][k] : 0.0f;
 }
+float rvcp_oracle_gamma_threshold(int k) { return rvcp_oracle_gamma_threshold_rule(k, 0); }
 
 /* ------------------------------------------------------------------------------------- */
 /* main, :486-501, over a sub-rectangle of a W x H frame, multi-threaded by rows           */
@@ -573,10 +594,12 @@ static void render_pixel(job_t *J, uint32_t x, uint32_t y, uint32_t out_idx)
         J->lin[3 * (size_t)out_idx + 2] = color.z;
     }
     if (J->rgba) {
-        uint8_t (*q)(float) = J->P->integrator == 1 ? rvcp_oracle_unorm_u8 : rvcp_oracle_gamma_u8;
-        J->rgba[4 * (size_t)out_idx + 0] = q(color.x);
-        J->rgba[4 * (size_t)out_idx + 1] = q(color.y);
-        J->rgba[4 * (size_t)out_idx + 2] = q(color.z);
+        uint8_t (*q)(float, int) = J->P->integrator == 1 ? rvcp_oracle_unorm_u8_rule
+                                                         : rvcp_oracle_gamma_u8_rule;
+        const int rule = J->P->unorm_rule;
+        J->rgba[4 * (size_t)out_idx + 0] = q(color.x, rule);
+        J->rgba[4 * (size_t)out_idx + 1] = q(color.y, rule);
+        J->rgba[4 * (size_t)out_idx + 2] = q(color.z, rule);
         J->rgba[4 * (size_t)out_idx + 3] = 255;
     }
 }
@@ -624,7 +647,7 @@ int rvcp_oracle_render(const rvcp_material_t *materials, uint32_t n_materials,
                    lum_face_ids, n_lum_face_ids, spheres, cfg->integrator == 1 ? n_spheres : 0 };
     params_t P = { cfg->spp, cfg->max_bounces, cfg->attenuation_stop_eps, cfg->ray_t_min,
                    cfg->ray_t_max, cfg->rr_probability, cfg->eps, cfg->lum_id_std140_quirk,
-                   cfg->integrator };
+                   cfg->integrator, cfg->unorm_rule };
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     job_t *jobs = (job_t *)calloc((size_t)nthreads, sizeof(job_t));
@@ -657,12 +680,16 @@ int rvcp_oracle_render(const rvcp_material_t *materials, uint32_t n_materials,
 /* ------------------------------------------------------------------------------------- */
 /* The Mandelbrot operator, assets/shaders/mandelbrot.comp:12-33 (single-threaded).       */
 /* out_rgba: W*H*4 grey UNORM8 of the escape time i; out_value (optional): i per pixel.    */
+/* The iteration is evaluated as the reference's compiled shader evaluated it (DESIGN.md  */
+/* §3.7): the two products of z.x' contracted into one fma, and z.y*z.x + z.x*z.y (which  */
+/* is exactly 2*(z.x*z.y)) contracted with + c.y into fma(z.x + z.x, z.y, c.y); with the   */
+/* driver's UNORM rule this reproduces Notes/README/fractal.png on every pixel; length is */
+/* √dot with the fused 2-D dot of §3.1.                                                   */
 /* ------------------------------------------------------------------------------------- */
 int rvcp_oracle_mandelbrot(const rvcp_mandelbrot_push_t *push, uint32_t W, uint32_t H,
-                           uint8_t *out_rgba, float *out_value)
+                           int unorm_rule, uint8_t *out_rgba, float *out_value)
 {
     if (!push || !out_rgba || !W || !H) return RVCP_E_INVALID;
-    pthread_once(&g_unorm_once, unorm_init);
     for (uint32_t y = 0; y < H; y++) {
         for (uint32_t x = 0; x < W; x++) {
             float nx = ((float)x + 0.5f) / (float)W;                  /* :13 */
@@ -674,14 +701,14 @@ int rvcp_oracle_mandelbrot(const rvcp_mandelbrot_push_t *push, uint32_t W, uint3
             cy = cy - 0.0f;
             float zx = 0.0f, zy = 0.0f, i;
             for (i = 0.0f; i < 1.0f; i += 0.005f) {                    /* :21 */
-                float nzx = zx * zx - zy * zy + cx;
-                float nzy = zy * zx + zx * zy + cy;
+                float nzx = fmaf(zx, zx, -(zy * zy)) + cx;            /* :22-25 */
+                float nzy = fmaf(zx + zx, zy, cy);
                 zx = nzx;
                 zy = nzy;
-                if (sqrtf(zx * zx + zy * zy) > 4.0f) break;          /* length(z) > 4 */
+                if (sqrtf(fmaf(zy, zy, zx * zx)) > 4.0f) break;      /* length(z) > 4, §3.1 dot */
             }
             const size_t p = (size_t)y * W + x;
-            const uint8_t u = rvcp_oracle_unorm_u8(i);                /* vec4(vec3(i), 1) */
+            const uint8_t u = rvcp_oracle_unorm_u8_rule(i, unorm_rule); /* vec4(vec3(i), 1) */
             out_rgba[4 * p + 0] = u;
             out_rgba[4 * p + 1] = u;
             out_rgba[4 * p + 2] = u;

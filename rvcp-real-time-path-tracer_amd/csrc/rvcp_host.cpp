@@ -282,6 +282,8 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
     if (cfg->n_gpus < 0 || cfg->n_gpus > 64)
         return fail(nullptr, RVCP_E_INVALID, "n_gpus must be in [0, 64]");
+    if (cfg->unorm_rule != RVCP_UNORM_DRIVER && cfg->unorm_rule != RVCP_UNORM_NEAREST)
+        return fail(nullptr, RVCP_E_INVALID, "unknown unorm_rule");
     if (cfg->accel != RVCP_ACCEL_NONE && cfg->accel != RVCP_ACCEL_BVH)
         return fail(nullptr, RVCP_E_INVALID, "unknown accel");
     if (cfg->accel == RVCP_ACCEL_BVH && cfg->integrator != RVCP_INTEGRATOR_GAMES101)
@@ -311,14 +313,21 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         hipEventCreate(&ctx->ev1) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "stream/event creation failed"));
 
-    // Gamma thresholds T[k] = float(((k - 0.5) / 255)^(1/0.6)), DESIGN.md §3.3
+    // UNORM8 thresholds on the stored value g: u8 >= k  <=>  g >= G[k].
+    // RVCP_UNORM_DRIVER: u8 = (floor(4096 g) * 255 + 2048) >> 12, so G[k] = m_k / 4096 with
+    // m_k = ceil((4096 k - 2048) / 255) (exact in float); RVCP_UNORM_NEAREST: G[k] = (k - 1/2) / 255.
+    // Gamma thresholds on the linear colour: T[k] = float(G[k]^(1/0.6)) (pow(c, 0.6), :498).
+    double G[256];
+    for (int k = 1; k < 256; k++)
+        G[k] = cfg->unorm_rule == RVCP_UNORM_NEAREST ? (k - 0.5) / 255.0
+                                                     : std::ceil((4096.0 * k - 2048.0) / 255.0) / 4096.0;
     float T[257];
     T[0] = 0.0f;
-    for (int k = 1; k < 256; k++) T[k] = (float)std::pow((k - 0.5) / 255.0, 1.0 / 0.6);
+    for (int k = 1; k < 256; k++) T[k] = (float)std::pow(G[k], 1.0 / 0.6);
     T[256] = INFINITY;
     if ((rc = dev_upload<float>(ctx, &ctx->d_gamma, T, 257)) != RVCP_OK) return bail(rc);
-    // UNORM8 thresholds U[k] = float((k - 0.5) / 255) for ray_tracer.comp's gamma-free store
-    for (int k = 1; k < 256; k++) T[k] = (float)((k - 0.5) / 255.0);
+    // the gamma-free store of ray_tracer.comp:820-822 and mandelbrot.comp:32-33
+    for (int k = 1; k < 256; k++) T[k] = (float)G[k];
     if ((rc = dev_upload<float>(ctx, &ctx->d_unorm, T, 257)) != RVCP_OK) return bail(rc);
     if (hipMalloc((void **)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "hipMalloc counters"));

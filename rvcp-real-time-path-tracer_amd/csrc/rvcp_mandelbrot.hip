@@ -1,8 +1,11 @@
 // rvcp_mandelbrot.hip -- the reference's second compute operator,
 // assets/shaders/mandelbrot.comp:1-33 (push constant {vec2 position; float scale}, one
 // invocation per pixel, escape "time" i in steps of 0.005 written as grey UNORM8).
-// Numeric contract as for the path tracer: f32, no contraction, IEEE
-// division / sqrt, so each pixel is bit-identical to oracle/rvcp_oracle.c.
+// Numeric contract: f32, IEEE division / sqrt, and the iteration contracted
+// the way the reference's compiled shader evaluates it -- z.x' = fma(z.x, z.x, -(z.y*z.y)) + c.x,
+// z.y' = fma(z.x + z.x, z.y, c.y) -- which, with the driver's UNORM8 conversion (the unorm_t
+// table), reproduces the reference's own render (Notes/README/fractal.png) on every pixel;
+// bit-identical to oracle/rvcp_oracle.c.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -31,11 +34,13 @@ __global__ __launch_bounds__(kTileX * kTileY) void mandelbrot_kernel(
     // :20-31
     float zx = 0.0f, zy = 0.0f, i;
     for (i = 0.0f; i < 1.0f; i += 0.005f) {
-        const float nzx = zx * zx - zy * zy + cx;
-        const float nzy = zy * zx + zx * zy + cy;
+        // :22-25; zy*zx + zx*zy == 2*(zx*zy) exactly, so the fma of (zx + zx) is the
+        // contracted form of the shader's expression, not a different one
+        const float nzx = __builtin_fmaf(zx, zx, -(zy * zy)) + cx;
+        const float nzy = __builtin_fmaf(zx + zx, zy, cy);
         zx = nzx;
         zy = nzy;
-        if (__builtin_sqrtf(zx * zx + zy * zy) > 4.0f) break;
+        if (__builtin_sqrtf(__builtin_fmaf(zy, zy, zx * zx)) > 4.0f) break;   // length: §3.1 dot
     }
     // :32-33, vec4(vec3(i), 1.0) stored as UNORM8: u8 = #{k : clamp(i) >= U[k]}
     const float c = (i > 0.0f) ? ((i < 1.0f) ? i : 1.0f) : 0.0f;

@@ -141,3 +141,14 @@ def test_c5_full_size_segments(c5_scene, accel):
     g = _gpu(c5_scene, cfg, 1024, 1024)
     for rect in C5_RECTS:
         _assert_rect(g, _oracle(c5_scene, rvcp_amd.abi.make_config(spp=30), 1024, 1024, rect=rect), rect)
+
+
+# ---------------------------------------------------------------- UNORM8 rules -------------
+@pytest.mark.parametrize("integrator", [0, 1], ids=["games101", "mode2"])
+@pytest.mark.parametrize("rule", [0, 1], ids=["driver", "nearest"])
+def test_unorm_rules_bitexact(cornell, integrator, rule):
+    """rvcp_config_t.unorm_rule: the driver's 12-bit conversion (default) and round-to-nearest,
+    through the gamma store (games101) and the gamma-free store (mode 2), C1 size."""
+    sc = cornell if integrator == 0 else rvcp_amd.scene.sphere_scene()
+    cfg = rvcp_amd.abi.make_config(spp=2, integrator=integrator, unorm_rule=rule)
+    _assert_frame(_gpu(sc, cfg, 128, 128), _oracle(sc, cfg, 128, 128))

@@ -81,18 +81,31 @@ def test_rand_is_uniform():
     assert hist.min() > 800 and hist.max() < 1200          # expected 1000 per bin
 
 
-def test_gamma_table_and_u8():
-    T = [O.lib().rvcp_oracle_gamma_threshold(k) for k in range(256)]
+def _driver_u8(g):
+    """The reference driver's UNORM8 rule on the stored value g."""
+    return (math.floor(min(max(g, 0.0), 1.0) * 4096.0) * 255 + 2048) // 4096
+
+
+@pytest.mark.parametrize("rule", [0, 1], ids=["driver", "nearest"])
+def test_gamma_table_and_u8(rule):
+    T = [O.gamma_threshold(k, rule) for k in range(256)]
     assert T[0] == 0.0 and all(T[k] < T[k + 1] for k in range(255))
-    assert O.gamma_u8(0.0) == 0 and O.gamma_u8(1.0) == 255 and O.gamma_u8(7.0) == 255
-    assert O.gamma_u8(-1.0) == 0 and O.gamma_u8(float("nan")) == 0
-    assert O.gamma_u8(0.1) == 64          # the miss colour: round(255 * 0.1^0.6)
+    assert O.gamma_u8(0.0, rule) == 0 and O.gamma_u8(1.0, rule) == 255
+    assert O.gamma_u8(7.0, rule) == 255
+    assert O.gamma_u8(-1.0, rule) == 0 and O.gamma_u8(float("nan"), rule) == 0
+    assert O.gamma_u8(0.1, rule) == 64    # the miss colour: 255 * 0.1^0.6 = 64.05 (SURVEY.md §0.1)
     rng = np.random.default_rng(3)
     for c in rng.uniform(0, 1, 2000).astype(np.float32):
-        exact = 255.0 * float(c) ** 0.6
-        if abs(exact - math.floor(exact) - 0.5) < 1e-3:
-            continue                       # too close to a rounding tie to call
-        assert O.gamma_u8(float(c)) == int(math.floor(exact + 0.5)), c
+        g = float(c) ** 0.6
+        if rule == 1:
+            exact = 255.0 * g
+            if abs(exact - math.floor(exact) - 0.5) < 1e-3:
+                continue                   # too close to a rounding tie to call
+            assert O.gamma_u8(float(c), rule) == int(math.floor(exact + 0.5)), c
+        else:
+            if abs(g * 4096.0 - round(g * 4096.0)) < 1e-3:
+                continue                   # too close to a truncation step to call
+            assert O.gamma_u8(float(c), rule) == _driver_u8(g), c
 
 
 TRI = [0, 0, 0, 1, 0, 0, 0, 1, 0]
