@@ -82,6 +82,8 @@ for s in $STEPS; do
         abpk) run abpk 600 bash -c 'bash tools/ab.sh "" packed scalar && bash tools/ab.sh "--size 384 --spp 10" packed scalar && bash tools/ab.sh "--size 2048 --spp 64 --frames 6" packed scalar' ;;
         configs) run pytest_configs 900 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         valupmc) run valu_rate_wall 120 tools/build/valu_rate && run valupmc 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/valupmc_$TAG" -o run --output-format csv -- tools/build/valu_rate ;;
+        calib) run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calibf_$TAG" -o run --output-format csv -- tools/build/traffic_calib && run calib_write 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calibw_$TAG" -o run --output-format csv -- tools/build/traffic_calib ;;
+        mtests) run pytest_m 600 python -u -m pytest tests/test_mandelbrot.py tests/test_golden_frames.py tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     esac
 done
