@@ -608,6 +608,15 @@ __device__ __forceinline__ void queue_take(Queue &q, uint64_t need, uint32_t lan
     }
 }
 
+// Wave-level counters already summed over the lanes (kept in SGPRs by the caller).
+__device__ __forceinline__ void flush_wave_counters(unsigned long long *__restrict__ counters,
+                                                    uint32_t lane, uint32_t trav_wave,
+                                                    uint32_t iters) {
+    if (lane == 0) {
+        atomicAdd(&counters[0], (unsigned long long)trav_wave);
+        atomicAdd(&counters[2], (unsigned long long)iters);
+    }
+}
 __device__ __forceinline__ void flush_counters(unsigned long long *__restrict__ counters,
                                                uint32_t lane, uint32_t trav, uint32_t iters) {
     unsigned long long t64 = trav;
@@ -1070,6 +1079,8 @@ __device__ __forceinline__ void path_body(
     auto st_put3 = [&](int f, f3 v) { st[f * kBlock] = v.x; st[(f + 1) * kBlock] = v.y; st[(f + 2) * kBlock] = v.z; };
     auto st_get3 = [&](int f) { return mk(st[f * kBlock], st[(f + 1) * kBlock], st[(f + 2) * kBlock]); };
     const uint32_t lane = lane_id();
+    // this wave's index in the block, made wave-uniform (an SGPR) for the LDS row bases
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     unsigned long long t_exhausted = 0ull;
     // the queue runs over the pre-pass's compact list; its length is in counters[3]
@@ -1087,7 +1098,8 @@ __device__ __forceinline__ void path_body(
     bool need_pixel = true, done = false, ended = false, surf_ev = false;
     // the pixel's surface record (cached primary hit, pixel index) is re-read from the list at
     // each sample start instead of being held in 10 VGPRs for the whole pixel
-    uint32_t pslot = 0, k = 0, depth = 0, trav = 0, iters = 0;
+    uint32_t pslot = 0, k = 0, depth = 0;
+    uint32_t trav_wave = 0, iters = 0;      // wave-uniform: traversals of all lanes, iterations
     float seed = 0.0f, ridx = 0.0f;
     f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
     f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0), S_alb = mk(0, 0, 0);
@@ -1174,11 +1186,11 @@ __device__ __forceinline__ void path_body(
                 float sd = seed, ri = ridx;
                 f3 pp = mk(0, 0, 0);
                 asm volatile("" : "+v"(sd), "+v"(ri));
-                coop_unit_sphere(need_dir, sd, ri, pp, lane, tail_tab[threadIdx.x / kWave]);
+                coop_unit_sphere(need_dir, sd, ri, pp, lane, tail_tab[wv]);
                 asm volatile("" :: "v"(pp.x), "v"(pp.y), "v"(pp.z), "v"(ri));
             }
 #endif
-            coop_unit_sphere(need_dir, seed, ridx, p, lane, tail_tab[threadIdx.x / kWave]);
+            coop_unit_sphere(need_dir, seed, ridx, p, lane, tail_tab[wv]);
             if (need_dir) {                                         // :464-478
 #if RVCP_EXP_REPEAT_BRDF
                 {
@@ -1216,7 +1228,7 @@ __device__ __forceinline__ void path_body(
             break;
         }
         if (wave_active) iters += 1;
-        trav += (sA ? 1u : 0u) + (sB ? 1u : 0u);
+        trav_wave += (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
         if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
 
         int bestA = -1, bestB = -1;
@@ -1232,7 +1244,7 @@ __device__ __forceinline__ void path_body(
             if (tail) {
                 R = 2;
                 while (nr * R * 2 <= (uint32_t)kWave) R *= 2;
-                uint8_t *tab = tail_tab[threadIdx.x / kWave];
+                uint8_t *tab = tail_tab[wv];
                 if (sA) tab[rank_in(mA)] = (uint8_t)lane;
                 if (sB) tab[na + rank_in(mB)] = (uint8_t)lane;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1313,7 +1325,7 @@ __device__ __forceinline__ void path_body(
             // order give the identical nearest hit.
             uint32_t R = 2;
             while (nr * R * 2 <= (uint32_t)kWave) R *= 2;
-            uint8_t *tab = tail_tab[threadIdx.x / kWave];
+            uint8_t *tab = tail_tab[wv];
             if (hasA) tab[rank_in(mA)] = (uint8_t)lane;
             if (hasB) tab[na + rank_in(mB)] = (uint8_t)lane;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1357,7 +1369,7 @@ __device__ __forceinline__ void path_body(
             // this wave's LDS rows, lane j tests it against every triangle, and the nearest hits
             // go back the same way.  Each ray meets the same triangles in the same order, so
             // every nearest hit is unchanged.
-            float4 *rows = compact_lds + (threadIdx.x / kWave) * (2 * kWave);
+            float4 *rows = compact_lds + wv * (2 * kWave);
             if (hasA) {
                 const uint32_t j = rank_in(mA);
                 rows[2 * j] = make_float4(a_o.x, a_o.y, a_o.z, 0.0f);
@@ -1371,7 +1383,12 @@ __device__ __forceinline__ void path_body(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const float4 ro = rows[2 * lane], rd = rows[2 * lane + 1];
+            // the lane index re-derived here (opaque to the compiler) so that its row address
+            // is not held live across the whole loop -- at 6 waves/SIMD it was spilled
+            uint32_t lane_r;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0"
+                         : "=v"(lane_r));
+            const float4 ro = rows[2 * lane_r], rd = rows[2 * lane_r + 1];
             const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
             float bt = A.t_max;
             int best = -1;
@@ -1385,7 +1402,7 @@ __device__ __forceinline__ void path_body(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            rows[2 * lane] = make_float4(bt, __int_as_float(best), 0.0f, 0.0f);
+            rows[2 * lane_r] = make_float4(bt, __int_as_float(best), 0.0f, 0.0f);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1466,7 +1483,7 @@ __device__ __forceinline__ void path_body(
         hasA = false;
         if (!defer_B) hasB = false;
     }
-    flush_counters(counters, lane, trav, iters);
+    flush_wave_counters(counters, lane, trav_wave, iters);
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;
         unsigned long long *rec = A.timeline + 4ull * w;
