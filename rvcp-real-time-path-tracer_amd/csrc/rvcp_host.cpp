@@ -634,6 +634,12 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                 const int v = std::atoi(c);
                 if (v >= 1) A.chunk_window = (uint32_t)v;
             }
+            A.spread_min = 0;
+            A.early_tail = 0;
+            if (const char *c = std::getenv("RVCP_DEBUG_SPREAD")) A.spread_min = (uint32_t)std::atoi(c);
+            if (const char *c = std::getenv("RVCP_DEBUG_EARLY_TAIL")) A.early_tail = (uint32_t)std::atoi(c);
+            // schedules 3/6 spreading a small surface list run the full resident grid
+            if (A.spread_min && !legacy && !A.accel && (A.variant == 3 || A.variant == 6)) blocks = cap;
             ctx->last_timeline_waves = 0;
             if (std::getenv("RVCP_DEBUG_TIMELINE") && !legacy && A.variant >= 3) {
                 const size_t waves = (size_t)blocks * (kBlock / kWave);

@@ -163,6 +163,12 @@ struct FrameArgs {
     uint32_t chunk_window;   // grab = pixels this wave consumes in chunk_window ticks (10 ns)
     int32_t accel;           // RVCP_ACCEL_*
     int32_t bvh_root;        // root reference (see BvhNode) when accel == RVCP_ACCEL_BVH
+    // small frames (path kernels of schedules 3/6): when the surface list fits the resident
+    // lanes, spread it over every resident wave, at least spread_min pixels each (0 = off),
+    // and let waves with <= 32 rays split each ray's scan over R lanes from the first
+    // iteration (early_tail), not only once the queue is empty
+    uint32_t spread_min;
+    uint32_t early_tail;
     // debug (RVCP_DEBUG_TIMELINE): per-wave {start, queue exhausted, end, iterations}
     // of the path kernel, s_memrealtime ticks (100 MHz); nullptr otherwise
     unsigned long long *timeline;

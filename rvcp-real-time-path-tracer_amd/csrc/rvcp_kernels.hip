@@ -1088,7 +1088,15 @@ __device__ __forceinline__ void path_body(
     Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
     {   // static chunks over the surface list, same rule as the host's (static_split)
         uint32_t waves, c;
-        static_split(Q.n_pixels, gridDim.x * (kBlock / kWave), A.n_simds, waves, c);
+        const uint32_t grid_waves = gridDim.x * (kBlock / kWave);
+        static_split(Q.n_pixels, grid_waves, A.n_simds, waves, c);
+        if (A.spread_min && Q.n_pixels <= grid_waves * kChunk) {
+            // small frame: every resident wave gets a share (latency hiding over lane count)
+            c = (Q.n_pixels + grid_waves - 1) / grid_waves;
+            if (c < A.spread_min) c = A.spread_min;
+            if (c > kChunk) c = kChunk;
+            waves = (Q.n_pixels + c - 1) / c;
+        }
         Q.static_chunk = c;
         Q.static_chunks = c * waves;
     }
@@ -1235,7 +1243,7 @@ __device__ __forceinline__ void path_body(
         float btA = A.t_max, btB = A.t_max;
         const uint32_t na = (uint32_t)__builtin_popcountll(mA);
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
-        const bool tail = wave_active && q.exhausted && nr <= kWave / 2 && !BVH;
+        const bool tail = wave_active && (q.exhausted || A.early_tail) && nr <= kWave / 2 && !BVH;
         if (TILED) {
             // ---- LDS-tiled scan (optionally with the tail partition below) ----
             uint32_t R = 1, part = 0;

@@ -86,6 +86,8 @@ for s in $STEPS; do
         mtests) run pytest_m 600 python -u -m pytest tests/test_mandelbrot.py tests/test_golden_frames.py tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         benchall) run bench_c3 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline && run bench_c2 300 python bench.py --workload c2 --steps 100 --warmup 10 --no-cpu-baseline && run bench_c4 300 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         parity) run pytest_parity 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        spreadab) run spreadab 600 bash tools/spread_ab.sh ;;
+        spreadparity) run spreadparity 600 env RVCP_DEBUG_SPREAD=8 RVCP_DEBUG_EARLY_TAIL=1 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     esac
 done

@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# Small-frame scheduling A/B: RVCP_DEBUG_SPREAD (pixels per wave floor when
+# the surface list is spread over every resident wave) x RVCP_DEBUG_EARLY_TAIL, over frame sizes.
+# Prints the median kernel ms of 20 frames (last 15) per setting.
+set -e
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+for sz in "384 10" "256 10" "512 10" "768 10" "128 30" "1024 30"; do
+  set -- $sz
+  for cfg in "0 0" "0 1" "8 0" "8 1" "16 1" "24 1"; do
+    read sp et <<< "$cfg"
+    RVCP_DEBUG_SPREAD=$sp RVCP_DEBUG_EARLY_TAIL=$et timeout -k 10 120 python tools/frames.py --frames 20 --size $1 --spp $2 > /tmp/sab.log 2>/dev/null
+    python3 - "$1" "$2" "$sp" "$et" <<'PY'
+import json, sys
+ms = sorted(json.loads(l)["kernel_ms"] for l in open("/tmp/sab.log") if l.startswith("{"))
+ms = sorted(ms)[:15]
+print(f"size {sys.argv[1]:>4} spp {sys.argv[2]:>2} spread {sys.argv[3]:>2} early {sys.argv[4]}  median {ms[len(ms)//2]:.4f} min {ms[0]:.4f}")
+PY
+  done
+done

@@ -26,7 +26,9 @@ def main():
         print(json.dumps({"frame": k, "span_ms": round(span / 1e5, 3),
                           "start_pct": q(st), "exhausted_pct": q(ex), "end_pct": q(en),
                           "mean_residency": round(float(np.mean((en - st) / span)), 4),
-                          "iters_p50": float(np.median(it)), "iters_max": float(it.max())}))
+                          "iters_p50": float(np.median(it)), "iters_max": float(it.max()),
+                          "us_per_iter_p50": round(float(np.median((en - st)[it > 0] / it[it > 0])) / 100.0, 3),
+                          "waves_with_work": int((it > 0).sum())}))
 
 
 if __name__ == "__main__":
