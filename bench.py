@@ -240,7 +240,9 @@ def main():
     if args.accel == "bvh":
         cfg_kw["accel"] = 1
     rt = rvcp_amd.RayTracer(**cfg_kw)
-    rt.upload_scene(sc)
+    t_up = time.perf_counter()
+    rt.upload_scene(sc)                  # includes the scene-specialised compile (§4.7)
+    upload_s = time.perf_counter() - t_up
     push = sc.push_constant(123.0)
     n_faces = len(sc.mesh.aligned_faces())
     n_spheres = len(sc.spheres) if legacy else 0
@@ -370,7 +372,10 @@ def main():
                      "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)"),
             "config": {"workload": wl["workload"], "width": W, "height": H, "spp": spp,
                        "faces": n_faces, "parallelism": f"pixel-stripes x{world}",
-                       "accel": args.accel, "kernel_schedule": variant,
+                       "accel": args.accel, "kernel_schedule": variant & ~rvcp_amd.abi.VARIANT_SPECIALIZED,
+                       "scan": ("scene-specialised (hipRTC at upload, DESIGN.md §4.7)"
+                                if variant & rvcp_amd.abi.VARIANT_SPECIALIZED else "generic"),
+                       "upload_s": round(upload_s, 3),
                        "gather": ("gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
                                   "rccl ncclGather via rvcp_gather_frame_async") if world > 1 else "none"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 2),

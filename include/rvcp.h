@@ -23,8 +23,18 @@
 #ifndef RVCP_H
 #define RVCP_H
 
+#ifndef __HIPCC_RTC__               /* hipRTC (the scene-specialised kernels) has these built in */
 #include <stddef.h>
 #include <stdint.h>
+#else
+using __hip_internal::int32_t;
+using __hip_internal::uint8_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#ifndef offsetof
+#define offsetof(t, m) __builtin_offsetof(t, m)
+#endif
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -124,6 +134,11 @@ enum {
 };
 
 enum {
+    RVCP_SPECIALIZE_AUTO = 0,
+    RVCP_SPECIALIZE_OFF = 1,
+};
+
+enum {
     RVCP_UNORM_DRIVER = 0,            /* the reference driver's 12-bit fixed-point conversion */
     RVCP_UNORM_NEAREST = 1,           /* round-to-nearest */
 };
@@ -173,7 +188,14 @@ typedef struct rvcp_config {
      * 1,048,576 pixels reproduced): u8 = (floor(4096 x) * 255 + 2048) >> 12.
      * RVCP_UNORM_NEAREST (1): round-to-nearest, u8 = floor(255 x + 1/2). */
     int32_t unorm_rule;
-    uint32_t _reserved[2];
+    /* Scene-specialised scan: RVCP_SPECIALIZE_AUTO (0, default) compiles, at
+     * rvcp_upload_scene, path kernels whose triangle scan is written out for the uploaded
+     * scene (games101 integrator, brute force, at most 64 faces; hipRTC, ~2 s once per scene
+     * and process) and uses them for schedules 3 and 6 when ray_t_min > 0.  Frames are
+     * bit-identical to the generic kernels; without hipRTC the generic kernels run.
+     * RVCP_SPECIALIZE_OFF (1): always the generic kernels. */
+    int32_t specialize;
+    uint32_t _reserved[1];
 } rvcp_config_t;
 
 /* Per-render statistics (all optional). */
@@ -187,13 +209,17 @@ typedef struct rvcp_stats {
     uint32_t faces;                   /* F, triangles tested per traversal */
     int32_t kernel_variant;           /* the kernel schedule that ran (rvcp_config_t::
                                          kernel_variant resolved; 7 = BVH path kernel,
-                                         8 = RVCP_INTEGRATOR_LEGACY kernel, 0 = none) */
+                                         8 = RVCP_INTEGRATOR_LEGACY kernel, 0 = none), plus
+                                         RVCP_VARIANT_SPECIALIZED when the scene-specialised
+                                         path kernel ran */
     uint64_t wave_iterations;         /* wave-level trace iterations; lane utilisation of the
                                          scan = traversals_executed / (64 * wave_iterations) */
     double main_kernel_ms;            /* device time of the dominant (path-tracing) kernel
                                          alone, HIP events on the launch stream; kernel_ms
                                          also covers the primary pre-pass and counter reset */
 } rvcp_stats_t;
+
+#define RVCP_VARIANT_SPECIALIZED 16
 
 /* Layout checks: sizes/offsets the reference's Rust structs and std140/std430 blocks imply. */
 #ifdef __cplusplus

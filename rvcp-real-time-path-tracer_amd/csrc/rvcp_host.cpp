@@ -23,6 +23,7 @@
 
 #include "../../include/rvcp.h"
 #include "rvcp_internal.h"
+#include "rvcp_jit.h"
 #include "rvcp_scene_prep.h"
 
 using namespace rvcp;
@@ -55,6 +56,9 @@ struct rvcp_ctx {
     float *d_unorm = nullptr;
     unsigned long long *d_counters = nullptr;
     uint32_t n_faces = 0, n_lights = 0, n_mats = 0, n_verts = 0, n_spheres = 0;
+    // scene-specialised path kernels (rvcp_jit.cpp), or null: generic kernels
+    std::shared_ptr<JitKernels> jit;
+    std::string jit_err;
     float light_total = 0.0f, light_pdf = 0.0f;
     bool has_scene = false;
 
@@ -90,6 +94,7 @@ struct rvcp_ctx {
     // last launch
     bool pending = false;
     bool last_trivial = false;
+    bool last_spec = false;
     int32_t last_variant = 0;
     uint64_t last_pixels = 0;
     uint32_t last_spp = 0;
@@ -220,6 +225,7 @@ void free_scene(rvcp_ctx *ctx)
     (void)hipFree(ctx->d_spheres); ctx->d_spheres = nullptr;
     (void)hipFree(ctx->d_bvh_nodes); ctx->d_bvh_nodes = nullptr;
     (void)hipFree(ctx->d_bvh_tris); ctx->d_bvh_tris = nullptr;
+    ctx->jit.reset();
     ctx->has_scene = false;
 }
 
@@ -282,6 +288,8 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
     if (cfg->n_gpus < 0 || cfg->n_gpus > 64)
         return fail(nullptr, RVCP_E_INVALID, "n_gpus must be in [0, 64]");
+    if (cfg->specialize != RVCP_SPECIALIZE_AUTO && cfg->specialize != RVCP_SPECIALIZE_OFF)
+        return fail(nullptr, RVCP_E_INVALID, "unknown specialize");
     if (cfg->unorm_rule != RVCP_UNORM_DRIVER && cfg->unorm_rule != RVCP_UNORM_NEAREST)
         return fail(nullptr, RVCP_E_INVALID, "unknown unorm_rule");
     if (cfg->accel != RVCP_ACCEL_NONE && cfg->accel != RVCP_ACCEL_BVH)
@@ -517,6 +525,15 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         ctx->bvh_root = root4;
         ctx->bvh_depth = depth;
     }
+    // scene-specialised scan: compiled here, once per scene and process
+    ctx->jit.reset();
+    ctx->jit_err.clear();
+    if (ctx->cfg.specialize == RVCP_SPECIALIZE_AUTO &&
+        ctx->cfg.integrator == RVCP_INTEGRATOR_GAMES101 && ctx->cfg.accel == RVCP_ACCEL_NONE &&
+        n_faces >= 1 && n_faces <= kJitMaxFaces && !std::getenv("RVCP_NO_SPECIALIZE")) {
+        ctx->jit = jit_path_kernels(ctx->device, tri.data(), n_faces, ctx->jit_err);
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+    }
     ctx->n_faces = n_faces;
     ctx->n_verts = n_vertices;
     ctx->n_mats = n_materials;
@@ -603,6 +620,7 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     // first traversal (:413-419): the frame is black.  ray_tracer.comp has no attenuation
     // test before its first traversal (:629-634).
     const bool trivial = A.max_bounces == 0 || (!legacy && 1.0f < A.att_stop);
+    ctx->last_spec = false;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(unsigned long long), s));
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     if (A.n_pixels > 0) {
@@ -612,9 +630,16 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             rc = rvcp_launch_fill((uint32_t *)d_rgba8, (float *)d_linear_rgb, A.n_pixels,
                                   0xFF000000u, s);
         } else {
-            const uint32_t cap = (uint32_t)(legacy ? ctx->legacy_capacity
-                                           : A.accel ? ctx->bvh_capacity
-                                                     : ctx->grid_capacity[A.variant]);
+            // the scene-specialised path kernel (§4.7) replaces schedules 3 and 6 when the
+            // upload compiled one; its exactness argument needs t_min > 0
+            const JitKernels *jk = ctx->jit.get();
+            const int jit_per_cu = !jk ? 0 : A.variant == 6 ? jk->blocks_per_cu6
+                                 : A.variant == 3 ? jk->blocks_per_cu5 : 0;
+            const bool spec = !legacy && !A.accel && jit_per_cu > 0 && A.t_min > 0.0f;
+            uint32_t cap = (uint32_t)(legacy ? ctx->legacy_capacity
+                                     : A.accel ? ctx->bvh_capacity
+                                               : ctx->grid_capacity[A.variant]);
+            if (spec) cap = (uint32_t)jit_per_cu * (ctx->n_simds / 4u);
             A.n_simds = ctx->n_simds;
             uint32_t waves = 0, chunk = 0;
             rvcp_static_split(A.n_pixels, cap * (kBlock / kWave), A.n_simds, &waves, &chunk);
@@ -671,7 +696,10 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                                              (uint32_t *)d_rgba8, (float *)d_linear_rgb,
                                              ctx->d_counters, ctx->d_surf, ctx->d_shade,
                                              ctx->d_bvh_nodes, ctx->d_bvh_tris,
-                                             blocks, s, ctx->evm);
+                                             blocks, s, ctx->evm,
+                                             spec ? (void *)(A.variant == 6 ? jk->path6 : jk->path5)
+                                                  : nullptr);
+                if (spec) ctx->last_spec = true;
             } else {
                 HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_games101(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts, ctx->d_mats,
@@ -688,6 +716,7 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     ctx->pending = true;
     ctx->last_trivial = trivial;
     ctx->last_variant = (trivial || A.n_pixels == 0) ? 0 : legacy ? 8 : A.accel ? 7 : A.variant;
+    if (ctx->last_spec && ctx->last_variant != 0) ctx->last_variant |= RVCP_VARIANT_SPECIALIZED;
     ctx->last_pixels = A.n_pixels;
     ctx->last_spp = A.spp;
     return RVCP_OK;

@@ -2,9 +2,16 @@
 // the gfx950 kernels (rvcp_kernels.hip).  Not part of the C-ABI.
 #pragma once
 
+#ifndef __HIPCC_RTC__             // hipRTC (rvcp_jit.cpp) provides the fixed-width types
 #include <stdint.h>
 
 #include <vector>
+#else
+using __hip_internal::int32_t;
+using __hip_internal::uint8_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#endif
 
 namespace rvcp {
 
@@ -174,6 +181,7 @@ struct FrameArgs {
     unsigned long long *timeline;
 };
 
+#ifndef __HIPCC_RTC__
 // rvcp_bvh.cpp: build the BVH over n faces (three vertex positions each); returns the depth.
 int bvh_build(const float (*pos)[3][3], uint32_t n, std::vector<BvhNode> &nodes,
               std::vector<uint32_t> &order, int32_t &root);
@@ -182,8 +190,10 @@ int bvh_build(const float (*pos)[3][3], uint32_t n, std::vector<BvhNode> &nodes,
 int bvh4_collapse(const std::vector<BvhNode> &nodes, int32_t root, std::vector<Bvh4Node> &out,
                   int32_t &root4);
 
+#endif  // __HIPCC_RTC__
 }  // namespace rvcp
 
+#ifndef __HIPCC_RTC__
 // Launchers (defined in rvcp_kernels.hip), called by rvcp_host.cpp.
 extern "C" {
 int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
@@ -197,7 +207,8 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *
                             uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
                             rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
                             const rvcp::Bvh4Node *bvh_nodes, const rvcp::TriRecord *bvh_tris,
-                            uint32_t grid_blocks, void *stream, void *main_event);
+                            uint32_t grid_blocks, void *stream, void *main_event,
+                            void *spec_path_fn);
 // Integrator RVCP_INTEGRATOR_LEGACY (ray_tracer.comp): materials / spheres are the raw
 // rvcp_material_t / rvcp_sphere_t arrays, unorm_t the UNORM8 threshold table.
 int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
@@ -217,3 +228,4 @@ int rvcp_games101_occupancy(int variant, int *blocks_per_cu);
 void rvcp_static_split(uint32_t n, uint32_t grid_waves, uint32_t n_simds, uint32_t *waves,
                        uint32_t *chunk);
 }
+#endif  // __HIPCC_RTC__

@@ -1,0 +1,384 @@
+// rvcp_jit.cpp -- scene-specialised path kernels.
+//
+// The brute-force nearest-hit scan of the path kernels (schedules 3 and 6) tests every ray
+// against every triangle with the exact operation sequence of the numeric contract (DESIGN.md
+// §3.1, §3.5): ~42 VALU instructions per test, read from a triangle record in SGPRs.  For a
+// small scene (the reference's Cornell box: 32 triangles) this module generates, at upload,
+// source code in which every triangle's test is written out with its v0 / e1 / e2 as literals
+// and every product with an exact-zero triangle component dropped (axis-aligned walls and box
+// faces have a third of their edge components zero), compiles rvcp_kernels.hip around it with
+// hipRTC for gfx950, and hands the host the two kernels.
+//
+// Why the result is bit-identical to the generic scan (for finite rays and t_min > 0; the
+// kernel falls back to the generic loop for a wave holding a non-finite ray, and the host uses
+// the generic kernels when ray_t_min <= 0):
+//  * a dropped term is a product c * x with c = +0 or -0 and x finite, i.e. a zero; removing a
+//    zero addend from a correctly rounded sum or fma changes at most the sign of a zero result;
+//  * so every intermediate equals the generic one up to the sign of zero, and the values that
+//    reach a decision are: f = 1/den (den = +-0 gives f = +-inf, and then t = +-inf or NaN is
+//    rejected by t >= t_min > 0 or t <= bt either way), b1, b2 (compared with >= 0 and
+//    b1 + b2 <= 1, blind to the sign of zero), t (an accepted t >= t_min > 0 is non-zero, so
+//    its bits are the generic ones);
+//  * a triangle whose denominator is identically zero is never accepted and is omitted; a
+//    vanished b1 or b2 drops its ">= 0" test, which a finite f would pass and an infinite f
+//    rejects through t anyway;
+//  * triangles are tested in index order with the shader's "t <= bt" rule, as the loop does.
+//
+// hipRTC is loaded at run time (dlopen), like RCCL: without it, or if compilation fails, the
+// context keeps the generic kernels (frames are the same either way).
+#include <hip/hip_runtime.h>
+
+#include <dlfcn.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <list>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rvcp_internal.h"
+#include "rvcp_jit.h"
+#include "build/rvcp_jit_src.h"   // kJitSrcKernels, kJitSrcInternal, kJitSrcAbi (Makefile)
+
+namespace rvcp {
+namespace {
+
+// ------------------------------------------------------------------ hipRTC, dlopen()ed --
+typedef int rtc_result;
+typedef void *rtc_program;
+struct RtcApi {
+    bool ok = false;
+    std::string why;
+    rtc_result (*create)(rtc_program *, const char *, const char *, int, const char *const *,
+                         const char *const *) = nullptr;
+    rtc_result (*compile)(rtc_program, int, const char *const *) = nullptr;
+    rtc_result (*log_size)(rtc_program, size_t *) = nullptr;
+    rtc_result (*log)(rtc_program, char *) = nullptr;
+    rtc_result (*code_size)(rtc_program, size_t *) = nullptr;
+    rtc_result (*code)(rtc_program, char *) = nullptr;
+    rtc_result (*destroy)(rtc_program *) = nullptr;
+};
+
+const RtcApi &rtc()
+{
+    static RtcApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = nullptr;
+        for (const char *name : {"libhiprtc.so", "libhiprtc.so.7", "/opt/rocm/lib/libhiprtc.so"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+        if (!h) {
+            api.why = "libhiprtc not found";
+            return;
+        }
+        api.create = (decltype(api.create))dlsym(h, "hiprtcCreateProgram");
+        api.compile = (decltype(api.compile))dlsym(h, "hiprtcCompileProgram");
+        api.log_size = (decltype(api.log_size))dlsym(h, "hiprtcGetProgramLogSize");
+        api.log = (decltype(api.log))dlsym(h, "hiprtcGetProgramLog");
+        api.code_size = (decltype(api.code_size))dlsym(h, "hiprtcGetCodeSize");
+        api.code = (decltype(api.code))dlsym(h, "hiprtcGetCode");
+        api.destroy = (decltype(api.destroy))dlsym(h, "hiprtcDestroyProgram");
+        api.ok = api.create && api.compile && api.log_size && api.log && api.code_size &&
+                 api.code && api.destroy;
+        if (!api.ok) api.why = "libhiprtc lacks a required symbol";
+    });
+    return api;
+}
+
+// ------------------------------------------------------------------ source generator ----
+// A value of the generated expression graph: an exact zero, a named float, or a non-zero
+// literal (the triangle's own float, written as its bit pattern).
+struct Val {
+    enum Kind { kZero, kVar, kLit } kind = kZero;
+    std::string name;
+    float lit = 0.0f;
+};
+
+Val zero() { return Val{}; }
+Val var(const std::string &n) { Val v; v.kind = Val::kVar; v.name = n; return v; }
+Val lit_or_zero(float x)
+{
+    if (x == 0.0f) return zero();          // +0 and -0: dropped terms (see the header)
+    Val v;
+    v.kind = Val::kLit;
+    v.lit = x;
+    return v;
+}
+
+std::string lit_text(float x)
+{
+    uint32_t bits;
+    std::memcpy(&bits, &x, 4);
+    char buf[48];
+    std::snprintf(buf, sizeof buf, "RVCP_F32(0x%08xu)", bits);
+    return buf;
+}
+
+struct Gen {
+    std::string out;
+    int n = 0;
+
+    std::string text(const Val &v) const { return v.kind == Val::kLit ? lit_text(v.lit) : v.name; }
+    Val tmp(const std::string &expr)
+    {
+        const std::string name = "r" + std::to_string(n++);
+        out += "        const float " + name + " = " + expr + ";\n";
+        return var(name);
+    }
+    Val mul(const Val &a, const Val &b)
+    {
+        if (a.kind == Val::kZero || b.kind == Val::kZero) return zero();
+        return tmp(text(a) + " * " + text(b));
+    }
+    Val neg(const Val &a)
+    {
+        if (a.kind == Val::kZero) return a;
+        if (a.kind == Val::kLit) return lit_or_zero(-a.lit);
+        return tmp("-" + a.name);
+    }
+    Val fma(const Val &a, const Val &b, const Val &c)
+    {
+        if (a.kind == Val::kZero || b.kind == Val::kZero) return c;
+        if (c.kind == Val::kZero) return mul(a, b);
+        return tmp("__builtin_fmaf(" + text(a) + ", " + text(b) + ", " + text(c) + ")");
+    }
+    Val sub(const Val &a, const Val &b)       // a - b; x - (+-0) == x exactly, so b = 0 drops
+    {
+        if (b.kind == Val::kZero) return a;
+        return tmp(text(a) + " - " + text(b));
+    }
+    // dot = fma(z, z', fma(y, y', x*x')), cross_i = fma(a_j, b_k, -(a_k*b_j)): DESIGN.md §3.1
+    Val dot(const Val *a, const Val *b) { return fma(a[2], b[2], fma(a[1], b[1], mul(a[0], b[0]))); }
+    void cross(const Val *a, const Val *b, Val *r)
+    {
+        r[0] = fma(a[1], b[2], neg(mul(a[2], b[1])));
+        r[1] = fma(a[2], b[0], neg(mul(a[0], b[2])));
+        r[2] = fma(a[0], b[1], neg(mul(a[1], b[0])));
+    }
+};
+
+// One triangle's test for ray `r` ("" / "A" / "B"); false when it can never accept.
+bool emit_triangle(std::string &out, const TriRecord &T, uint32_t index, const char *r)
+{
+    Gen g;
+    const std::string R(r);
+    Val o[3] = {var("o" + R + ".x"), var("o" + R + ".y"), var("o" + R + ".z")};
+    Val d[3] = {var("d" + R + ".x"), var("d" + R + ".y"), var("d" + R + ".z")};
+    Val v0[3], e1[3], e2[3];
+    for (int k = 0; k < 3; k++) {
+        v0[k] = lit_or_zero(T.v0[k]);
+        e1[k] = lit_or_zero(T.e1[k]);
+        e2[k] = lit_or_zero(T.e2[k]);
+    }
+    Val s[3] = {g.sub(o[0], v0[0]), g.sub(o[1], v0[1]), g.sub(o[2], v0[2])};   // :249
+    Val s1[3], s2[3];
+    g.cross(d, e2, s1);                                                        // :250
+    const Val den = g.dot(s1, e1);                                             // :254
+    if (den.kind == Val::kZero) return false;
+    g.cross(s, e1, s2);                                                        // :251
+    const Val n1 = g.dot(s1, s);
+    const Val n2 = g.dot(s2, d);
+    const Val tt = g.dot(s2, e2);
+    const Val f = g.tmp("rcp_ieee(" + g.text(den) + ")");
+    // t = f * dot(s2, e2) (:255); a vanished dot leaves t = +-0 or NaN, rejected by
+    // t >= t_min > 0 in both forms
+    const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.tmp(f.name + " * " + g.text(tt)).name;
+    std::string cond;
+    auto add = [&](const std::string &c) { cond += (cond.empty() ? "" : " & ") + c; };
+    std::string b1, b2;
+    if (n1.kind != Val::kZero) b1 = g.tmp(f.name + " * " + g.text(n1)).name;   // :256
+    if (n2.kind != Val::kZero) b2 = g.tmp(f.name + " * " + g.text(n2)).name;   // :257
+    if (!b1.empty()) add("(" + b1 + " >= 0.0f)");
+    if (!b2.empty()) add("(" + b2 + " >= 0.0f)");
+    if (!b1.empty() && !b2.empty()) add("(" + b1 + " + " + b2 + " <= 1.0f)");
+    else if (!b1.empty()) add("(" + b1 + " <= 1.0f)");
+    else if (!b2.empty()) add("(" + b2 + " <= 1.0f)");
+    add("(" + t + " >= tmin)");
+    add("(" + t + " <= bt" + R + ")");
+    out += "    {\n" + g.out;
+    out += "        if (" + cond + ") { bt" + R + " = " + t + "; best" + R + " = " +
+           std::to_string(index) + "; }\n    }\n";
+    // commit the triangle's result before the next one: keeps the unrolled scan one test
+    // deep in registers (without it the compiler interleaves all tests and spills)
+    out += "    RVCP_SPEC_COMMIT(bt" + R + ", best" + R + ");\n";
+    return true;
+}
+
+}  // namespace
+
+std::string jit_scan_source(const TriRecord *tri, uint32_t n)
+{
+    // RVCP_F32(bits): the triangle's float by its bit pattern; RVCP_SPEC_COMMIT(t, i): the
+    // test's result is final here (on the GPU an empty asm on the two registers plus a
+    // scheduling barrier, so the unrolled scan stays one test deep in registers; the CPU
+    // check in tests/test_jit_cpu.py compiles the same text with plain C definitions)
+    std::string out = "// generated by rvcp_jit.cpp: the scan of DESIGN.md §4.7 over " +
+                      std::to_string(n) + " triangles\n";
+    out += "__device__ __forceinline__ void spec_scan1(f3 o, f3 d, float tmin, float &bt, "
+           "int &best) {\n";
+    for (uint32_t i = 0; i < n; i++) emit_triangle(out, tri[i], i, "");
+    out += "}\n";
+    out += "__device__ __forceinline__ void spec_scan2(f3 oA, f3 dA, f3 oB, f3 dB, float tmin, "
+           "float &btA, int &bestA, float &btB, int &bestB) {\n";
+    for (uint32_t i = 0; i < n; i++) {
+        emit_triangle(out, tri[i], i, "A");
+        emit_triangle(out, tri[i], i, "B");
+    }
+    out += "}\n";
+    return out;
+}
+
+// ------------------------------------------------------------------ compile + cache -----
+namespace {
+
+uint64_t fnv1a(const std::string &s)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : s) {
+        h ^= c;
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+struct CacheEntry {
+    int device;
+    uint64_t hash;
+    std::string scan;
+    std::shared_ptr<JitKernels> kernels;
+};
+std::mutex g_mu;
+std::list<CacheEntry> g_cache;            // most recently used first
+constexpr size_t kCacheEntries = 16;
+
+}  // namespace
+
+JitKernels::~JitKernels()
+{
+    if (module) {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        (void)hipModuleUnload(module);
+        if (cur >= 0) (void)hipSetDevice(cur);
+    }
+}
+
+int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err)
+{
+    const RtcApi &api = rtc();
+    if (!api.ok) {
+        err = api.why;
+        return -1;
+    }
+    const char *hdr_src[] = {kJitSrcInternal, kJitSrcAbi, scan.c_str()};
+    const char *hdr_name[] = {"rvcp_internal.h", "../../include/rvcp.h", "rvcp_spec_scan.inc"};
+    rtc_program prog = nullptr;
+    if (api.create(&prog, kJitSrcKernels, "rvcp_kernels.hip", 3, hdr_src, hdr_name) != 0) {
+        err = "hiprtcCreateProgram failed";
+        return -1;
+    }
+    // the flags of the static build (Makefile): the numeric contract depends on them
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                          "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-fast-math",
+                          "-fno-slp-vectorize", "-DRVCP_JIT", "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
+    const int rc = api.compile(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+    if (rc != 0) {
+        size_t ls = 0;
+        api.log_size(prog, &ls);
+        std::string log(ls, '\0');
+        if (ls) api.log(prog, &log[0]);
+        err = "hipRTC compile failed: " + log.substr(0, 4000);
+        api.destroy(&prog);
+        return -1;
+    }
+    size_t cs = 0;
+    api.code_size(prog, &cs);
+    code.assign(cs, 0);
+    if (cs) api.code(prog, code.data());
+    api.destroy(&prog);
+    return cs ? 0 : -1;
+}
+
+std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
+                                             std::string &err)
+{
+    const std::string scan = jit_scan_source(tri, n);
+    const uint64_t h = fnv1a(scan);
+    std::lock_guard<std::mutex> lock(g_mu);
+    for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
+        if (it->device == device && it->hash == h && it->scan == scan) {
+            g_cache.splice(g_cache.begin(), g_cache, it);
+            return g_cache.front().kernels;
+        }
+    }
+    std::vector<char> code;
+    if (jit_compile_code(scan, code, err) != 0) return nullptr;
+    auto k = std::make_shared<JitKernels>();
+    k->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&k->module, code.data()) != hipSuccess) {
+        k->module = nullptr;
+        err = "hipModuleLoadData failed";
+        return nullptr;
+    }
+    if (hipModuleGetFunction(&k->path5, k->module, "rvcp_spec_path_kernel5") != hipSuccess ||
+        hipModuleGetFunction(&k->path6, k->module, "rvcp_spec_path_kernel6") != hipSuccess) {
+        err = "specialised kernels missing from the module";
+        return nullptr;
+    }
+    int bpc = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->path5, kBlock, 0) == hipSuccess)
+        k->blocks_per_cu5 = bpc;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->path6, kBlock, 0) == hipSuccess)
+        k->blocks_per_cu6 = bpc;
+    g_cache.push_front(CacheEntry{device, h, scan, k});
+    if (g_cache.size() > kCacheEntries) g_cache.pop_back();
+    return k;
+}
+
+}  // namespace rvcp
+
+// Self-test hook for the CPU test suite (not part of rvcp.h): generate and compile the
+// specialised module for n triangle records without a GPU.  Returns 0 and the code-object size,
+// or -1 with the message in err (err_cap bytes).
+extern "C" int rvcp_internal_jit_compile_check(const void *tri_records, uint32_t n,
+                                                size_t *code_bytes, char *err, size_t err_cap)
+{
+    try {
+        std::string e;
+        std::vector<char> code;
+        const std::string scan =
+            rvcp::jit_scan_source(static_cast<const rvcp::TriRecord *>(tri_records), n);
+        const int rc = rvcp::jit_compile_code(scan, code, e);
+        if (code_bytes) *code_bytes = code.size();
+        if (err && err_cap) {
+            std::strncpy(err, e.c_str(), err_cap - 1);
+            err[err_cap - 1] = '\0';
+        }
+        return rc;
+    } catch (...) {
+        return -1;
+    }
+}
+
+// The generated scan source for n triangle records (for inspection): writes at most cap bytes
+// including the terminator and returns the full length.
+extern "C" size_t rvcp_internal_jit_scan_source(const void *tri_records, uint32_t n, char *out,
+                                                size_t cap)
+{
+    try {
+        const std::string s =
+            rvcp::jit_scan_source(static_cast<const rvcp::TriRecord *>(tri_records), n);
+        if (out && cap) {
+            std::strncpy(out, s.c_str(), cap - 1);
+            out[cap - 1] = '\0';
+        }
+        return s.size();
+    } catch (...) {
+        return 0;
+    }
+}

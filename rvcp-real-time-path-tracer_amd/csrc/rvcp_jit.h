@@ -1,0 +1,36 @@
+// rvcp_jit.h -- scene-specialised path kernels compiled at upload with hipRTC (rvcp_jit.cpp,
+// DESIGN.md §4.7).  Host-side only; not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "rvcp_internal.h"
+
+namespace rvcp {
+
+// Scenes up to this many faces get the specialised scan (the unrolled code grows with F).
+constexpr uint32_t kJitMaxFaces = 64;
+
+struct JitKernels {
+    int device = 0;
+    hipModule_t module = nullptr;
+    hipFunction_t path5 = nullptr;     // schedule 3 (5 waves per SIMD)
+    hipFunction_t path6 = nullptr;     // schedule 6 (6 waves per SIMD)
+    int blocks_per_cu5 = 0, blocks_per_cu6 = 0;
+    ~JitKernels();
+};
+
+// The generated scan (spec_scan1 / spec_scan2) for n triangle records.
+std::string jit_scan_source(const TriRecord *tri, uint32_t n);
+// Compile rvcp_kernels.hip with the given scan for gfx950 (hipRTC); 0 or -1 with err set.
+int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err);
+// Compiled + loaded kernels for the scene on `device` (process-wide cache keyed by the scan
+// source); nullptr with err set when hipRTC is unavailable or compilation fails.
+std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
+                                             std::string &err);
+
+}  // namespace rvcp

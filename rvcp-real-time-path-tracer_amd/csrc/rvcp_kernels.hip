@@ -24,7 +24,9 @@
 // builtins dot/cross are explicit fma chains), IEEE correctly rounded division and sqrt,
 // the software sin of the contract, so every pixel is
 // bit-identical to oracle/rvcp_oracle.c whichever variant runs.
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 
 #include "rvcp_internal.h"
 #include "../../include/rvcp.h"
@@ -188,6 +190,21 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
                                            float &t_out) {
     return tri_stage2(T, tri_stage1(T, o, d), tmin, bt, t_out);
 }
+#ifdef RVCP_SPEC_SCAN        // the scene-specialised scan generated by rvcp_jit.cpp (§4.7)
+#define RVCP_F32(bits) __uint_as_float(bits)
+// a test's (t, index) is committed before the next test starts: without this the compiler
+// interleaves all unrolled tests and spills hundreds of registers
+#define RVCP_SPEC_COMMIT(t, i) do { asm volatile("" : "+v"(t), "+v"(i)); \
+                                    __builtin_amdgcn_sched_barrier(0); } while (0)
+#include RVCP_SPEC_SCAN
+// The specialised scan drops products with exact-zero triangle components, which is exact
+// only for finite rays; a wave holding any non-finite ray uses the generic loop instead.
+// (One sum: it is non-finite if any component is, and an overflowing sum of finite values
+// only sends a wave to the generic loop.)
+__device__ __forceinline__ bool ray_finite(f3 o, f3 d) {
+    return __builtin_isfinite(((o.x + o.y) + (o.z + d.x)) + (d.y + d.z));
+}
+#endif
 // A necessary condition for tri_stage2 to accept, from stage 1 alone: |n1| and |n2| at most
 // RN(|den| (1 + 2^-20)) (proof: DESIGN.md §4.2).  A wave skips stage 2 of a triangle when no
 // lane passes it; no result changes.
@@ -634,6 +651,7 @@ enum : int { K_NONE = -1, K_PRIMARY = 0, K_PATH = 1, K_SHADOW = 2 };
 
 }  // namespace
 
+#ifndef RVCP_JIT   // the scene-specialised module (rvcp_jit.cpp) holds only the path kernels
 // ======================================================================================
 // Variant 1: one ray per lane per iteration
 // ======================================================================================
@@ -1032,6 +1050,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     }
 }
 
+#endif  // RVCP_JIT
 // ======================================================================================
 // Variant 3/4, kernel 2: the dual-ray machine over the surface pixels of the pre-pass.  Every
 // pixel starts with a surface event at its cached primary hit, so no iteration is spent on
@@ -1400,11 +1419,18 @@ __device__ __forceinline__ void path_body(
             const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
             float bt = A.t_max;
             int best = -1;
+#ifdef RVCP_SPEC_SCAN
+            if (!__any(lane_r < nr && !ray_finite(o, d))) {
+                spec_scan1(o, d, A.t_min, bt, best);
+            } else
+#endif
+            {
 #pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
                 float t;
                 if (tri_accept(T, o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
+            }
             }
             // lanes >= nr traced stale rows; their results are never read
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1431,6 +1457,12 @@ __device__ __forceinline__ void path_body(
 #ifndef RVCP_EXP_SCAN_REPEAT
 #define RVCP_EXP_SCAN_REPEAT 1
 #endif
+#ifdef RVCP_SPEC_SCAN
+            if (!__any((hasA && !ray_finite(a_o, a_d)) || (hasB && !ray_finite(b_o, b_d)))) {
+                spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
+            } else
+#endif
+            {
             for (int rep = 0; rep < RVCP_EXP_SCAN_REPEAT; ++rep) {
 #pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {
@@ -1438,6 +1470,7 @@ __device__ __forceinline__ void path_body(
                 float tA, tB;
                 if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
                 if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
+            }
             }
             }
         }
@@ -1502,6 +1535,7 @@ __device__ __forceinline__ void path_body(
     }
 }
 
+#ifndef RVCP_JIT
 template <int MIN_WAVES>
 __global__ __launch_bounds__(kBlock, MIN_WAVES) void games101_path_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
@@ -1850,7 +1884,43 @@ __global__ __launch_bounds__(kBlock) void legacy_kernel(
     flush_counters(counters, lane, trav, iters);
 }
 
+#endif  // RVCP_JIT
+#ifdef RVCP_JIT
+// Scene-specialised path kernels (rvcp_jit.cpp compiles this file with hipRTC, RVCP_JIT and
+// RVCP_SPEC_SCAN set): schedules 3 and 6 with the scan unrolled over the uploaded scene
+// (DESIGN.md §4.7).  extern "C" so that the host finds them by name in the module.
+extern "C" __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void rvcp_spec_path_kernel5(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];
+    __shared__ float state_lds[10 * kBlock];
+    path_body<false, false, false, true>(
+        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
+        nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+}
+extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];
+    __shared__ float state_lds[10 * kBlock];
+    path_body<false, false, false, true>(
+        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
+        nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+}
+#endif  // RVCP_JIT
 }  // namespace rvcp
+
+#ifndef RVCP_JIT
 
 extern "C" int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
                                     const void *faces, const void *verts,
@@ -1875,7 +1945,8 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                                        const rvcp::FaceShade *shade,
                                        const rvcp::Bvh4Node *bvh_nodes,
                                        const rvcp::TriRecord *bvh_tris,
-                                       uint32_t grid_blocks, void *stream, void *main_event)
+                                       uint32_t grid_blocks, void *stream, void *main_event,
+                                       void *spec_path_fn)
 {
     const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
     auto pre = args->accel ? rvcp::games101_primary_kernel<true> : rvcp::games101_primary_kernel<false>;
@@ -1885,7 +1956,15 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                        surf, shade, bvh_nodes, bvh_tris);
     if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
         return -2;
-    if (args->accel)
+    if (spec_path_fn) {
+        // the scene-specialised schedule 3 / 6 kernel of rvcp_jit.cpp (same signature)
+        rvcp::FrameArgs a = *args;
+        void *params[] = {&a, &tri, &mats, &lights, &gamma_t, &out_rgba, &out_lin, &counters,
+                          &surf, &shade};
+        if (hipModuleLaunchKernel((hipFunction_t)spec_path_fn, grid_blocks, 1, 1, rvcp::kBlock,
+                                  1, 1, 0, (hipStream_t)stream, params, nullptr) != hipSuccess)
+            return -2;
+    } else if (args->accel)
         hipLaunchKernelGGL(rvcp::games101_bvh_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade, bvh_nodes, bvh_tris);
@@ -1973,3 +2052,4 @@ extern "C" int rvcp_legacy_occupancy(int *blocks_per_cu)
     *blocks_per_cu = b;
     return 0;
 }
+#endif  // RVCP_JIT

@@ -99,7 +99,14 @@ def test_gather_without_communicator(cornell):
 def test_stats_report_schedule(cornell):
     """rvcp_stats_t.kernel_variant names the schedule that ran (bench.py picks the rocprof
     kernel name from it)."""
-    with rvcp_amd.RayTracer(spp=30) as rt:
+    spec = rvcp_amd.abi.VARIANT_SPECIALIZED
+    with rvcp_amd.RayTracer(spp=30) as rt:          # Cornell: the scene-specialised kernels
+        rt.upload_scene(cornell)
+        rt.render(1024, 1024, TIME)
+        assert int(rt.last_stats["kernel_variant"]) == 6 | spec
+        rt.render(64, 64, TIME)
+        assert int(rt.last_stats["kernel_variant"]) == 3 | spec
+    with rvcp_amd.RayTracer(spp=30, specialize=rvcp_amd.abi.SPECIALIZE_OFF) as rt:
         rt.upload_scene(cornell)
         rt.render(1024, 1024, TIME)
         assert int(rt.last_stats["kernel_variant"]) == 6

@@ -1,0 +1,91 @@
+"""The scene-specialised path kernels (rvcp_jit.cpp) on the GPU.
+
+Every frame here is compared bit for bit (linear RGB bitwise, RGBA8 bytes, traversal count)
+with the CPU oracle and/or with the generic kernels (rvcp_config_t.specialize = OFF); the
+stats report which kernel ran (kernel_variant | RVCP_VARIANT_SPECIALIZED)."""
+import time
+
+import numpy as np
+import pytest
+
+import oracle as O
+import rvcp_amd
+from conftest import scene_arrays
+
+pytestmark = pytest.mark.gpu
+TIME = 123.0
+SPEC = rvcp_amd.abi.VARIANT_SPECIALIZED
+
+
+def _render(sc, W, H, time_=TIME, **kw):
+    with rvcp_amd.RayTracer(**kw) as rt:
+        rt.upload_scene(sc)
+        rgba, lin = rt.render(W, H, time_, want_linear=True)
+        return rgba, lin, rt.last_stats.copy()
+
+
+def _same(a, b):
+    assert np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32))
+    assert np.array_equal(a[0], b[0])
+    assert int(a[2]["traversals"]) == int(b[2]["traversals"])
+
+
+@pytest.mark.parametrize("W,H,spp", [(1024, 1024, 30), (384, 384, 10), (129, 67, 7)])
+def test_specialised_equals_generic(cornell, W, H, spp):
+    s = _render(cornell, W, H, spp=spp)
+    g = _render(cornell, W, H, spp=spp, specialize=rvcp_amd.abi.SPECIALIZE_OFF)
+    assert int(s[2]["kernel_variant"]) & SPEC and not int(g[2]["kernel_variant"]) & SPEC
+    _same(s, g)
+
+
+@pytest.mark.parametrize("case", ["quirk_off", "params", "moved_camera", "extra_tris", "seed"])
+def test_specialised_vs_oracle(cornell, case):
+    sc, kw, t = cornell, dict(spp=3), TIME
+    if case == "quirk_off":
+        kw["lum_id_std140_quirk"] = 0
+    elif case == "params":
+        kw.update(max_bounces=4, rr_probability=0.6, eps=0.01, ray_t_min=0.5, ray_t_max=900.0)
+    elif case == "moved_camera":
+        sc = rvcp_amd.Scene(rvcp_amd.Camera.new([120.0, 400.0, -700.0], [-50.0, 150.0, 100.0],
+                                                0.1, 10000.0, 55.0, 150.0, 5.0),
+                            cornell.materials, [], cornell.mesh)
+    elif case == "extra_tris":        # 52 faces, 20 of them with no zero component
+        sc = rvcp_amd.scene.with_random_triangles(cornell, 20)
+    else:
+        t = 987.0
+    W, H = 96, 80
+    s = _render(sc, W, H, t, **kw)
+    assert int(s[2]["kernel_variant"]) & SPEC
+    cfg = rvcp_amd.abi.make_config(**kw)
+    o_lin, o_rgba, o_trav = O.render(scene_arrays(sc), sc.push_constant(t), cfg, W, H)
+    assert np.array_equal(s[1].view(np.uint32), o_lin.view(np.uint32))
+    assert np.array_equal(s[0], o_rgba) and int(s[2]["traversals"]) == o_trav
+
+
+def test_nonpositive_t_min_uses_generic(cornell):
+    """The exactness argument needs t_min > 0: with ray_t_min = 0 the generic kernel runs."""
+    s = _render(cornell, 64, 64, spp=2, ray_t_min=0.0)
+    assert not int(s[2]["kernel_variant"]) & SPEC
+    cfg = rvcp_amd.abi.make_config(spp=2, ray_t_min=0.0)
+    o_lin, o_rgba, _ = O.render(scene_arrays(cornell), cornell.push_constant(TIME), cfg, 64, 64)
+    assert np.array_equal(s[1].view(np.uint32), o_lin.view(np.uint32))
+
+
+def test_large_scene_not_specialised(cornell):
+    sc = rvcp_amd.scene.with_random_triangles(cornell, 100)
+    s = _render(sc, 32, 32, spp=1)
+    assert not int(s[2]["kernel_variant"]) & SPEC
+
+
+def test_compiled_once_per_scene(cornell):
+    """The module cache: a second context uploading the same scene does not recompile."""
+    sc = rvcp_amd.scene.with_random_triangles(cornell, 7)     # a scene no other test uses
+    times = []
+    for _ in range(2):
+        with rvcp_amd.RayTracer(spp=1) as rt:
+            t0 = time.perf_counter()
+            rt.upload_scene(sc)
+            times.append(time.perf_counter() - t0)
+            rt.render(16, 16, TIME)
+            assert int(rt.last_stats["kernel_variant"]) & SPEC
+    assert times[1] < 0.5 * times[0] or times[0] < 0.05, times
