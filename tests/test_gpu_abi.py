@@ -103,7 +103,7 @@ def test_stats_report_schedule(cornell):
     with rvcp_amd.RayTracer(spp=30) as rt:          # Cornell: the scene-specialised kernels
         rt.upload_scene(cornell)
         rt.render(1024, 1024, TIME)
-        assert int(rt.last_stats["kernel_variant"]) == 6 | spec
+        assert int(rt.last_stats["kernel_variant"]) == 3 | spec      # 5 waves beats 6 here
         rt.render(64, 64, TIME)
         assert int(rt.last_stats["kernel_variant"]) == 3 | spec
     with rvcp_amd.RayTracer(spp=30, specialize=rvcp_amd.abi.SPECIALIZE_OFF) as rt:
