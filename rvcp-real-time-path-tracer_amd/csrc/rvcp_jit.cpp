@@ -33,6 +33,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <list>
 #include <memory>
@@ -183,7 +184,10 @@ bool emit_triangle(std::string &out, const TriRecord &T, uint32_t index, const c
     const Val n1 = g.dot(s1, s);
     const Val n2 = g.dot(s2, d);
     const Val tt = g.dot(s2, e2);
-    const Val f = g.tmp("rcp_ieee(" + g.text(den) + ")");
+    // the fast reciprocal; a non-normal result flags the lane's ray (`bad`, `badA`, `badB`)
+    // and the caller redoes the wave's scan with the generic loop (rcp_ieee's IEEE fallback)
+    // when a flagged ray is live, so there is no branch here
+    const Val f = g.tmp("RVCP_SPEC_RCP(" + g.text(den) + ", bad" + R + ")");
     // t = f * dot(s2, e2) (:255); a vanished dot leaves t = +-0 or NaN, rejected by
     // t >= t_min > 0 in both forms
     const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.tmp(f.name + " * " + g.text(tt)).name;
@@ -219,11 +223,11 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n)
     std::string out = "// generated by rvcp_jit.cpp: the scan of DESIGN.md §4.7 over " +
                       std::to_string(n) + " triangles\n";
     out += "__device__ __forceinline__ void spec_scan1(f3 o, f3 d, float tmin, float &bt, "
-           "int &best) {\n";
+           "int &best, bool &bad) {\n";
     for (uint32_t i = 0; i < n; i++) emit_triangle(out, tri[i], i, "");
     out += "}\n";
     out += "__device__ __forceinline__ void spec_scan2(f3 oA, f3 dA, f3 oB, f3 dB, float tmin, "
-           "float &btA, int &bestA, float &btB, int &bestB) {\n";
+           "float &btA, int &bestA, float &btB, int &bestB, bool &badA, bool &badB) {\n";
     for (uint32_t i = 0; i < n; i++) {
         emit_triangle(out, tri[i], i, "A");
         emit_triangle(out, tri[i], i, "B");
@@ -283,10 +287,25 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
         return -1;
     }
     // the flags of the static build (Makefile): the numeric contract depends on them
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                          "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-fast-math",
-                          "-fno-slp-vectorize", "-DRVCP_JIT", "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
-    const int rc = api.compile(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+    std::vector<std::string> extra;            // RVCP_JIT_FLAGS: experiment -D options
+    if (const char *e = std::getenv("RVCP_JIT_FLAGS")) {
+        std::string cur;
+        for (const char *c = e;; c++) {
+            if (*c == ' ' || *c == '\0') {
+                if (!cur.empty()) extra.push_back(cur);
+                cur.clear();
+                if (!*c) break;
+            } else {
+                cur += *c;
+            }
+        }
+    }
+    std::vector<const char *> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17",
+                                      "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+                                      "-fno-fast-math", "-fno-slp-vectorize", "-DRVCP_JIT",
+                                      "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
+    for (const std::string &x : extra) opts.push_back(x.c_str());
+    const int rc = api.compile(prog, (int)opts.size(), opts.data());
     if (rc != 0) {
         size_t ls = 0;
         api.log_size(prog, &ls);

@@ -131,6 +131,28 @@ __device__ __forceinline__ float rcp_ieee(float den) {
     return f;
 }
 
+// The scan's 1 / den: rcp_ieee, except that a zero or NaN denominator keeps the fast result
+// (NaN) instead of taking the IEEE division (+-inf / NaN).  Exact for the scan's decision: with
+// den = +-0 the shader's t = f * dot(s2, e2) is +-inf or NaN and fails t >= t_min & t <= t_max
+// (t_max < 2^24), as NaN does.  Such denominators are common -- rand() returns exactly 0.5 one
+// time in a few hundred (fract of a float near 2^15 has 8 fraction bits), which gives ray
+// directions with an exact zero component, parallel to the axis-aligned Cornell walls --
+// and each took the whole wave through the division.
+// (The denominator's class is tested inside the rare branch, so the fast path costs what
+// rcp_ieee's does; a class test outside it measured 2 % slower.)
+__device__ __forceinline__ float rcp_scan(float den) {
+#ifdef RVCP_SCAN_RCP_IEEE         // A/B experiment: the plain rcp_ieee
+    return rcp_ieee(den);
+#endif
+    const float r = __builtin_amdgcn_rcpf(den);
+    float f = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    if (__builtin_expect(!__builtin_amdgcn_classf(f, (1 << 8) | (1 << 3)), 0)) {
+        if (__builtin_amdgcn_classf(den, 0x39c))                     // +-normal/subnormal/inf
+            f = 1.0f / den;
+    }
+    return f;
+}
+
 // Tone map + UNORM8 (:498-500) by the threshold table of DESIGN.md §3.3.
 __device__ __forceinline__ uint32_t gamma_u8(float c, const float *__restrict__ T) {
     const float x = (c > 0.0f) ? ((c < 1.0f) ? c : 1.0f) : 0.0f;
@@ -179,7 +201,7 @@ __device__ __forceinline__ TriPart tri_stage1(const TriRecord &T, f3 o, f3 d) {
 // would replace the current nearest hit whose time is `bt`.  5-compare form, DESIGN.md §3.5.
 __device__ __forceinline__ bool tri_stage2(const TriRecord &T, const TriPart &P, float tmin,
                                            float bt, float &t_out) {
-    const float f = rcp_ieee(P.den);
+    const float f = rcp_scan(P.den);
     const float t = f * dot(P.s2, ld3(T.e2));
     const float b1 = f * P.n1;
     const float b2 = f * P.n2;
@@ -196,6 +218,12 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
 // interleaves all unrolled tests and spills hundreds of registers
 #define RVCP_SPEC_COMMIT(t, i) do { asm volatile("" : "+v"(t), "+v"(i)); \
                                     __builtin_amdgcn_sched_barrier(0); } while (0)
+// The reciprocal of the specialised tests: rcp_scan, with its rare IEEE branch inline.  (A
+// branch-free variant that flags non-normal reciprocals and re-runs the wave's scan with the
+// generic loop is bit-exact too but measured 1.9x slower: the flag bookkeeping across 64
+// unrolled tests costs more than the branches it removes -- DESIGN.md §4.7.)  `flag` stays
+// false; the callers' re-scan path is kept for that experiment.
+#define RVCP_SPEC_RCP(den, flag) rcp_scan(den)
 #include RVCP_SPEC_SCAN
 // The specialised scan drops products with exact-zero triangle components, which is exact
 // only for finite rays; a wave holding any non-finite ray uses the generic loop instead.
@@ -1420,11 +1448,17 @@ __device__ __forceinline__ void path_body(
             float bt = A.t_max;
             int best = -1;
 #ifdef RVCP_SPEC_SCAN
+            bool spec_done = false;
             if (!__any(lane_r < nr && !ray_finite(o, d))) {
-                spec_scan1(o, d, A.t_min, bt, best);
-            } else
+                bool bad = false;
+                spec_scan1(o, d, A.t_min, bt, best, bad);
+                spec_done = !__any(lane_r < nr && bad);
+            }
+            if (!spec_done)
 #endif
             {
+                bt = A.t_max;
+                best = -1;
 #pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
@@ -1458,11 +1492,22 @@ __device__ __forceinline__ void path_body(
 #define RVCP_EXP_SCAN_REPEAT 1
 #endif
 #ifdef RVCP_SPEC_SCAN
+            bool spec_done = false;
             if (!__any((hasA && !ray_finite(a_o, a_d)) || (hasB && !ray_finite(b_o, b_d)))) {
-                spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
-            } else
+                // a lane's idle slot holds a stale ray (often axis-parallel, so a zero
+                // denominator): only the flags of live rays count
+                bool badA = false, badB = false;
+                spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB, badA, badB);
+                spec_done = !__any((hasA && badA) || (hasB && badB));
+            }
+            if (!spec_done)
 #endif
             {
+#if defined(RVCP_SPEC_SCAN) && defined(RVCP_DEBUG_COUNT_RESCAN)
+                if (lane == 0) atomicAdd(&counters[2], 1ull << 32);   // experiment only
+#endif
+                btA = btB = A.t_max;
+                bestA = bestB = -1;
             for (int rep = 0; rep < RVCP_EXP_SCAN_REPEAT; ++rep) {
 #pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {

@@ -1,7 +1,7 @@
 """The scene-specialised scan of rvcp_jit.cpp, checked on the CPU.
 
 1. The generated source (librvcp's rvcp_internal_jit_scan_source) is compiled with g++ and a
-   plain-C prelude (rcp_ieee = the IEEE quotient, commits as no-ops) and run against the CPU
+   plain-C prelude (the reciprocal = the IEEE quotient, commits as no-ops) and run against the CPU
    oracle's ray-triangle test (oracle/rvcp_oracle.c is_intersect_with_face, with the nearest-
    hit rule of get_intersection_with_scene): the nearest (t, face) of every ray must be
    bit-identical.  Rays: random, axis-aligned, parallel to walls, aimed at shared edges and
@@ -30,7 +30,7 @@ PRELUDE = r"""
 #define __forceinline__ inline
 struct f3 { float x, y, z; };
 static inline float RVCP_F32(uint32_t b) { float f; std::memcpy(&f, &b, 4); return f; }
-static inline float rcp_ieee(float d) { return 1.0f / d; }
+#define RVCP_SPEC_RCP(d, flag) (1.0f / (d))
 #define RVCP_SPEC_COMMIT(t, i) ((void)0)
 """
 DRIVER = r"""
@@ -43,9 +43,11 @@ extern "C" void scan_all(const float *rays, int n, float tmin, float tmax, float
         if (dual) {           // the two-ray form, with a second (different) ray in slot B
             f3 o2{q[0] + 1.0f, q[1], q[2]}, d2{q[4], q[5], q[3]};
             float bt2 = tmax; int best2 = -1;
-            spec_scan2(o, d, o2, d2, tmin, bt, best, bt2, best2);
+            bool badA = false, badB = false;
+            spec_scan2(o, d, o2, d2, tmin, bt, best, bt2, best2, badA, badB);
         } else {
-            spec_scan1(o, d, tmin, bt, best);
+            bool bad = false;
+            spec_scan1(o, d, tmin, bt, best, bad);
         }
         bt_out[r] = bt; best_out[r] = best;
     }
