@@ -79,3 +79,30 @@ def test_gloo_two_rank_gather(tmp_path):
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     assert bool(np.load(tmp_path / "ok.npy")[0])
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 5, 7, 8])
+@pytest.mark.parametrize("H", [2048, 1024, 37, 8, 1])
+def test_gather_entry_point_geometry(world, H):
+    """The buffer geometry rvcp_gather_frame_async relies on (include/rvcp.h), from the C-ABI's
+    rvcp_shard_rows: every rank sends rvcp_shard_rows(H, 0, world) rows (shard 0 has the most;
+    shorter shards send padding), the N slots cover the frame exactly once, and the device
+    assembly (assemble_kernel, stripe s -> slot s % N, row (s / N) * 8 + y % 8) puts every row
+    where a 1-GPU render has it."""
+    L = rvcp_amd.abi.load()
+    rows = [int(L.rvcp_shard_rows(H, k, world)) for k in range(world)]
+    slot = int(L.rvcp_shard_rows(H, 0, world))
+    assert sum(rows) == H and max(rows) == slot == FR.slot_rows(H, world)
+    # the gathered buffer carries each row's global index; the kernel's index arithmetic
+    gathered = np.full((world, slot), -1, np.int64)
+    for k in range(world):
+        ids = FR.shard_row_ids(H, k, world)
+        assert len(ids) == rows[k]
+        gathered[k, :rows[k]] = ids
+    frame_rows = np.empty(H, np.int64)
+    for y in range(H):
+        stripe = y >> 3
+        shard = stripe % world
+        lrow = (stripe // world) * 8 + (y & 7)
+        frame_rows[y] = gathered[shard, lrow]
+    assert np.array_equal(frame_rows, np.arange(H))
