@@ -184,10 +184,7 @@ bool emit_triangle(std::string &out, const TriRecord &T, uint32_t index, const c
     const Val n1 = g.dot(s1, s);
     const Val n2 = g.dot(s2, d);
     const Val tt = g.dot(s2, e2);
-    // the fast reciprocal; a non-normal result flags the lane's ray (`bad`, `badA`, `badB`)
-    // and the caller redoes the wave's scan with the generic loop (rcp_ieee's IEEE fallback)
-    // when a flagged ray is live, so there is no branch here
-    const Val f = g.tmp("RVCP_SPEC_RCP(" + g.text(den) + ", bad" + R + ")");
+    const Val f = g.tmp("RVCP_SPEC_RCP(" + g.text(den) + ")");               // :254
     // t = f * dot(s2, e2) (:255); a vanished dot leaves t = +-0 or NaN, rejected by
     // t >= t_min > 0 in both forms
     const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.tmp(f.name + " * " + g.text(tt)).name;
@@ -223,11 +220,11 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n)
     std::string out = "// generated by rvcp_jit.cpp: the scan of DESIGN.md §4.7 over " +
                       std::to_string(n) + " triangles\n";
     out += "__device__ __forceinline__ void spec_scan1(f3 o, f3 d, float tmin, float &bt, "
-           "int &best, bool &bad) {\n";
+           "int &best) {\n";
     for (uint32_t i = 0; i < n; i++) emit_triangle(out, tri[i], i, "");
     out += "}\n";
     out += "__device__ __forceinline__ void spec_scan2(f3 oA, f3 dA, f3 oB, f3 dB, float tmin, "
-           "float &btA, int &bestA, float &btB, int &bestB, bool &badA, bool &badB) {\n";
+           "float &btA, int &bestA, float &btB, int &bestB) {\n";
     for (uint32_t i = 0; i < n; i++) {
         emit_triangle(out, tri[i], i, "A");
         emit_triangle(out, tri[i], i, "B");

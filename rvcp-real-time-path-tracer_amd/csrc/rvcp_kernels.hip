@@ -219,11 +219,10 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
 #define RVCP_SPEC_COMMIT(t, i) do { asm volatile("" : "+v"(t), "+v"(i)); \
                                     __builtin_amdgcn_sched_barrier(0); } while (0)
 // The reciprocal of the specialised tests: rcp_scan, with its rare IEEE branch inline.  (A
-// branch-free variant that flags non-normal reciprocals and re-runs the wave's scan with the
-// generic loop is bit-exact too but measured 1.9x slower: the flag bookkeeping across 64
-// unrolled tests costs more than the branches it removes -- DESIGN.md §4.7.)  `flag` stays
-// false; the callers' re-scan path is kept for that experiment.
-#define RVCP_SPEC_RCP(den, flag) rcp_scan(den)
+// branch-free variant that only flags non-normal reciprocals and re-runs the wave's scan with
+// the generic loop when a live ray was flagged is bit-exact too but measured 1.9x slower --
+// DESIGN.md §4.7.)
+#define RVCP_SPEC_RCP(den) rcp_scan(den)
 #include RVCP_SPEC_SCAN
 // The specialised scan drops products with exact-zero triangle components, which is exact
 // only for finite rays; a wave holding any non-finite ray uses the generic loop instead.
@@ -1448,17 +1447,11 @@ __device__ __forceinline__ void path_body(
             float bt = A.t_max;
             int best = -1;
 #ifdef RVCP_SPEC_SCAN
-            bool spec_done = false;
             if (!__any(lane_r < nr && !ray_finite(o, d))) {
-                bool bad = false;
-                spec_scan1(o, d, A.t_min, bt, best, bad);
-                spec_done = !__any(lane_r < nr && bad);
-            }
-            if (!spec_done)
+                spec_scan1(o, d, A.t_min, bt, best);
+            } else
 #endif
             {
-                bt = A.t_max;
-                best = -1;
 #pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
@@ -1492,22 +1485,11 @@ __device__ __forceinline__ void path_body(
 #define RVCP_EXP_SCAN_REPEAT 1
 #endif
 #ifdef RVCP_SPEC_SCAN
-            bool spec_done = false;
             if (!__any((hasA && !ray_finite(a_o, a_d)) || (hasB && !ray_finite(b_o, b_d)))) {
-                // a lane's idle slot holds a stale ray (often axis-parallel, so a zero
-                // denominator): only the flags of live rays count
-                bool badA = false, badB = false;
-                spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB, badA, badB);
-                spec_done = !__any((hasA && badA) || (hasB && badB));
-            }
-            if (!spec_done)
+                spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
+            } else
 #endif
             {
-#if defined(RVCP_SPEC_SCAN) && defined(RVCP_DEBUG_COUNT_RESCAN)
-                if (lane == 0) atomicAdd(&counters[2], 1ull << 32);   // experiment only
-#endif
-                btA = btB = A.t_max;
-                bestA = bestB = -1;
             for (int rep = 0; rep < RVCP_EXP_SCAN_REPEAT; ++rep) {
 #pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {

@@ -30,7 +30,7 @@ PRELUDE = r"""
 #define __forceinline__ inline
 struct f3 { float x, y, z; };
 static inline float RVCP_F32(uint32_t b) { float f; std::memcpy(&f, &b, 4); return f; }
-#define RVCP_SPEC_RCP(d, flag) (1.0f / (d))
+#define RVCP_SPEC_RCP(d) (1.0f / (d))
 #define RVCP_SPEC_COMMIT(t, i) ((void)0)
 """
 DRIVER = r"""
@@ -43,11 +43,9 @@ extern "C" void scan_all(const float *rays, int n, float tmin, float tmax, float
         if (dual) {           // the two-ray form, with a second (different) ray in slot B
             f3 o2{q[0] + 1.0f, q[1], q[2]}, d2{q[4], q[5], q[3]};
             float bt2 = tmax; int best2 = -1;
-            bool badA = false, badB = false;
-            spec_scan2(o, d, o2, d2, tmin, bt, best, bt2, best2, badA, badB);
+            spec_scan2(o, d, o2, d2, tmin, bt, best, bt2, best2);
         } else {
-            bool bad = false;
-            spec_scan1(o, d, tmin, bt, best, bad);
+            spec_scan1(o, d, tmin, bt, best);
         }
         bt_out[r] = bt; best_out[r] = best;
     }
