@@ -76,24 +76,22 @@ static inline float fractf(float x) { return x - floorf(x); }     /* GLSL fract 
 static inline v3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 
 /* ------------------------------------------------------------------------------------- */
-/* Software sin: Cody-Waite reduction by pi/2 with fma, Cephes minimax    */
-/* polynomials on [-pi/4, pi/4].  Bit-identical wherever fmaf/rintf/floorf are IEEE.       */
+/* Software sin: q = rint(x / pi), Cody-Waite reduction by pi with fma,   */
+/* one odd minimax polynomial on [-pi/2, pi/2], sign flipped for odd q.  Bit-identical     */
+/* wherever fmaf/rintf/floorf are IEEE.                                                    */
 /* ------------------------------------------------------------------------------------- */
 float rvcp_oracle_sinf(float x)
 {
     if (!(fabsf(x) < 1.0e30f)) return x - x;            /* NaN for inf/NaN */
-    const float q = rintf(x * 0.636619772367581343f);   /* nearest quadrant */
-    float r = fmaf(q, -1.57079637050628662109375f, x);  /* x - q*float(pi/2) */
-    r = fmaf(q, 4.37113900018624283e-8f, r);            /* - q*(pi/2 - float(pi/2)) */
+    const float q = rintf(x * 0x1.45f306p-2f);          /* nearest multiple of pi */
+    float r = fmaf(q, -0x1.921fb6p+1f, x);              /* x - q*float(pi) */
+    r = fmaf(q, 0x1.777a5cp-24f, r);                    /* - q*(pi - float(pi)) */
     const float z = r * r;
-    const float ps = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
-    const float s = fmaf(ps, z * r, r);
-    const float pc = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
-                          4.166664568298827e-2f);
-    const float c = fmaf(pc, z * z, fmaf(-0.5f, z, 1.0f));
-    const float qm = q - 4.0f * floorf(q * 0.25f);     /* q mod 4, exact */
-    const int j = (int)qm;
-    return j == 0 ? s : (j == 1 ? c : (j == 2 ? -s : -c));
+    const float p = fmaf(fmaf(fmaf(0x1.5dbdfep-19f, z, -0x1.9f7p-13f), z, 0x1.110ed4p-7f), z,
+                         -0x1.55554cp-3f);
+    const float s = fmaf(p, z * r, r);
+    const float odd = q - 2.0f * floorf(q * 0.5f);      /* q mod 2, exact */
+    return odd != 0.0f ? -s : s;
 }
 
 /* ------------------------------------------------------------------------------------- */

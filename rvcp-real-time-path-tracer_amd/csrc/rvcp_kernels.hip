@@ -64,44 +64,38 @@ __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]);
 
 constexpr uint32_t kLight = 3u;         // MATERIAL_LIGHT, ray_tracer_games101_branch.comp:25
 
-// Software sin: the DESIGN.md §3.2 contract (same algorithm as the oracle).
+// Software sin: the DESIGN.md §3.2 contract (same algorithm as the oracle): reduction by pi
+// (q = rint(x / pi), two-constant Cody-Waite with fma), one odd minimax polynomial on
+// [-pi/2, pi/2], sign flipped for odd q.
+constexpr float kInvPi = 0x1.45f306p-2f;          // float(1 / pi)
+constexpr float kPiHi = 0x1.921fb6p+1f;           // float(pi)
+constexpr float kPiLo = 0x1.777a5cp-24f;          // float(float(pi) - pi)
+__device__ __forceinline__ float sin_poly(float r) {
+    const float z = r * r;
+    const float p = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(0x1.5dbdfep-19f, z, -0x1.9f7p-13f),
+                                                  z, 0x1.110ed4p-7f), z, -0x1.55554cp-3f);
+    return __builtin_fmaf(p, z * r, r);
+}
 __device__ __forceinline__ float pt_sinf(float x) {
     if (!(__builtin_fabsf(x) < 1.0e30f)) return x - x;
-    const float q = __builtin_rintf(x * 0.636619772367581343f);
-    float r = __builtin_fmaf(q, -1.57079637050628662109375f, x);
-    r = __builtin_fmaf(q, 4.37113900018624283e-8f, r);
-    const float z = r * r;
-    const float ps = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
-                                    -1.6666654611e-1f);
-    const float s = __builtin_fmaf(ps, z * r, r);
-    const float pc = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f),
-                                    z, 4.166664568298827e-2f);
-    const float c = __builtin_fmaf(pc, z * z, __builtin_fmaf(-0.5f, z, 1.0f));
-    const float qm = q - 4.0f * __builtin_floorf(q * 0.25f);
-    const int j = (int)qm;
-    const float v = (j & 1) ? c : s;
-    return (j & 2) ? -v : v;
+    const float q = __builtin_rintf(x * kInvPi);
+    float r = __builtin_fmaf(q, -kPiHi, x);
+    r = __builtin_fmaf(q, kPiLo, r);
+    const float s = sin_poly(r);
+    const float odd = q - 2.0f * __builtin_floorf(q * 0.5f);      // q mod 2, exact
+    return odd != 0.0f ? -s : s;
 }
 
 // pt_sinf for rand()'s arguments only: seed + index with seed in [0, 1] (a fract) and index a
 // float counter that stops growing at 2^24, so x lies in [1, 2^24 + 4]: finite and positive,
-// q = rint(x * 2/pi) < 2^24 is an exact integer, and (int)q & 3 equals q - 4 floor(q / 4).
-// The same arithmetic as pt_sinf without its range guard and with the integer quadrant
-// (6 fewer VALU instructions per rand()).
+// q = rint(x / pi) < 2^23 is an exact integer, and its parity is the low bit of (int)q, moved
+// into the sign bit.  The same arithmetic as pt_sinf without its range guard.
 __device__ __forceinline__ float pt_sinf_rand(float x) {
-    const float q = __builtin_rintf(x * 0.636619772367581343f);
-    float r = __builtin_fmaf(q, -1.57079637050628662109375f, x);
-    r = __builtin_fmaf(q, 4.37113900018624283e-8f, r);
-    const float z = r * r;
-    const float ps = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
-                                    -1.6666654611e-1f);
-    const float s = __builtin_fmaf(ps, z * r, r);
-    const float pc = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f),
-                                    z, 4.166664568298827e-2f);
-    const float c = __builtin_fmaf(pc, z * z, __builtin_fmaf(-0.5f, z, 1.0f));
-    const int j = (int)q;
-    const float v = (j & 1) ? c : s;
-    return (j & 2) ? -v : v;
+    const float q = __builtin_rintf(x * kInvPi);
+    float r = __builtin_fmaf(q, -kPiHi, x);
+    r = __builtin_fmaf(q, kPiLo, r);
+    const float s = sin_poly(r);
+    return __uint_as_float(__float_as_uint(s) ^ ((uint32_t)(int)q << 31));
 }
 
 __device__ __forceinline__ uint32_t lane_id() {
@@ -1487,6 +1481,19 @@ __device__ __forceinline__ void path_body(
 #ifdef RVCP_SPEC_SCAN
             if (!__any((hasA && !ray_finite(a_o, a_d)) || (hasB && !ray_finite(b_o, b_d)))) {
                 spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
+#if defined(RVCP_EXP_SCAN_REPEAT) && RVCP_EXP_SCAN_REPEAT > 1
+                // experiment: the scan again on laundered copies of the rays,
+                // results discarded -- its marginal cost is the scan's share of the frame
+                for (int rep = 1; rep < RVCP_EXP_SCAN_REPEAT; ++rep) {
+                    f3 ao = a_o, ad = a_d, bo = b_o, bd = b_d;
+                    asm volatile("" : "+v"(ao.x), "+v"(ao.y), "+v"(ao.z), "+v"(ad.x), "+v"(ad.y), "+v"(ad.z));
+                    asm volatile("" : "+v"(bo.x), "+v"(bo.y), "+v"(bo.z), "+v"(bd.x), "+v"(bd.y), "+v"(bd.z));
+                    float t1 = A.t_max, t2 = A.t_max;
+                    int i1 = -1, i2 = -1;
+                    spec_scan2(ao, ad, bo, bd, A.t_min, t1, i1, t2, i2);
+                    asm volatile("" :: "v"(t1), "v"(i1), "v"(t2), "v"(i2));
+                }
+#endif
             } else
 #endif
             {

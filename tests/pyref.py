@@ -72,17 +72,15 @@ def fma_exact(a, b, c) -> np.float32:
 def sinf(x) -> np.float32:
     """DESIGN.md §3.2 software sin."""
     x = F(x)
-    q = F(np.rint(F(x * F(0.636619772367581343))))
-    r = fma(q, F(-1.57079637050628662109375), x)
-    r = fma(q, F(4.37113900018624283e-8), r)
+    q = F(np.rint(F(x * F(float.fromhex("0x1.45f306p-2")))))
+    r = fma(q, F(-float.fromhex("0x1.921fb6p+1")), x)
+    r = fma(q, F(float.fromhex("0x1.777a5cp-24")), r)
     z = F(r * r)
-    ps = fma(fma(F(-1.9515295891e-4), z, F(8.3321608736e-3)), z, F(-1.6666654611e-1))
-    s = fma(ps, F(z * r), r)
-    pc = fma(fma(F(2.443315711809948e-5), z, F(-1.388731625493765e-3)), z, F(4.166664568298827e-2))
-    c = fma(pc, F(z * z), fma(F(-0.5), z, F(1.0)))
-    qm = F(q - F(F(4.0) * F(np.floor(F(q * F(0.25))))))
-    j = int(qm)
-    return [s, c, F(-s), F(-c)][j]
+    p = fma(fma(fma(F(float.fromhex("0x1.5dbdfep-19")), z, F(-float.fromhex("0x1.9f7p-13"))), z,
+                F(float.fromhex("0x1.110ed4p-7"))), z, F(-float.fromhex("0x1.55554cp-3")))
+    s = fma(p, F(z * r), r)
+    odd = F(q - F(F(2.0) * F(np.floor(F(q * F(0.5))))))
+    return F(-s) if odd != 0 else s
 
 
 def fract(x):
