@@ -65,7 +65,7 @@ def c3_frame(cornell_arrays, cornell):
 def test_readme_blocks_full_resolution(c3_frame):
     rgba, trav = c3_frame
     rms, mean = _rms_vs_readme(rgba)
-    assert rms < 0.006, rms                  # measured 0.0032 (quirk off: 0.027)
+    assert rms < 0.006, rms                  # measured 0.0033 (quirk off: 0.027)
     # miss pixels outside the open box are exactly 64 in the screenshot and here
     assert (rgba[0, 0, :3] == 64).all() and (rgba[1023, 1023, :3] == 64).all()
     assert 4.85 < trav / (1024 * 1024 * 30) < 5.0
