@@ -4,8 +4,11 @@
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
 
 One step = one frame: every rank renders its 8-row stripes of the frame with the HIP kernel
-(rvcp_render_shard_async), the stripes are gathered to rank 0 over RCCL (torch.distributed
-'nccl' backend) and rank 0 assembles the frame on the device.  Scene and camera are uploaded
+(rvcp_render_shard_async), the stripes are gathered to rank 0 over RCCL
+(rvcp_gather_frame_async: ncclGather inside librvcp) and rank 0 assembles the frame on the
+device.  Two frames are in flight (--frames-in-flight, default 2): two contexts, each on its
+own stream, render consecutive frames, so a frame's start overlaps the previous frame's tail
+(DESIGN.md §4.8); every step still renders its whole frame.  Scene and camera are uploaded
 once, before timing (inputs resident in HBM).
 
 Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
@@ -201,6 +204,9 @@ def main():
                     help="oracle threads for cpu_baseline (default: every hardware thread "
                          "this process may use; the OMP_NUM_THREADS share is timed beside it)")
     ap.add_argument("--save-frame", default="")
+    ap.add_argument("--frames-in-flight", type=int, default=2,
+                    help="contexts rendering consecutive frames concurrently (1 = one frame "
+                         "at a time; N>1 rehearsals always use 1)")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
     args = ap.parse_args()
@@ -239,63 +245,101 @@ def main():
         cfg_kw["integrator"] = 1
     if args.accel == "bvh":
         cfg_kw["accel"] = 1
-    rt = rvcp_amd.RayTracer(**cfg_kw)
+    # Frames in flight: `fif` contexts render consecutive frames on their own
+    # streams, so frame f+1's pre-pass and path kernel fill the CUs that frame f's tail leaves
+    # idle -- the per-image fences of the reference's swapchain loop (vulkan.rs:367-369).  A
+    # context holds one frame at a time (rvcp.h), so frame f waits, at its enqueue, for the
+    # frame its context rendered fif steps earlier.
+    fif = 1 if rehearsal else max(1, args.frames_in_flight)
+    rts = [rvcp_amd.RayTracer(**cfg_kw) for _ in range(fif)]
     t_up = time.perf_counter()
-    rt.upload_scene(sc)                  # includes the scene-specialised compile (§4.7)
+    rts[0].upload_scene(sc)              # includes the scene-specialised compile (§4.7)
     upload_s = time.perf_counter() - t_up
+    for r in rts[1:]:
+        r.upload_scene(sc)               # (the compiled module is cached per process)
+    rt = rts[0]
     push = sc.push_constant(123.0)
     n_faces = len(sc.mesh.aligned_faces())
     n_spheres = len(sc.spheres) if legacy else 0
     if world > 1 and not rehearsal:
-        uid = [rvcp_amd.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        rt.rccl_init(uid[0], world, rank)
+        for r in rts:                    # one communicator per context, created in order
+            uid = [rvcp_amd.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            r.rccl_init(uid[0], world, rank)
 
     rows = rvcp_amd.shard_rows(H, rank, world)
     slot = rvcp_amd.shard_rows(H, 0, world)          # shard 0 has the most rows
     dev = torch.device("cuda", local_rank)
-    shard_buf = torch.zeros((slot, W), dtype=torch.int32, device=dev)
-    frame = torch.zeros((H, W), dtype=torch.int32, device=dev) if rank == 0 else None
-    gat_flat = torch.zeros((world, slot, W), dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
-    stream = torch.cuda.current_stream().cuda_stream
+    shard_bufs = [torch.zeros((slot, W), dtype=torch.int32, device=dev) for _ in range(fif)]
+    frames = [torch.zeros((H, W), dtype=torch.int32, device=dev) if rank == 0 else None
+              for _ in range(fif)]
+    gat_flats = [torch.zeros((world, slot, W), dtype=torch.int32, device=dev)
+                 if (world > 1 and rank == 0) else None for _ in range(fif)]
+    torch.cuda.synchronize()
+    pending = [False] * fif
 
-    def step():
+    def enqueue(i):
+        """Enqueue one frame on context i's own stream (stream 0 = the context's stream)."""
+        r, frame, shard_buf, gat_flat = rts[i], frames[i], shard_bufs[i], gat_flats[i]
         if world == 1:
-            rt.render_shard_async(push, W, H, 0, 1, frame.data_ptr(), stream=stream)
-            return rt.sync_stats()
-        rt.render_shard_async(push, W, H, rank, world, shard_buf.data_ptr(), stream=stream)
+            r.render_shard_async(push, W, H, 0, 1, frame.data_ptr())
+            return
+        r.render_shard_async(push, W, H, rank, world, shard_buf.data_ptr())
         if rehearsal:
-            st = rt.sync_stats()
-            got = rvcp_amd.frame.gather_shards(shard_buf.cpu(), rank, world, dst=0)
-            if rank == 0:
-                gat_flat.copy_(torch.stack(got))
-                rt.assemble_frame_async(gat_flat.data_ptr(), slot, W, H, world, frame.data_ptr(),
-                                        stream=stream)
-            return st
+            return
         # RCCL gather + device assembly, enqueued behind the render without a host sync
-        rt.gather_frame_async(shard_buf.data_ptr(), W, H,
-                              gat_flat.data_ptr() if rank == 0 else 0,
-                              frame.data_ptr() if rank == 0 else 0, stream=stream)
-        return rt.sync_stats()
+        r.gather_frame_async(shard_buf.data_ptr(), W, H,
+                             gat_flat.data_ptr() if rank == 0 else 0,
+                             frame.data_ptr() if rank == 0 else 0)
 
-    for _ in range(args.warmup):
-        step()
+    def finish(i):
+        """Wait for context i's frame; return its stats."""
+        st = rts[i].sync_stats()
+        pending[i] = False
+        if rehearsal:      # gloo gather through host memory (one GPU, all ranks on it)
+            got = rvcp_amd.frame.gather_shards(shard_bufs[i].cpu(), rank, world, dst=0)
+            if rank == 0:
+                gat_flats[i].copy_(torch.stack(got))
+                rts[i].assemble_frame_async(gat_flats[i].data_ptr(), slot, W, H, world,
+                                            frames[i].data_ptr())
+                torch.cuda.synchronize()
+        return st
+
+    def step(f):
+        """Frame f: returns the stats of the frame it waited for (or None)."""
+        i = f % fif
+        st = finish(i) if pending[i] else None
+        enqueue(i)
+        pending[i] = True
+        return st
+
+    def drain():
+        return [finish(i) for i in range(fif) if pending[i]]
+
+    for f in range(args.warmup):
+        step(f)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, main_ms, trav, trav_exec, variant = [], [], 0, 0, 0
+    stats = []
     t0 = time.perf_counter()
     step_ms = []
-    for _ in range(args.steps):
+    for f in range(args.steps):
         ts = time.perf_counter()
-        st = step()
+        st = step(f)
         step_ms.append((time.perf_counter() - ts) * 1000.0)
-        kernel_ms.append(float(st["kernel_ms"]))
-        main_ms.append(float(st["main_kernel_ms"]))
-        trav += int(st["traversals"])
-        trav_exec += int(st["traversals_executed"])
-        variant = int(st["kernel_variant"])
+        if st is not None:
+            stats.append(st)
+    stats += drain()
+    kernel_ms = [float(st["kernel_ms"]) for st in stats]
+    main_ms = [float(st["main_kernel_ms"]) for st in stats]
+    trav = sum(int(st["traversals"]) for st in stats)
+    trav_exec = sum(int(st["traversals_executed"]) for st in stats)
+    variant = int(stats[-1]["kernel_variant"])
+    assert len(stats) == args.steps
+    frame = frames[0]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -338,7 +382,7 @@ def main():
         for _ in range(3):
             torch.cuda.synchronize()
             ts = time.perf_counter()
-            rt.render_shard_async(push, W, H, 0, 1, single.data_ptr(), stream=stream)
+            rt.render_shard_async(push, W, H, 0, 1, single.data_ptr())
             rt.sync_stats()
             torch.cuda.synchronize()
             times.append((time.perf_counter() - ts) * 1000.0)
@@ -376,11 +420,17 @@ def main():
                        "scan": ("scene-specialised (hipRTC at upload, DESIGN.md §4.7)"
                                 if variant & rvcp_amd.abi.VARIANT_SPECIALIZED else "generic"),
                        "upload_s": round(upload_s, 3),
+                       "frames_in_flight": fif,
                        "gather": ("gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
                                   "rccl ncclGather via rvcp_gather_frame_async") if world > 1 else "none"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 2),
                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
+                         # the same useful FLOP over the wall time per frame: with frames in
+                         # flight a launch's event time includes the other frame's overlap
+                         "achieved_wall": round(flop_per_launch / (ms_per_step / 1000.0) / 1e12, 2),
+                         "frac_wall": round(flop_per_launch / (ms_per_step / 1000.0) / 1e12
+                                            / FP32_PEAK_TFLOPS, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
                          "traffic_hbm_frac": None if traffic is None else
@@ -423,7 +473,8 @@ def main():
                                                share_threads=O.default_threads())
         print(json.dumps(out), flush=True)
 
-    rt.close()
+    for r in rts:
+        r.close()
     if world > 1:
         dist.destroy_process_group()
 

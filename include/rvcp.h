@@ -18,7 +18,7 @@
  *     flight.
  *   - Host pointers stay owned by the caller; the library copies what it needs.
  *   - Pointers named `d_*` are HIP device pointers; `stream` is a `hipStream_t` (NULL = the
- *     legacy default stream).
+ *     context's own stream, created by rvcp_create).
  */
 #ifndef RVCP_H
 #define RVCP_H

@@ -87,6 +87,42 @@ def test_rccl_gather_world1(cornell, W, H):
     assert np.array_equal(frame.cpu().numpy().view(np.uint8).reshape(H, W, 4), ref)
 
 
+def test_two_frames_in_flight_with_two_communicators(cornell):
+    """bench.py's frames-in-flight pattern: two contexts, each with its own RCCL communicator
+    and its own stream, render and gather alternate frames without a host sync between
+    enqueues; every assembled frame equals the direct render."""
+    torch = pytest.importorskip("torch")
+    W, H = 160, 72
+    rts = [rvcp_amd.RayTracer(spp=3) for _ in range(2)]
+    try:
+        for rt in rts:
+            rt.upload_scene(cornell)
+            rt.rccl_init(rvcp_amd.rccl_unique_id(), 1, 0)
+        ref = rts[0].render(W, H, TIME)
+        slot = rvcp_amd.shard_rows(H, 0, 1)
+        shards = [torch.zeros((slot, W), dtype=torch.int32, device="cuda") for _ in range(2)]
+        gath = [torch.zeros((1, slot, W), dtype=torch.int32, device="cuda") for _ in range(2)]
+        frames = [torch.zeros((H, W), dtype=torch.int32, device="cuda") for _ in range(2)]
+        pending = [False, False]
+        push = cornell.push_constant(TIME)
+        for f in range(6):
+            i = f % 2
+            if pending[i]:
+                rts[i].sync_stats()
+            rts[i].render_shard_async(push, W, H, 0, 1, shards[i].data_ptr())
+            rts[i].gather_frame_async(shards[i].data_ptr(), W, H, gath[i].data_ptr(),
+                                      frames[i].data_ptr())
+            pending[i] = True
+        for i in range(2):
+            rts[i].sync_stats()
+        torch.cuda.synchronize()
+        for fr in frames:
+            assert np.array_equal(fr.cpu().numpy().view(np.uint8).reshape(H, W, 4), ref)
+    finally:
+        for rt in rts:
+            rt.close()
+
+
 def test_gather_without_communicator(cornell):
     torch = pytest.importorskip("torch")
     d = torch.zeros(64, dtype=torch.int32, device="cuda")
