@@ -204,9 +204,10 @@ def main():
                     help="oracle threads for cpu_baseline (default: every hardware thread "
                          "this process may use; the OMP_NUM_THREADS share is timed beside it)")
     ap.add_argument("--save-frame", default="")
-    ap.add_argument("--frames-in-flight", type=int, default=2,
+    ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="contexts rendering consecutive frames concurrently (1 = one frame "
-                         "at a time; N>1 rehearsals always use 1)")
+                         "at a time; 0 = auto: 3 below 4 Msamples per rank-frame, else 2; "
+                         "N>1 rehearsals always use 1)")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
     args = ap.parse_args()
@@ -250,7 +251,10 @@ def main():
     # idle -- the per-image fences of the reference's swapchain loop (vulkan.rs:367-369).  A
     # context holds one frame at a time (rvcp.h), so frame f waits, at its enqueue, for the
     # frame its context rendered fif steps earlier.
-    fif = 1 if rehearsal else max(1, args.frames_in_flight)
+    # (measured, profiles/r02_fif_sweep.log: C3 1/2/3/4 in flight 4.35/3.83/3.83/3.95 ms,
+    # C2 0.59/0.32/0.27/0.33 ms -- a small frame is mostly tail, so it gains from a third)
+    auto_fif = 3 if (W * spp * rvcp_amd.shard_rows(H, rank, world)) < (4 << 20) else 2
+    fif = 1 if rehearsal else (args.frames_in_flight or auto_fif)
     rts = [rvcp_amd.RayTracer(**cfg_kw) for _ in range(fif)]
     t_up = time.perf_counter()
     rts[0].upload_scene(sc)              # includes the scene-specialised compile (§4.7)
