@@ -60,7 +60,7 @@ for s in $STEPS; do
         c5small) run c5small 300 python tools/frames.py --variant 3 --frames 2 --tris 100000 --size 128 --spp 2 ;;
         c5cmp) run c5cmp 600 bash -c "python tools/frames.py --variant 4 --frames 2 --tris 100000 --size 512 --spp 4 && python tools/frames.py --variant 3 --frames 1 --tris 100000 --size 512 --spp 4" ;;
         split3) run split3 300 env RVCP_KERNEL_VARIANT=3 python tools/exp_split.py ;;
-        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         sqpmc) run sqpmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         sqpmc2) run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         c5pmc) run c5pmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c5pmc_$TAG" -o run --output-format csv -- python3 tools/frames.py --frames 2 --tris 100000 --size 512 --spp 4 ;;
