@@ -607,12 +607,15 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     A.light_total = ctx->light_total;
     A.light_pdf = ctx->light_pdf;
     A.want_linear = d_linear_rgb ? 1u : 0u;
-    // automatic schedule: 5 (LDS tiles) for large meshes, else 3, or 6 (6 waves/SIMD) for
+    // automatic schedule: 4 / 5 (LDS tiles; two rays per lane on large frames, one on small
+    // ones) for large meshes, 4 also for mid-size meshes on large frames, else 3, or 6 (6 waves/SIMD) for
     // large frames -- except with the scene-specialised scan, whose 6-wave build spills and
     // measures slower than its 5-wave one at every size
     const bool jit_ok = ctx->jit && ctx->cfg.ray_t_min > 0.0f;
+    const bool big_frame = (uint64_t)A.n_pixels * A.spp >= kTiledDualMinSamples;
     A.variant = ctx->cfg.kernel_variant != 0 ? ctx->cfg.kernel_variant
-              : ctx->n_faces >= kTiledMinFaces ? 5
+              : ctx->n_faces >= kTiledMinFaces ? (big_frame ? 4 : 5)
+              : (!jit_ok && ctx->n_faces > kTiledWideMinFaces && big_frame) ? 4
               : (!jit_ok && (uint64_t)A.n_pixels * A.spp >= kWideMinSamples) ? 6 : kDefaultVariant;
     A.accel = (ctx->cfg.accel == RVCP_ACCEL_BVH && ctx->n_faces > 0) ? RVCP_ACCEL_BVH : RVCP_ACCEL_NONE;
     if (A.accel == RVCP_ACCEL_BVH) A.variant = 3;    // the BVH traversal lives in the v3 kernels

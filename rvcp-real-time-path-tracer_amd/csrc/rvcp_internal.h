@@ -34,9 +34,11 @@ constexpr uint32_t kChunkWindow = 10000;    // 100 us
 // 2 = shadow + continuation ray per lane per iteration, 3 = primary pre-pass kernel + the
 // variant-2 loop over surface pixels only.
 // 4 = variant 3 with the triangle scan staged through LDS tiles shared by the workgroup
-// (selectable; variant 5 is the automatic choice for meshes of kTiledMinFaces faces or more).
+// (the automatic choice for meshes of kTiledMinFaces faces or more on frames of
+// kTiledDualMinSamples pixel-samples or more).
 // 5 = variant 4 with one ray per lane per iteration (the shadow ray, then the path ray), so no
-// ray slot is empty; for scan-bound meshes.
+// ray slot is empty; the automatic choice for large meshes on smaller frames, whose rays do not
+// fill the chip twice over.
 // 6 = variant 3 compiled for 6 waves per SIMD instead of 5 (80 VGPRs, a few spills): faster
 // once the frame is large enough that latency hiding beats the spills (automatic from
 // kWideMinSamples pixel-samples per frame).
@@ -48,6 +50,11 @@ constexpr int kOccupancyBvh = 100;          // rvcp_games101_occupancy code of t
 #define RVCP_TILE 256
 #endif
 constexpr uint32_t kTile = RVCP_TILE;       // triangles per LDS tile (12 KiB at 256)
+constexpr uint64_t kTiledDualMinSamples = 1ull << 19;   // auto: variant 4 rather than 5 from here
+                                            // (4 wins at 512x512x4, 5 at 256x256x4)
+constexpr uint32_t kTiledWideMinFaces = 64;   // auto: variant 4 above this many faces on
+                                            // frames of kTiledDualMinSamples or more (F = 72:
+                                            // 4 beats 3 and 6 from 2 Msamples)
 constexpr uint32_t kTiledMinFaces = 256;   // auto: variant 5 from here (measured crossover
                                             // vs variant 3 at ~230 faces)
 

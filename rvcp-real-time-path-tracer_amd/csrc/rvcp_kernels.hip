@@ -229,6 +229,33 @@ __device__ __forceinline__ bool ray_finite(f3 o, f3 d) {
 // A necessary condition for tri_stage2 to accept, from stage 1 alone: |n1| and |n2| at most
 // RN(|den| (1 + 2^-20)) (proof: DESIGN.md §4.2).  A wave skips stage 2 of a triangle when no
 // lane passes it; no result changes.
+// The pretest in two halves (LDS-tiled scans): stage 1a computes s, s1 = d x e2, den and
+// n1 = s1.s; only if some lane has |n1| <= m does the wave compute s2 = s x e1 and n2 (stage
+// 1b) and test |n2| <= m.  The same operations on the same values as tri_stage1, so exact;
+// for a mesh of small triangles most (ray, triangle) pairs of a wave already fail the first
+// half, saving the 9 instructions of s2 and n2.
+struct TriPartA {
+    f3 s, s1;
+    float den, n1, m;
+};
+__device__ __forceinline__ TriPartA tri_stage1a(const TriRecord &T, f3 o, f3 d) {
+    TriPartA P;
+    P.s = mk(o.x - T.v0[0], o.y - T.v0[1], o.z - T.v0[2]);
+    P.s1 = cross(d, ld3(T.e2));
+    P.den = dot(P.s1, ld3(T.e1));
+    P.n1 = dot(P.s1, P.s);
+    P.m = __builtin_fabsf(P.den) * 1.00000095367431640625f;      // 1 + 2^-20
+    return P;
+}
+__device__ __forceinline__ bool tri_maybe_a(const TriPartA &P) { return __builtin_fabsf(P.n1) <= P.m; }
+__device__ __forceinline__ TriPart tri_stage1b(const TriRecord &T, const TriPartA &Pa, f3 d) {
+    TriPart P;
+    P.s2 = cross(Pa.s, ld3(T.e1));
+    P.den = Pa.den;
+    P.n1 = Pa.n1;
+    P.n2 = dot(P.s2, d);
+    return P;
+}
 __device__ __forceinline__ bool tri_maybe(const TriPart &P) {
     const float m = __builtin_fabsf(P.den) * 1.00000095367431640625f;     // 1 + 2^-20
     return (__builtin_fabsf(P.n1) <= m) & (__builtin_fabsf(P.n2) <= m);
@@ -1089,6 +1116,9 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_BVH_SINGLE
 #define RVCP_BVH_SINGLE true
 #endif
+#ifndef RVCP_SPLIT_PRETEST
+#define RVCP_SPLIT_PRETEST 1
+#endif
 #ifndef RVCP_TILED_MIN_WAVES
 #define RVCP_TILED_MIN_WAVES 4
 #endif
@@ -1148,6 +1178,9 @@ __device__ __forceinline__ void path_body(
     // each sample start instead of being held in 10 VGPRs for the whole pixel
     uint32_t pslot = 0, k = 0, depth = 0;
     uint32_t trav_wave = 0, iters = 0;      // wave-uniform: traversals of all lanes, iterations
+#ifdef RVCP_DEBUG_NR_HIST
+    unsigned long long nr_hist = 0;
+#endif
     float seed = 0.0f, ridx = 0.0f;
     f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
     f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0), S_alb = mk(0, 0, 0);
@@ -1276,6 +1309,12 @@ __device__ __forceinline__ void path_body(
             break;
         }
         if (wave_active) iters += 1;
+#ifdef RVCP_DEBUG_NR_HIST
+        {
+            const uint32_t n_r = (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
+            if (wave_active) nr_hist += n_r <= 64u ? (1ull << 42) : n_r <= 96u ? (1ull << 21) : 1ull;
+        }
+#endif
         trav_wave += (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
         if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
 
@@ -1331,6 +1370,26 @@ __device__ __forceinline__ void path_body(
                     // the next triangle costs 12 VGPRs and was slower at 4 waves/SIMD.)
                     for (uint32_t i = 0; i < n; ++i) {
                         const TriRecord T = tile[i];
+#if RVCP_SPLIT_PRETEST
+                        const TriPartA PaA = tri_stage1a(T, s_ao, s_ad);
+                        if (__any(sA && tri_maybe_a(PaA))) {
+                            const TriPart PA = tri_stage1b(T, PaA, s_ad);
+                            if (__any(sA && tri_maybe(PA))) {
+                                float tA;
+                                if (tri_stage2(T, PA, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
+                            }
+                        }
+                        if (!SINGLE) {
+                            const TriPartA PaB = tri_stage1a(T, b_o, b_d);
+                            if (__any(sB && tri_maybe_a(PaB))) {
+                                const TriPart PB = tri_stage1b(T, PaB, b_d);
+                                if (__any(sB && tri_maybe(PB))) {
+                                    float tB;
+                                    if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
+                                }
+                            }
+                        }
+#else
                         const TriPart PA = tri_stage1(T, s_ao, s_ad);
                         if (__any(sA && tri_maybe(PA))) {
                             float tA;
@@ -1343,6 +1402,7 @@ __device__ __forceinline__ void path_body(
                                 if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
                             }
                         }
+#endif
                     }
                 }
                 __syncthreads();
@@ -1558,7 +1618,15 @@ __device__ __forceinline__ void path_body(
         hasA = false;
         if (!defer_B) hasB = false;
     }
+#ifdef RVCP_DEBUG_NR_HIST
+    // experiment: wave-iterations by rays per wave, in the wave-iteration counter's place
+    // (bits 0-20: > 96 rays, 21-41: 65-96, 42-62: <= 64)
+    iters = 0;
+    flush_wave_counters(counters, lane, trav_wave, 0u);
+    if (lane == 0) atomicAdd(&counters[2], nr_hist);
+#else
     flush_wave_counters(counters, lane, trav_wave, iters);
+#endif
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;
         unsigned long long *rec = A.timeline + 4ull * w;
