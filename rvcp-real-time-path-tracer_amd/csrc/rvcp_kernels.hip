@@ -1371,19 +1371,24 @@ __device__ __forceinline__ void path_body(
                     for (uint32_t i = 0; i < n; ++i) {
                         const TriRecord T = tile[i];
 #if RVCP_SPLIT_PRETEST
+                        // the gates are lane masks ANDed in scalar registers (ballot of one
+                        // compare each): __any(sA && p) materialised the predicate in a VGPR
+                        // and compared it again, 2 VALU per gate (C5 schedule 4: -7 %)
                         const TriPartA PaA = tri_stage1a(T, s_ao, s_ad);
-                        if (__any(sA && tri_maybe_a(PaA))) {
+                        const uint64_t gA = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaA)) & mA;
+                        if (gA != 0ull) {
                             const TriPart PA = tri_stage1b(T, PaA, s_ad);
-                            if (__any(sA && tri_maybe(PA))) {
+                            if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PA.n2) <= PaA.m) & gA) != 0ull) {
                                 float tA;
                                 if (tri_stage2(T, PA, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
                             }
                         }
                         if (!SINGLE) {
                             const TriPartA PaB = tri_stage1a(T, b_o, b_d);
-                            if (__any(sB && tri_maybe_a(PaB))) {
+                            const uint64_t gB = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaB)) & mB;
+                            if (gB != 0ull) {
                                 const TriPart PB = tri_stage1b(T, PaB, b_d);
-                                if (__any(sB && tri_maybe(PB))) {
+                                if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PB.n2) <= PaB.m) & gB) != 0ull) {
                                     float tB;
                                     if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
                                 }
