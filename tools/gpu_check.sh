@@ -54,12 +54,8 @@ for s in $STEPS; do
         rcp2) run rcp_check2 300 tools/build/rcp_check2 ;;
         valu) run valu_rate 120 tools/build/valu_rate ;;
         pretest) run pretest_check 300 tools/build/pretest_check ;;
-        split) run split 300 python tools/exp_split.py ;;
-        split2) run split2 300 env RVCP_KERNEL_VARIANT=2 python tools/exp_split.py ;;
-        occ) run occ 400 bash tools/exp_occ.sh ;;
         c5small) run c5small 300 python tools/frames.py --variant 3 --frames 2 --tris 100000 --size 128 --spp 2 ;;
         c5cmp) run c5cmp 600 bash -c "python tools/frames.py --variant 4 --frames 2 --tris 100000 --size 512 --spp 4 && python tools/frames.py --variant 3 --frames 1 --tris 100000 --size 512 --spp 4" ;;
-        split3) run split3 300 env RVCP_KERNEL_VARIANT=3 python tools/exp_split.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         sqpmc) run sqpmc 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         sqpmc2) run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
