@@ -1762,15 +1762,28 @@ __device__ __forceinline__ float fresnel_schlick(float cosine, float ratio) {
 // nearest-hit rule of get_intersection_with_scene (:376-381): true iff the shader would take
 // this sphere as the new nearest hit, whose time is written to t_out.  a = dot(d, d) and
 // two_a = 2 a are per-ray constants (the shader recomputes the same values per sphere).
+// FAST: the two roots (-b +- sq) / two_a as Markstein quotients from y = RN(1 / two_a)
+// (rcp_ieee, once per ray): q = x y, r = fma(-two_a, q, x) (exact), t = fma(r, y, q) =
+// RN(x / two_a) whenever 2^-60 <= |x| <= 2^60 with two_a in [2^-30, 2^30].  Outside that
+// range both the IEEE root and this one lie below 2^-30 or above 2^30 in magnitude (or are
+// NaN), so with t_min >= 2^-29 and t_max < 2^29 both are rejected, and the root order of the
+// swap differs at most between two rejected roots: the decision and the accepted t are the
+// IEEE ones.  The caller checks the ranges per wave.
+__device__ __forceinline__ float quot_markstein(float x, float s, float y) {
+    const float q = x * y;
+    return __builtin_fmaf(__builtin_fmaf(-s, q, x), y, q);
+}
+template <bool FAST>
 __device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d, float a,
-                                              float two_a, float tmin, float bt, float &t_out) {
+                                              float two_a, float y, float tmin, float bt,
+                                              float &t_out) {
     const f3 co = mk(o.x - S.center[0], o.y - S.center[1], o.z - S.center[2]);
     const float b = 2.0f * dot(d, co);
     const float c = dot(co, co) - S.radius * S.radius;
     const float delta = b * b - 4.0f * a * c;
     const float sq = __builtin_sqrtf(delta);
-    float t0 = (-b + sq) / two_a;
-    float t1 = (-b - sq) / two_a;
+    float t0 = FAST ? quot_markstein(-b + sq, two_a, y) : (-b + sq) / two_a;
+    float t1 = FAST ? quot_markstein(-b - sq, two_a, y) : (-b - sq) / two_a;
     if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
     const bool h0 = (tmin <= t0) & (t0 <= bt);
     const bool h1 = (tmin <= t1) & (t1 <= bt);
@@ -1917,12 +1930,27 @@ __global__ __launch_bounds__(kBlock) void legacy_kernel(
         // ============ trace: get_intersection_with_scene, spheres then faces (:369-393) ============
         int best = -1;
         float bt = rtmax;
+        const float a = dot(rd, rd), two_a = 2.0f * a;
+        // the sphere roots by Markstein quotients when every tracing lane is in range (above)
+#ifndef RVCP_SPHERE_MARKSTEIN
+#define RVCP_SPHERE_MARKSTEIN 1
+#endif
+        const bool fast = RVCP_SPHERE_MARKSTEIN && A.t_max < 0x1p29f &&
+                          __all(st != L_TRACE || ((two_a >= 0x1p-30f) & (two_a <= 0x1p30f) &
+                                                  (rtmin >= 0x1p-29f)));
         if (st == L_TRACE) {
             trav += 1;
-            const float a = dot(rd, rd), two_a = 2.0f * a;
-            for (uint32_t i = 0; i < A.n_spheres; ++i) {
-                float t;
-                if (sphere_accept(sph[i], ro, rd, a, two_a, rtmin, bt, t)) { bt = t; best = (int)i; }
+            if (fast) {
+                const float y = rcp_ieee(two_a);
+                for (uint32_t i = 0; i < A.n_spheres; ++i) {
+                    float t;
+                    if (sphere_accept<true>(sph[i], ro, rd, a, two_a, y, rtmin, bt, t)) { bt = t; best = (int)i; }
+                }
+            } else {
+                for (uint32_t i = 0; i < A.n_spheres; ++i) {
+                    float t;
+                    if (sphere_accept<false>(sph[i], ro, rd, a, two_a, 0.0f, rtmin, bt, t)) { bt = t; best = (int)i; }
+                }
             }
 #pragma unroll 2
             for (uint32_t i = 0; i < A.n_faces; ++i) {
