@@ -528,10 +528,10 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     // scene-specialised scan: compiled here, once per scene and process
     ctx->jit.reset();
     ctx->jit_err.clear();
-    if (ctx->cfg.specialize == RVCP_SPECIALIZE_AUTO &&
-        ctx->cfg.integrator == RVCP_INTEGRATOR_GAMES101 && ctx->cfg.accel == RVCP_ACCEL_NONE &&
+    if (ctx->cfg.specialize == RVCP_SPECIALIZE_AUTO && ctx->cfg.accel == RVCP_ACCEL_NONE &&
         n_faces >= 1 && n_faces <= kJitMaxFaces && !std::getenv("RVCP_NO_SPECIALIZE")) {
-        ctx->jit = jit_path_kernels(ctx->device, tri.data(), n_faces, ctx->jit_err);
+        ctx->jit = jit_path_kernels(ctx->device, tri.data(), n_faces, ctx->jit_err,
+                                    ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY);
         HIP_TRY(ctx, hipSetDevice(ctx->device));
     }
     ctx->n_faces = n_faces;
@@ -643,10 +643,14 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             const int jit_per_cu = !jk ? 0 : A.variant == 6 ? jk->blocks_per_cu6
                                  : A.variant == 3 ? jk->blocks_per_cu5 : 0;
             const bool spec = !legacy && !A.accel && jit_per_cu > 0 && A.t_min > 0.0f;
+            // mode 2 with the specialised triangle scan (its kernel also checks per wave
+            // that every ray is finite and has t_min > 0)
+            const bool spec_legacy = legacy && jk && jk->legacy && jk->blocks_per_cu_legacy > 0;
             uint32_t cap = (uint32_t)(legacy ? ctx->legacy_capacity
                                      : A.accel ? ctx->bvh_capacity
                                                : ctx->grid_capacity[A.variant]);
             if (spec) cap = (uint32_t)jit_per_cu * (ctx->n_simds / 4u);
+            if (spec_legacy) cap = (uint32_t)jk->blocks_per_cu_legacy * (ctx->n_simds / 4u);
             A.n_simds = ctx->n_simds;
             uint32_t waves = 0, chunk = 0;
             rvcp_static_split(A.n_pixels, cap * (kBlock / kWave), A.n_simds, &waves, &chunk);
@@ -689,7 +693,9 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                 HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_legacy(&A, ctx->d_tri, ctx->d_shade, ctx->d_spheres,
                                         ctx->d_rawmats, ctx->d_unorm, (uint32_t *)d_rgba8,
-                                        (float *)d_linear_rgb, ctx->d_counters, blocks, s);
+                                        (float *)d_linear_rgb, ctx->d_counters, blocks, s,
+                                        spec_legacy ? (void *)jk->legacy : nullptr);
+                if (spec_legacy) ctx->last_spec = true;
             } else if (A.variant >= 3) {
                 if (ctx->cap_surf < A.n_pixels) {
                     (void)hipFree(ctx->d_surf);

@@ -221,7 +221,8 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *
 int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
                        const rvcp::FaceShade *shade, const void *spheres, const void *materials,
                        const float *unorm_t, uint32_t *out_rgba, float *out_lin,
-                       unsigned long long *counters, uint32_t grid_blocks, void *stream);
+                       unsigned long long *counters, uint32_t grid_blocks, void *stream,
+                       void *spec_legacy_fn);
 int rvcp_legacy_occupancy(int *blocks_per_cu);
 // mandelbrot.comp (rvcp_mandelbrot.hip)
 int rvcp_launch_mandelbrot(float pos_x, float pos_y, float scale, uint32_t width,

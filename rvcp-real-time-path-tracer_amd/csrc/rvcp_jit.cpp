@@ -269,7 +269,8 @@ JitKernels::~JitKernels()
     }
 }
 
-int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err)
+int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
+                     bool legacy)
 {
     const RtcApi &api = rtc();
     if (!api.ok) {
@@ -301,6 +302,7 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
                                       "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
                                       "-fno-fast-math", "-fno-slp-vectorize", "-DRVCP_JIT",
                                       "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
+    if (legacy) opts.push_back("-DRVCP_JIT_LEGACY");
     for (const std::string &x : extra) opts.push_back(x.c_str());
     const int rc = api.compile(prog, (int)opts.size(), opts.data());
     if (rc != 0) {
@@ -321,9 +323,9 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
 }
 
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
-                                             std::string &err)
+                                             std::string &err, bool legacy)
 {
-    const std::string scan = jit_scan_source(tri, n);
+    const std::string scan = jit_scan_source(tri, n) + (legacy ? "// +legacy\n" : "");
     const uint64_t h = fnv1a(scan);
     std::lock_guard<std::mutex> lock(g_mu);
     for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
@@ -333,7 +335,7 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         }
     }
     std::vector<char> code;
-    if (jit_compile_code(scan, code, err) != 0) return nullptr;
+    if (jit_compile_code(scan, code, err, legacy) != 0) return nullptr;
     auto k = std::make_shared<JitKernels>();
     k->device = device;
     if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&k->module, code.data()) != hipSuccess) {
@@ -346,7 +348,13 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         err = "specialised kernels missing from the module";
         return nullptr;
     }
+    if (legacy && hipModuleGetFunction(&k->legacy, k->module, "rvcp_spec_legacy_kernel") != hipSuccess) {
+        err = "specialised mode-2 kernel missing from the module";
+        return nullptr;
+    }
     int bpc = 0;
+    if (legacy && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->legacy, kBlock, 0) == hipSuccess)
+        k->blocks_per_cu_legacy = bpc;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->path5, kBlock, 0) == hipSuccess)
         k->blocks_per_cu5 = bpc;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->path6, kBlock, 0) == hipSuccess)
@@ -358,18 +366,19 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
 
 }  // namespace rvcp
 
-// Self-test hook for the CPU test suite (not part of rvcp.h): generate and compile the
-// specialised module for n triangle records without a GPU.  Returns 0 and the code-object size,
-// or -1 with the message in err (err_cap bytes).
-extern "C" int rvcp_internal_jit_compile_check(const void *tri_records, uint32_t n,
-                                                size_t *code_bytes, char *err, size_t err_cap)
+// Self-test hooks for the CPU test suite (not part of rvcp.h): generate and compile the
+// specialised module for n triangle records without a GPU (`legacy`: with the mode-2 kernel).
+// Returns 0 and the code-object size, or -1 with the message in err (err_cap bytes).
+extern "C" int rvcp_internal_jit_compile_check_mode(const void *tri_records, uint32_t n,
+                                                     int legacy, size_t *code_bytes, char *err,
+                                                     size_t err_cap)
 {
     try {
         std::string e;
         std::vector<char> code;
         const std::string scan =
             rvcp::jit_scan_source(static_cast<const rvcp::TriRecord *>(tri_records), n);
-        const int rc = rvcp::jit_compile_code(scan, code, e);
+        const int rc = rvcp::jit_compile_code(scan, code, e, legacy != 0);
         if (code_bytes) *code_bytes = code.size();
         if (err && err_cap) {
             std::strncpy(err, e.c_str(), err_cap - 1);
@@ -379,6 +388,12 @@ extern "C" int rvcp_internal_jit_compile_check(const void *tri_records, uint32_t
     } catch (...) {
         return -1;
     }
+}
+
+extern "C" int rvcp_internal_jit_compile_check(const void *tri_records, uint32_t n,
+                                                size_t *code_bytes, char *err, size_t err_cap)
+{
+    return rvcp_internal_jit_compile_check_mode(tri_records, n, 0, code_bytes, err, err_cap);
 }
 
 // The generated scan source for n triangle records (for inspection): writes at most cap bytes

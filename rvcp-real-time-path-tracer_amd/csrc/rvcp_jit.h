@@ -20,17 +20,20 @@ struct JitKernels {
     hipModule_t module = nullptr;
     hipFunction_t path5 = nullptr;     // schedule 3 (5 waves per SIMD)
     hipFunction_t path6 = nullptr;     // schedule 6 (6 waves per SIMD)
-    int blocks_per_cu5 = 0, blocks_per_cu6 = 0;
+    hipFunction_t legacy = nullptr;    // integrator mode 2 (modules compiled with `legacy`)
+    int blocks_per_cu5 = 0, blocks_per_cu6 = 0, blocks_per_cu_legacy = 0;
     ~JitKernels();
 };
 
 // The generated scan (spec_scan1 / spec_scan2) for n triangle records.
 std::string jit_scan_source(const TriRecord *tri, uint32_t n);
 // Compile rvcp_kernels.hip with the given scan for gfx950 (hipRTC); 0 or -1 with err set.
-int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err);
+// `legacy` also builds the mode-2 kernel (RVCP_JIT_LEGACY).
+int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
+                     bool legacy = false);
 // Compiled + loaded kernels for the scene on `device` (process-wide cache keyed by the scan
-// source); nullptr with err set when hipRTC is unavailable or compilation fails.
+// source and `legacy`); nullptr with err set when hipRTC is unavailable or compilation fails.
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
-                                             std::string &err);
+                                             std::string &err, bool legacy = false);
 
 }  // namespace rvcp

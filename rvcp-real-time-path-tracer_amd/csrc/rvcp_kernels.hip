@@ -1730,6 +1730,8 @@ __global__ void fill_kernel(uint32_t *__restrict__ out_rgba, float *__restrict__
     }
 }
 
+#endif  // RVCP_JIT
+#if !defined(RVCP_JIT) || defined(RVCP_JIT_LEGACY)
 // ======================================================================================
 // Integrator RVCP_INTEGRATOR_LEGACY: ray_trace of assets/shaders/ray_tracer.comp
 // (:618-694, main :802-822) -- spheres then triangles, Lambertian / metal / dielectric
@@ -1769,6 +1771,9 @@ __device__ __forceinline__ float fresnel_schlick(float cosine, float ratio) {
 // NaN), so with t_min >= 2^-29 and t_max < 2^29 both are rejected, and the root order of the
 // swap differs at most between two rejected roots: the decision and the accepted t are the
 // IEEE ones.  The caller checks the ranges per wave.
+#ifndef RVCP_SPHERE_SKIP
+#define RVCP_SPHERE_SKIP 1
+#endif
 __device__ __forceinline__ float quot_markstein(float x, float s, float y) {
     const float q = x * y;
     return __builtin_fmaf(__builtin_fmaf(-s, q, x), y, q);
@@ -1781,6 +1786,12 @@ __device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d
     const float b = 2.0f * dot(d, co);
     const float c = dot(co, co) - S.radius * S.radius;
     const float delta = b * b - 4.0f * a * c;
+#if RVCP_SPHERE_SKIP
+    // no lane's line meets the sphere (delta < 0 or NaN everywhere): every lane rejects it
+    // below (!(delta < 0) fails, or NaN roots fail the compares), so the wave skips the
+    // square root, the roots and the compares
+    if (!__any(delta >= 0.0f)) { t_out = bt; return false; }
+#endif
     const float sq = __builtin_sqrtf(delta);
     float t0 = FAST ? quot_markstein(-b + sq, two_a, y) : (-b + sq) / two_a;
     float t1 = FAST ? quot_markstein(-b - sq, two_a, y) : (-b - sq) / two_a;
@@ -1795,13 +1806,13 @@ constexpr int L_IDLE = 0, L_TRACE = 1, L_SCATTER = 2, L_END = 3;
 
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) void legacy_kernel(
-    FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
+__device__ __forceinline__ void legacy_body(
+    const FrameArgs &A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
-    float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
+    uint8_t (*coop_tab)[kWave])
 {
-    __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
     uint8_t *tab = coop_tab[threadIdx.x / kWave];
     const uint32_t lane = lane_id();
     Queue q = queue_init(A);
@@ -1938,6 +1949,9 @@ __global__ __launch_bounds__(kBlock) void legacy_kernel(
         const bool fast = RVCP_SPHERE_MARKSTEIN && A.t_max < 0x1p29f &&
                           __all(st != L_TRACE || ((two_a >= 0x1p-30f) & (two_a <= 0x1p30f) &
                                                   (rtmin >= 0x1p-29f)));
+#ifdef RVCP_SPEC_SCAN
+        const bool spec = __all(st != L_TRACE || (ray_finite(ro, rd) && rtmin > 0.0f));
+#endif
         if (st == L_TRACE) {
             trav += 1;
             if (fast) {
@@ -1952,10 +1966,20 @@ __global__ __launch_bounds__(kBlock) void legacy_kernel(
                     if (sphere_accept<false>(sph[i], ro, rd, a, two_a, 0.0f, rtmin, bt, t)) { bt = t; best = (int)i; }
                 }
             }
+#ifdef RVCP_SPEC_SCAN
+            if (spec) {
+                // the scene-specialised scan (§4.7), exact for finite rays with t_min > 0
+                int bf = -1;
+                spec_scan1(ro, rd, rtmin, bt, bf);
+                if (bf >= 0) best = (int)A.n_spheres + bf;
+            } else
+#endif
+            {
 #pragma unroll 2
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 float t;
                 if (tri_accept(tri[i], ro, rd, rtmin, bt, t)) { bt = t; best = (int)(A.n_spheres + i); }
+            }
             }
         }
 
@@ -2019,7 +2043,29 @@ __global__ __launch_bounds__(kBlock) void legacy_kernel(
     flush_counters(counters, lane, trav, iters);
 }
 
-#endif  // RVCP_JIT
+#ifndef RVCP_JIT
+__global__ __launch_bounds__(kBlock) void legacy_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
+    const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
+    const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
+{
+    __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
+    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
+}
+#else
+// mode 2 with the scene-specialised triangle scan (rvcp_jit.cpp, RVCP_JIT_LEGACY)
+extern "C" __global__ __launch_bounds__(kBlock) void rvcp_spec_legacy_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
+    const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
+    const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
+{
+    __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
+    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
+}
+#endif
+#endif  // !RVCP_JIT || RVCP_JIT_LEGACY
 #ifdef RVCP_JIT
 // Scene-specialised path kernels (rvcp_jit.cpp compiles this file with hipRTC, RVCP_JIT and
 // RVCP_SPEC_SCAN set): schedules 3 and 6 with the scan unrolled over the uploaded scene
@@ -2170,8 +2216,17 @@ extern "C" int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRe
                                   const rvcp::FaceShade *shade, const void *spheres,
                                   const void *materials, const float *unorm_t, uint32_t *out_rgba,
                                   float *out_lin, unsigned long long *counters,
-                                  uint32_t grid_blocks, void *stream)
+                                  uint32_t grid_blocks, void *stream, void *spec_legacy_fn)
 {
+    if (spec_legacy_fn) {
+        // the mode-2 kernel with the scene-specialised triangle scan (rvcp_jit.cpp)
+        rvcp::FrameArgs a = *args;
+        void *params[] = {&a, &tri, &shade, &spheres, &materials, &unorm_t, &out_rgba, &out_lin,
+                          &counters};
+        return hipModuleLaunchKernel((hipFunction_t)spec_legacy_fn, grid_blocks, 1, 1,
+                                     rvcp::kBlock, 1, 1, 0, (hipStream_t)stream, params,
+                                     nullptr) == hipSuccess ? 0 : -2;
+    }
     hipLaunchKernelGGL(rvcp::legacy_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                        (hipStream_t)stream, *args, tri, shade, (const rvcp_sphere_t *)spheres,
                        (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters);

@@ -89,3 +89,39 @@ def test_compiled_once_per_scene(cornell):
             rt.render(16, 16, TIME)
             assert int(rt.last_stats["kernel_variant"]) & SPEC
     assert times[1] < 0.5 * times[0] or times[0] < 0.05, times
+
+
+@pytest.mark.parametrize("W,H,spp", [(1024, 1024, 5), (97, 61, 3)])
+def test_specialised_mode2_equals_generic(W, H, spp):
+    """Mode 2 (ray_tracer.comp) with the specialised triangle scan equals the generic mode-2
+    kernel bit for bit (sphere room, 12 faces)."""
+    sc = rvcp_amd.scene.sphere_scene()
+    s = _render(sc, W, H, spp=spp, integrator=1)
+    g = _render(sc, W, H, spp=spp, integrator=1, specialize=rvcp_amd.abi.SPECIALIZE_OFF)
+    assert int(s[2]["kernel_variant"]) & SPEC and not int(g[2]["kernel_variant"]) & SPEC
+    _same(s, g)
+
+
+def test_specialised_mode2_vs_oracle():
+    sc = rvcp_amd.scene.sphere_scene()
+    kw = dict(spp=2, integrator=1)
+    W, H = 80, 64
+    s = _render(sc, W, H, **kw)
+    assert int(s[2]["kernel_variant"]) & SPEC
+    cfg = rvcp_amd.abi.make_config(**kw)
+    o_lin, o_rgba, o_trav = O.render(scene_arrays(sc), sc.push_constant(TIME), cfg, W, H)
+    assert np.array_equal(s[1].view(np.uint32), o_lin.view(np.uint32))
+    assert np.array_equal(s[0], o_rgba)
+    assert int(s[2]["traversals"]) == int(o_trav)
+
+
+def test_specialised_mode2_t_min_zero_vs_oracle():
+    """Secondary rays with t_min = 0: the specialised mode-2 kernel's per-wave guard takes the
+    generic scan (and the IEEE sphere roots) for them."""
+    sc = rvcp_amd.scene.sphere_scene()
+    kw = dict(spp=2, integrator=1, ray_t_min=0.0)
+    s = _render(sc, 48, 40, **kw)
+    cfg = rvcp_amd.abi.make_config(**kw)
+    o_lin, o_rgba, o_trav = O.render(scene_arrays(sc), sc.push_constant(TIME), cfg, 48, 40)
+    assert np.array_equal(s[1].view(np.uint32), o_lin.view(np.uint32))
+    assert np.array_equal(s[0], o_rgba)

@@ -211,3 +211,24 @@ def test_hiprtc_compiles_specialised_module():
         pytest.skip("hipRTC not installed")
     assert rc == 0, err.value.decode()
     assert size.value > 10000
+
+
+def test_hiprtc_compiles_specialised_mode2_module():
+    """The mode-2 (ray_tracer.comp) kernel with the specialised triangle scan, compiled for the
+    sphere room's 12 faces (RVCP_JIT_LEGACY)."""
+    L = rvcp_amd.abi.load()
+    fn = L.rvcp_internal_jit_compile_check_mode
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t),
+                   ctypes.c_char_p, ctypes.c_size_t]
+    sc = rvcp_amd.scene.sphere_scene()
+    verts = sc.mesh.aligned_vertices()["position"][:, :3]
+    faces = sc.mesh.aligned_faces()["vertices"]
+    rec = _tri_records(verts[faces].astype(np.float32))
+    size = ctypes.c_size_t(0)
+    err = ctypes.create_string_buffer(4096)
+    rc = fn(rec.ctypes.data, len(rec), 1, ctypes.byref(size), err, 4096)
+    if rc != 0 and b"libhiprtc not found" in err.value:
+        pytest.skip("hipRTC not installed")
+    assert rc == 0, err.value.decode()
+    assert size.value > 10000
