@@ -160,3 +160,8 @@ def test_stats_report_schedule(cornell):
         assert int(rt.last_stats["kernel_variant"]) == 3
         rt.render(1024, 512, TIME)
         assert int(rt.last_stats["kernel_variant"]) == 4
+    with rvcp_amd.RayTracer(spp=2, integrator=1) as rt:                         # mode 2
+        rt.upload_scene(rvcp_amd.scene.sphere_scene())
+        rt.render(64, 64, TIME)
+        v = int(rt.last_stats["kernel_variant"])
+        assert v == 8 | spec and rvcp_amd.abi.KERNEL_NAMES[v] == "rvcp_spec_legacy_kernel"
