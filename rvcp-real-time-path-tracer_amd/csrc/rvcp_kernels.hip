@@ -1122,6 +1122,9 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_TILED_MIN_WAVES
 #define RVCP_TILED_MIN_WAVES 4
 #endif
+#ifndef RVCP_TILED_PAIR
+#define RVCP_TILED_PAIR 1
+#endif
 // The variant-3 path kernel runs 5 waves per SIMD: 95 VGPRs without spills once the scan loop
 // is not unrolled and the pixel's surface record is re-read per sample instead of held in
 // registers (C3 5.93 -> 5.73 ms, C4 44.2 -> 41.3 ms, C2 unchanged, over 105 VGPRs / 4 waves;
@@ -1368,7 +1371,47 @@ __device__ __forceinline__ void path_body(
                     // Two-stage exact test: stage 2 (1/den, t, b1, b2, the
                     // compares) only when some lane may accept.  (A software-pipelined read of
                     // the next triangle costs 12 VGPRs and was slower at 4 waves/SIMD.)
+#if RVCP_TILED_PAIR
+                    // Two triangles per step: the first pretest halves of both (slots A and B)
+                    // are four independent chains issued together; their results stay live
+                    // and the gates then run per triangle, in index order.
+                    uint32_t i = 0;
+                    for (; i + 1 < n; i += 2) {
+                        const TriRecord Tp[2] = {tile[i], tile[i + 1]};
+                        TriPartA Pa[2], Pb[2];
+                        uint64_t ga[2], gb[2] = {0ull, 0ull};
+#pragma unroll
+                        for (uint32_t h = 0; h < 2; ++h) {
+                            Pa[h] = tri_stage1a(Tp[h], s_ao, s_ad);
+                            ga[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pa[h])) & mA;
+                            if (!SINGLE) {
+                                Pb[h] = tri_stage1a(Tp[h], b_o, b_d);
+                                gb[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pb[h])) & mB;
+                            }
+                        }
+#pragma unroll
+                        for (uint32_t h = 0; h < 2; ++h) {
+                            const TriRecord &T = Tp[h];
+                            if (ga[h] != 0ull) {
+                                const TriPart PA = tri_stage1b(T, Pa[h], s_ad);
+                                if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PA.n2) <= Pa[h].m) & ga[h]) != 0ull) {
+                                    float tA;
+                                    if (tri_stage2(T, PA, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i + h); }
+                                }
+                            }
+                            if (!SINGLE && gb[h] != 0ull) {
+                                const TriPart PB = tri_stage1b(T, Pb[h], b_d);
+                                if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PB.n2) <= Pb[h].m) & gb[h]) != 0ull) {
+                                    float tB;
+                                    if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i + h); }
+                                }
+                            }
+                        }
+                    }
+                    for (; i < n; ++i) {          // the odd last triangle of a tile
+#else
                     for (uint32_t i = 0; i < n; ++i) {
+#endif
                         const TriRecord T = tile[i];
 #if RVCP_SPLIT_PRETEST
                         // the gates are lane masks ANDed in scalar registers (ballot of one
