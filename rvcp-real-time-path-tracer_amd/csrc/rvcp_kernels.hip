@@ -1125,6 +1125,9 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_TILED_PAIR
 #define RVCP_TILED_PAIR 1
 #endif
+#ifndef RVCP_TILED_STEP1
+#define RVCP_TILED_STEP1 2
+#endif
 // The variant-3 path kernel runs 5 waves per SIMD: 95 VGPRs without spills once the scan loop
 // is not unrolled and the pixel's surface record is re-read per sample instead of held in
 // registers (C3 5.93 -> 5.73 ms, C4 44.2 -> 41.3 ms, C2 unchanged, over 105 VGPRs / 4 waves;
@@ -1375,13 +1378,17 @@ __device__ __forceinline__ void path_body(
                     // Two triangles per step: the first pretest halves of both (slots A and B)
                     // are four independent chains issued together; their results stay live
                     // and the gates then run per triangle, in index order.
+                    // (SINGLE scans one slot: RVCP_TILED_STEP1 triangles per step, same form)
+                    constexpr uint32_t kStep = SINGLE ? RVCP_TILED_STEP1 : 2u;
                     uint32_t i = 0;
-                    for (; i + 1 < n; i += 2) {
-                        const TriRecord Tp[2] = {tile[i], tile[i + 1]};
-                        TriPartA Pa[2], Pb[2];
-                        uint64_t ga[2], gb[2] = {0ull, 0ull};
+                    for (; i + kStep <= n; i += kStep) {
+                        TriRecord Tp[kStep];
+                        TriPartA Pa[kStep], Pb[kStep];
+                        uint64_t ga[kStep], gb[kStep];
 #pragma unroll
-                        for (uint32_t h = 0; h < 2; ++h) {
+                        for (uint32_t h = 0; h < kStep; ++h) { Tp[h] = tile[i + h]; gb[h] = 0ull; }
+#pragma unroll
+                        for (uint32_t h = 0; h < kStep; ++h) {
                             Pa[h] = tri_stage1a(Tp[h], s_ao, s_ad);
                             ga[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pa[h])) & mA;
                             if (!SINGLE) {
@@ -1390,7 +1397,7 @@ __device__ __forceinline__ void path_body(
                             }
                         }
 #pragma unroll
-                        for (uint32_t h = 0; h < 2; ++h) {
+                        for (uint32_t h = 0; h < kStep; ++h) {
                             const TriRecord &T = Tp[h];
                             if (ga[h] != 0ull) {
                                 const TriPart PA = tri_stage1b(T, Pa[h], s_ad);
@@ -1408,7 +1415,7 @@ __device__ __forceinline__ void path_body(
                             }
                         }
                     }
-                    for (; i < n; ++i) {          // the odd last triangle of a tile
+                    for (; i < n; ++i) {          // the last triangles of a tile
 #else
                     for (uint32_t i = 0; i < n; ++i) {
 #endif
