@@ -23,6 +23,8 @@ Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
   c5: Cornell + 100k random triangles, 1024x1024 SPP=30.
   spheres: integrator mode 2 (ray_tracer.comp) on the deprecated host's sphere room,
       1024x1024 at its SPP=5 (not a BASELINE config; reported for coverage).
+  c3m2: the C3 frame (Cornell 1024x1024 SPP=30) through integrator mode 2 (ray_tracer.comp,
+      the shader north_star names) instead of the games101 branch the current host binds.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the path-tracing kernel,
 >99% of the frame's GPU time), whose bound is FP32 VALU issue: `achieved` =
@@ -79,7 +81,10 @@ def workload(name, n_gpus):
                     extra_tris=100000, scaling="strong")
     if name == "spheres":
         return dict(workload="spheres_mode2_1024sq_spp5", W=1024, H=1024, spp=5, extra_tris=0,
-                    scaling="strong", integrator=1)
+                    scaling="strong", integrator=1, scene="spheres")
+    if name == "c3m2":
+        return dict(workload="cornell_mode2_1024sq_spp30", W=1024, H=1024, spp=30, extra_tris=0,
+                    scaling="strong", integrator=1, scene="cornell")
     raise SystemExit(f"unknown workload {name}")
 
 
@@ -197,7 +202,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "spheres"],
+    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "spheres", "c3m2"],
                     help="default: c3 at N=1 (headline), c4 at N>1 (BASELINE's 8-GPU config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -238,7 +243,7 @@ def main():
     wl = workload(wname, world)
     W, H, spp = wl["W"], wl["H"], wl["spp"]
     legacy = wl.get("integrator", 0) == 1
-    sc = rvcp_amd.scene.sphere_scene() if legacy else rvcp_amd.Scene.default()
+    sc = rvcp_amd.scene.sphere_scene() if wl.get("scene") == "spheres" else rvcp_amd.Scene.default()
     if wl["extra_tris"]:
         sc = rvcp_amd.scene.with_random_triangles(sc, wl["extra_tris"])
     cfg_kw = dict(spp=spp, device=local_rank)
@@ -416,6 +421,8 @@ def main():
                             if world == 1 and wname in REFERENCE_MSAMPLES else None),
             "dtype": "f32",
             "data": ("synthetic (the reference's deprecated sphere-room scene, integrator mode 2, "
+                     "fixed time seed 123.0)" if wl.get("scene") == "spheres" else
+                     "synthetic (the reference's built-in Cornell box scene, integrator mode 2, "
                      "fixed time seed 123.0)" if legacy else
                      "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)"),
             "config": {"workload": wl["workload"], "width": W, "height": H, "spp": spp,

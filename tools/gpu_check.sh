@@ -70,6 +70,7 @@ for s in $STEPS; do
         benchc5) run bench_c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
         benchc4) run bench_c4 300 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         c5pmcall) run c5pmcall 900 bash tools/c5_pmc.sh ;;
+        benchc3m2) run bench_c3m2 300 python bench.py --workload c3m2 --steps 10 --warmup 2 --no-cpu-baseline ;;
         benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 ;;
         profs) run profs 600 rocprofv3 --kernel-trace --stats -d "$OUT/profs_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 20 --warmup 2 --no-cpu-baseline ;;
         abi) run pytest_abi 300 python -u -m pytest tests/test_gpu_abi.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
