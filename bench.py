@@ -260,6 +260,25 @@ def main():
     # C2 0.59/0.32/0.27/0.33 ms -- a small frame is mostly tail, so it gains from a third)
     auto_fif = 3 if (W * spp * rvcp_amd.shard_rows(H, rank, world)) < (4 << 20) else 2
     fif = 1 if rehearsal else (args.frames_in_flight or auto_fif)
+    # RCCL communicator ids (one per context), made on rank 0 and shared over the control
+    # plane.  If rank 0 cannot make them (no usable librccl) every rank learns it from the
+    # broadcast and the frame is gathered through host memory over gloo instead, labelled as
+    # such in the JSON line ("gather"), so that a scaling run still yields a measured line.
+    rccl_ids, rccl_error = None, None
+    if world > 1 and not rehearsal:
+        got = [None]
+        if rank == 0:
+            try:
+                got = [[rvcp_amd.rccl_unique_id() for _ in range(fif)]]
+            except Exception as e:          # noqa: BLE001 -- reported in the JSON line
+                got = [repr(e)]
+        dist.broadcast_object_list(got, src=0)
+        if isinstance(got[0], list):
+            rccl_ids = got[0]
+        else:
+            rccl_error = got[0]
+            fif = 1
+    host_gather = rehearsal or rccl_error is not None
     rts = [rvcp_amd.RayTracer(**cfg_kw) for _ in range(fif)]
     t_up = time.perf_counter()
     rts[0].upload_scene(sc)              # includes the scene-specialised compile (§4.7)
@@ -270,11 +289,9 @@ def main():
     push = sc.push_constant(123.0)
     n_faces = len(sc.mesh.aligned_faces())
     n_spheres = len(sc.spheres) if legacy else 0
-    if world > 1 and not rehearsal:
-        for r in rts:                    # one communicator per context, created in order
-            uid = [rvcp_amd.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            r.rccl_init(uid[0], world, rank)
+    if rccl_ids is not None:
+        for r, uid in zip(rts, rccl_ids):    # one communicator per context, created in order
+            r.rccl_init(uid, world, rank)
 
     rows = rvcp_amd.shard_rows(H, rank, world)
     slot = rvcp_amd.shard_rows(H, 0, world)          # shard 0 has the most rows
@@ -294,7 +311,7 @@ def main():
             r.render_shard_async(push, W, H, 0, 1, frame.data_ptr())
             return
         r.render_shard_async(push, W, H, rank, world, shard_buf.data_ptr())
-        if rehearsal:
+        if host_gather:
             return
         # RCCL gather + device assembly, enqueued behind the render without a host sync
         r.gather_frame_async(shard_buf.data_ptr(), W, H,
@@ -305,7 +322,7 @@ def main():
         """Wait for context i's frame; return its stats."""
         st = rts[i].sync_stats()
         pending[i] = False
-        if rehearsal:      # gloo gather through host memory (one GPU, all ranks on it)
+        if host_gather:    # gloo gather through host memory (rehearsal / no usable RCCL)
             got = rvcp_amd.frame.gather_shards(shard_bufs[i].cpu(), rank, world, dst=0)
             if rank == 0:
                 gat_flats[i].copy_(torch.stack(got))
@@ -433,6 +450,8 @@ def main():
                        "upload_s": round(upload_s, 3),
                        "frames_in_flight": fif,
                        "gather": ("gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
+                                  f"gloo through host memory (RCCL unavailable: {rccl_error})"
+                                  if rccl_error is not None else
                                   "rccl ncclGather via rvcp_gather_frame_async") if world > 1 else "none"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 2),
                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
