@@ -4,10 +4,11 @@
   valu_busy = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction occupies a SIMD for two
               cycles on CDNA4, MI355X_MICROARCH.md) / (GRBM_GUI_ACTIVE per XCD x SIMDs)
 
-  issue_frac = (SQ_INSTS_VALU / (cycles x SIMDs)) / 0.35, the wave-instructions per SIMD per
-              clock the chip sustains on independent v_fma_f32 / v_add_f32 streams with every
-              SIMD full (tools/valu_rate.hip, profiles/r01_valu_rate.log): how close the kernel
-              is to the VALU issue rate actually reachable
+  issue_frac = (SQ_INSTS_VALU / (cycles x SIMDs)) / 0.3888, the wave-instructions per SIMD
+              per GRBM clock the chip sustains on independent v_fma_f32 streams with every SIMD
+              full, measured in the same clock (tools/valu_rate.hip under the same PMC pass,
+              profiles/r02_valu_rate_pmc.txt): how close the kernel is to the
+              VALU issue rate actually reachable
 
 GRBM_GUI_ACTIVE is summed over the 8 XCDs by rocprofv3, so it is divided by 8 to get the
 kernel's cycles.  Writes the JSON bench.py reads into roofline.valu_busy_pmc /
@@ -39,7 +40,7 @@ def main():
     ap.add_argument("--workload", required=True)
     ap.add_argument("--simds", type=int, default=1024)
     ap.add_argument("--xcds", type=int, default=8)
-    ap.add_argument("--issue-peak", type=float, default=0.35)
+    ap.add_argument("--issue-peak", type=float, default=0.3888)
     a = ap.parse_args()
     valu = per_kernel(a.sq_csv, "SQ_INSTS_VALU")
     grbm = per_kernel(a.grbm_csv, "GRBM_GUI_ACTIVE")
