@@ -211,7 +211,8 @@ def main():
     ap.add_argument("--save-frame", default="")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="contexts rendering consecutive frames concurrently (1 = one frame "
-                         "at a time; 0 = auto: 3 below 4 Msamples per rank-frame, else 2; "
+                         "at a time; 0 = auto: 3 below 4 Msamples per rank-frame or in "
+                         "integrator mode 2, else 2; "
                          "N>1 rehearsals always use 1)")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
@@ -258,7 +259,9 @@ def main():
     # frame its context rendered fif steps earlier.
     # (measured, profiles/r02_fif_sweep.log: C3 1/2/3/4 in flight 4.35/3.83/3.83/3.95 ms,
     # C2 0.59/0.32/0.27/0.33 ms -- a small frame is mostly tail, so it gains from a third)
-    auto_fif = 3 if (W * spp * rvcp_amd.shard_rows(H, rank, world)) < (4 << 20) else 2
+    # (mode 2 -- one kernel per frame, no pre-pass -- gains from a third frame at every size:
+    # C3 frame 2.84/2.40/2.29/2.46 ms for 1/2/3/4 in flight, profiles/r02_m2_fif_sweep.log)
+    auto_fif = 3 if (legacy or W * spp * rvcp_amd.shard_rows(H, rank, world) < (4 << 20)) else 2
     fif = 1 if rehearsal else (args.frames_in_flight or auto_fif)
     # RCCL communicator ids (one per context), made on rank 0 and shared over the control
     # plane.  If rank 0 cannot make them (no usable librccl) every rank learns it from the
