@@ -285,11 +285,11 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
         return -1;
     }
     // the flags of the static build (Makefile): the numeric contract depends on them
-    std::vector<std::string> extra;            // RVCP_JIT_FLAGS: experiment -D options
-    if (const char *e = std::getenv("RVCP_JIT_FLAGS")) {
+    std::vector<std::string> extra;            // RVCP_JIT_FLAGS: experiment options,
+    if (const char *e = std::getenv("RVCP_JIT_FLAGS")) {   // separated by spaces or commas
         std::string cur;
         for (const char *c = e;; c++) {
-            if (*c == ' ' || *c == '\0') {
+            if (*c == ' ' || *c == ',' || *c == '\0') {
                 if (!cur.empty()) extra.push_back(cur);
                 cur.clear();
                 if (!*c) break;
