@@ -2094,7 +2094,10 @@ __device__ __forceinline__ void legacy_body(
 }
 
 #ifndef RVCP_JIT
-__global__ __launch_bounds__(kBlock) void legacy_kernel(
+#ifndef RVCP_LEGACY_MIN_WAVES
+#define RVCP_LEGACY_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void legacy_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
@@ -2105,7 +2108,10 @@ __global__ __launch_bounds__(kBlock) void legacy_kernel(
 }
 #else
 // mode 2 with the scene-specialised triangle scan (rvcp_jit.cpp, RVCP_JIT_LEGACY)
-extern "C" __global__ __launch_bounds__(kBlock) void rvcp_spec_legacy_kernel(
+#ifndef RVCP_LEGACY_MIN_WAVES
+#define RVCP_LEGACY_MIN_WAVES 1
+#endif
+extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp_spec_legacy_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
