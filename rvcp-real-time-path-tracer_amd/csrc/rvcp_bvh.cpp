@@ -288,4 +288,51 @@ int bvh4_collapse(const std::vector<BvhNode> &nodes, int32_t root, std::vector<B
     return need;
 }
 
+// Byte quantisation of the 4-wide nodes (Bvh4QNode).  Per node and axis: origin = the
+// smallest child lo (a float), scale = the smallest power of two (>= 2^-60) with
+// (largest child hi - origin) / scale <= 255, q_lo = floor((lo - origin) / scale),
+// q_hi = ceil((hi - origin) / scale), evaluated in double, where both are exact (scale is a
+// power of two and the operands floats).  So origin + q_lo * scale <= lo and
+// origin + q_hi * scale >= hi in exact arithmetic: every quantised box contains its float box,
+// which already carries the build's enlargement (far above the few-ulp rounding of the
+// kernel's decode), so the traversal culls nothing the float boxes keep.
+void bvh4_quantize(const std::vector<Bvh4Node> &in, std::vector<Bvh4QNode> &out)
+{
+    out.resize(in.size());
+    for (size_t j = 0; j < in.size(); j++) {
+        const Bvh4Node &N = in[j];
+        Bvh4QNode &Q = out[j];
+        for (int k = 0; k < 3; k++) {
+            float lo = 0.0f, hi = 0.0f;
+            bool any = false;
+            for (int c = 0; c < 4; c++) {
+                if (N.ref[c] == ~0) continue;
+                lo = any ? std::min(lo, N.lo[k][c]) : N.lo[k][c];
+                hi = any ? std::max(hi, N.hi[k][c]) : N.hi[k][c];
+                any = true;
+            }
+            const double ext = any ? (double)hi - (double)lo : 0.0;
+            int e = -60;
+            while (std::ldexp(255.0, e) < ext) e++;
+            const double sc = std::ldexp(1.0, e);
+            Q.origin[k] = lo;
+            Q.scale[k] = (float)sc;
+            uint32_t wl = 0, wh = 0;
+            for (int c = 0; c < 4; c++) {
+                uint32_t ql = 255, qh = 0;                     // unused: inverted, never entered
+                if (N.ref[c] != ~0) {
+                    ql = (uint32_t)std::floor(((double)N.lo[k][c] - (double)lo) / sc);
+                    qh = (uint32_t)std::ceil(((double)N.hi[k][c] - (double)lo) / sc);
+                    if (qh > 255) qh = 255;                    // cannot happen: ext / sc <= 255
+                }
+                wl |= ql << (8 * c);
+                wh |= qh << (8 * c);
+            }
+            Q.qlo[k] = wl;
+            Q.qhi[k] = wh;
+        }
+        for (int c = 0; c < 4; c++) Q.ref[c] = N.ref[c];
+    }
+}
+
 }  // namespace rvcp

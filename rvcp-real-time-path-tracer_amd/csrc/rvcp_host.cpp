@@ -51,6 +51,7 @@ struct rvcp_ctx {
     Bvh4Node *d_bvh_nodes = nullptr;
     TriRecord *d_bvh_tris = nullptr;
     int32_t bvh_root = 0;
+    uint32_t bvh_n4 = 0;
     int bvh_depth = 0;
     float *d_gamma = nullptr;
     float *d_unorm = nullptr;
@@ -519,6 +520,13 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         int32_t root4 = 0;
         if (bvh4_collapse(nodes, root, nodes4, root4) > kBvhStack)
             return fail(ctx, RVCP_E_UNSUPPORTED, "BVH traversal stack bound exceeded");
+        // the Bvh4QNode copy rides behind the nodes in the same buffer (FrameArgs::bvh_n4)
+        std::vector<Bvh4QNode> q4;
+        bvh4_quantize(nodes4, q4);
+        const size_t n4 = nodes4.size();
+        nodes4.resize(n4 + (q4.size() + 1) / 2);
+        if (!q4.empty()) std::memcpy(static_cast<void *>(nodes4.data() + n4), q4.data(), q4.size() * sizeof(Bvh4QNode));
+        ctx->bvh_n4 = (uint32_t)n4;
         if ((rc = dev_upload<Bvh4Node>(ctx, &ctx->d_bvh_nodes, nodes4.data(), nodes4.size())) ||
             (rc = dev_upload<TriRecord>(ctx, &ctx->d_bvh_tris, btri.data(), btri.size())))
             return rc;
@@ -620,6 +628,7 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     A.accel = (ctx->cfg.accel == RVCP_ACCEL_BVH && ctx->n_faces > 0) ? RVCP_ACCEL_BVH : RVCP_ACCEL_NONE;
     if (A.accel == RVCP_ACCEL_BVH) A.variant = 3;    // the BVH traversal lives in the v3 kernels
     A.bvh_root = ctx->bvh_root;
+    A.bvh_n4 = ctx->bvh_n4;
     const bool legacy = ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY;
     A.n_spheres = legacy ? ctx->n_spheres : 0u;
 

@@ -342,17 +342,57 @@ __device__ __forceinline__ void bvh4_cas(float &ka, int32_t &ca, float &kb, int3
     ca = c;
 }
 
+// RVCP_BVH_QUANT: traverse the byte-quantised copy of the nodes (Bvh4QNode, four 16-B loads
+// per step instead of seven).  Each child bound is decoded straight into slab time,
+// t = q * (scale * inv) + (origin - o) * inv, with the near and far bytes chosen by the sign of
+// the ray's inverse direction (the ordered slab test: an inverted unused child is never
+// entered); the roundings of that form are relative errors of a few ulp of t, far below the
+// build's box enlargement, and a NaN from it only widens a slab, so nothing a float box keeps
+// is culled.
+#ifndef RVCP_BVH_QUANT
+#define RVCP_BVH_QUANT 1
+#endif
+__device__ __forceinline__ float ubyte_f(uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xFFu); }
+
 template <bool LDS>
 __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
                                          const TriRecord *__restrict__ btri, int32_t root,
                                          lds_i32 *stk, f3 o, f3 d, float tmin, float &bt,
-                                         int &best) {
+                                         int &best, uint32_t n4 = 0) {
     const f3 inv = slab_inv(d);
     int32_t priv[LDS ? 1 : kBvhStack];
     int sp = 0;
     int32_t ref = root;
+#if RVCP_BVH_QUANT
+    const Bvh4QNode *__restrict__ qn = reinterpret_cast<const Bvh4QNode *>(nodes + n4);
+    const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+#endif
     for (;;) {
         if (ref >= 0) {
+#if RVCP_BVH_QUANT
+            const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
+            const float4 w0 = q[0], w1 = q[1], w2 = q[2];
+            const int4 r = reinterpret_cast<const int4 *>(qn + ref)[3];
+            const float ax = w0.w * inv.x, ay = w1.x * inv.y, az = w1.y * inv.z;
+            const float bx = (w0.x - o.x) * inv.x, by = (w0.y - o.y) * inv.y, bz = (w0.z - o.z) * inv.z;
+            const uint32_t lx = __float_as_uint(w1.z), ly = __float_as_uint(w1.w), lz = __float_as_uint(w2.x);
+            const uint32_t hx = __float_as_uint(w2.y), hy = __float_as_uint(w2.z), hz = __float_as_uint(w2.w);
+            const uint32_t nx = px ? lx : hx, fx = px ? hx : lx;
+            const uint32_t ny = py ? ly : hy, fy = py ? hy : ly;
+            const uint32_t nz = pz ? lz : hz, fz = pz ? hz : lz;
+            float kk[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float tn = __builtin_fmaxf(
+                    __builtin_fmaxf(__builtin_fmaf(ubyte_f(nx, c), ax, bx), __builtin_fmaf(ubyte_f(ny, c), ay, by)),
+                    __builtin_fmaxf(__builtin_fmaf(ubyte_f(nz, c), az, bz), tmin));
+                const float tf = __builtin_fminf(
+                    __builtin_fminf(__builtin_fmaf(ubyte_f(fx, c), ax, bx), __builtin_fmaf(ubyte_f(fy, c), ay, by)),
+                    __builtin_fminf(__builtin_fmaf(ubyte_f(fz, c), az, bz), bt));
+                kk[c] = tn <= tf ? tn : __builtin_inff();
+            }
+            float k0 = kk[0], k1 = kk[1], k2 = kk[2], k3 = kk[3];
+#else
             const float4 *q = reinterpret_cast<const float4 *>(nodes + ref);
             const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
             const int4 r = reinterpret_cast<const int4 *>(nodes + ref)[6];
@@ -361,6 +401,7 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
             bvh4_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, o, inv, tmin, bt, k1);
             bvh4_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, o, inv, tmin, bt, k2);
             bvh4_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, o, inv, tmin, bt, k3);
+#endif
             int32_t c0 = r.x, c1 = r.y, c2 = r.z, c3 = r.w;
             bvh4_cas(k0, c0, k1, c1);
             bvh4_cas(k2, c2, k3, c3);
@@ -1050,7 +1091,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
         int best = -1;
         float bt = tmax;
         if (BVH) {
-            bvh_nearest<false>(bvh_nodes, bvh_tris, A.bvh_root, nullptr, o, d, tmin, bt, best);
+            bvh_nearest<false>(bvh_nodes, bvh_tris, A.bvh_root, nullptr, o, d, tmin, bt, best, A.bvh_n4);
         } else {
 #pragma unroll 2
             for (uint32_t i = 0; i < A.n_faces; ++i) {
@@ -1478,8 +1519,8 @@ __device__ __forceinline__ void path_body(
         } else if (BVH) {
             // ---- opt-in BVH: each lane traverses for its own rays ----
             lds_i32 *stk = (lds_i32 *)bvh_stack;
-            if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA);
-            if (sB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB);
+            if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA, A.bvh_n4);
+            if (sB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB, A.bvh_n4);
         } else if (tail) {
             // ---- tail: R lanes per ray, each scanning every R-th triangle ----
             // The frame queue is empty, so what is left are the serial sample chains of the

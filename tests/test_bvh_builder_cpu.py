@@ -75,3 +75,4 @@ def test_bvh4_builder_sanitized(tmp_path):
         assert r.returncode == 0, (name, r.stdout[-500:], r.stderr[-2000:])
         assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr
         assert "mismatches 0 of 200" in r.stdout, (name, r.stdout)
+        assert "quantized: violations 0" in r.stdout, (name, r.stdout)

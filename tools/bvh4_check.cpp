@@ -36,6 +36,24 @@ int main(int argc, char **argv) {
     std::vector<Bvh4Node> n4; int32_t r4;
     int need = bvh4_collapse(nodes, root, n4, r4);
     printf("n=%u nodes2=%zu depth=%d nodes4=%zu stack bound=%d\n", n, nodes.size(), depth, n4.size(), need);
+    // bvh4_quantize: every used child's decoded box (exact, in double) contains its float box,
+    // every unused child is inverted on all three axes, refs are copied
+    std::vector<Bvh4QNode> q4; bvh4_quantize(n4, q4); int qbad = 0; double grow = 0, ext = 0;
+    for (size_t j = 0; j < n4.size(); j++)
+        for (int c = 0; c < 4; c++) {
+            qbad += q4[j].ref[c] != n4[j].ref[c];
+            for (int k = 0; k < 3; k++) {
+                const uint32_t ql = (q4[j].qlo[k] >> (8 * c)) & 255, qh = (q4[j].qhi[k] >> (8 * c)) & 255;
+                const double lo = (double)q4[j].origin[k] + ql * (double)q4[j].scale[k];
+                const double hi = (double)q4[j].origin[k] + qh * (double)q4[j].scale[k];
+                if (n4[j].ref[c] == ~0) { qbad += !(ql == 255 && qh == 0); continue; }
+                qbad += !(lo <= n4[j].lo[k][c] && hi >= n4[j].hi[k][c]);
+                grow += (hi - lo) - ((double)n4[j].hi[k][c] - n4[j].lo[k][c]);
+                ext += (double)n4[j].hi[k][c] - n4[j].lo[k][c];
+            }
+        }
+    printf("quantized: violations %d, box growth %.4f of extent\n", qbad, ext > 0 ? grow / ext : 0.0);
+    if (qbad) return 1;
     std::mt19937 rng(1); std::uniform_real_distribution<float> U(0, 1);
     double steps = 0, tris = 0; int R = argc > 2 ? atoi(argv[2]) : 5000, bad = 0, maxsp = 0;
     for (int r = 0; r < R; r++) {
