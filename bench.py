@@ -211,12 +211,21 @@ def main():
     ap.add_argument("--save-frame", default="")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="contexts rendering consecutive frames concurrently (1 = one frame "
-                         "at a time; 0 = auto: 3 below 4 Msamples per rank-frame or in "
+                         "at a time; 0 = auto: 4 below 4 Msamples per rank-frame, 3 in "
                          "integrator mode 2, else 2; "
                          "N>1 rehearsals always use 1)")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
     args = ap.parse_args()
+
+    # Hardware queues per process: HIP's default is 4; with 4 frames in flight on small frames
+    # (C2) the contexts' streams then share queues and serialise.  8 queues let C2 take a fourth
+    # frame: 0.284 -> 0.269 ms (profiles/r02_hwq_fif_sweep.log).  Set before HIP initialises.
+    try:
+        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        hwq = 4
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, hwq)))
 
     import torch
     import torch.distributed as dist
@@ -261,7 +270,10 @@ def main():
     # C2 0.59/0.32/0.27/0.33 ms -- a small frame is mostly tail, so it gains from a third)
     # (mode 2 -- one kernel per frame, no pre-pass -- gains from a third frame at every size:
     # C3 frame 2.84/2.40/2.29/2.46 ms for 1/2/3/4 in flight, profiles/r02_m2_fif_sweep.log)
-    auto_fif = 3 if (legacy or W * spp * rvcp_amd.shard_rows(H, rank, world) < (4 << 20)) else 2
+    # (small frames, 8 hardware queues: C2 4 in flight 0.269 ms vs 3 in flight 0.284 ms,
+    # profiles/r02_hwq_fif_sweep.log; C3 2 and 3 equal)
+    rank_samples = W * spp * rvcp_amd.shard_rows(H, rank, world)
+    auto_fif = 4 if rank_samples < (4 << 20) else (3 if legacy else 2)
     fif = 1 if rehearsal else (args.frames_in_flight or auto_fif)
     # RCCL communicator ids (one per context), made on rank 0 and shared over the control
     # plane.  If rank 0 cannot make them (no usable librccl) every rank learns it from the
