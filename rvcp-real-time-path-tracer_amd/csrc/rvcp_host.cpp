@@ -539,7 +539,8 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     if (ctx->cfg.specialize == RVCP_SPECIALIZE_AUTO && ctx->cfg.accel == RVCP_ACCEL_NONE &&
         n_faces >= 1 && n_faces <= kJitMaxFaces && !std::getenv("RVCP_NO_SPECIALIZE")) {
         ctx->jit = jit_path_kernels(ctx->device, tri.data(), n_faces, ctx->jit_err,
-                                    ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY);
+                                    ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY,
+                                    n_spheres == 0);
         HIP_TRY(ctx, hipSetDevice(ctx->device));
     }
     ctx->n_faces = n_faces;

@@ -270,7 +270,7 @@ JitKernels::~JitKernels()
 }
 
 int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
-                     bool legacy)
+                     bool legacy, int legacy_waves)
 {
     const RtcApi &api = rtc();
     if (!api.ok) {
@@ -303,6 +303,8 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
                                       "-fno-fast-math", "-fno-slp-vectorize", "-DRVCP_JIT",
                                       "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
     if (legacy) opts.push_back("-DRVCP_JIT_LEGACY");
+    const std::string lw = "-DRVCP_LEGACY_MIN_WAVES=" + std::to_string(legacy_waves);
+    if (legacy && legacy_waves > 0) opts.push_back(lw.c_str());
     for (const std::string &x : extra) opts.push_back(x.c_str());
     const int rc = api.compile(prog, (int)opts.size(), opts.data());
     if (rc != 0) {
@@ -323,9 +325,15 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
 }
 
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
-                                             std::string &err, bool legacy)
+                                             std::string &err, bool legacy, bool sphereless)
 {
-    const std::string scan = jit_scan_source(tri, n) + (legacy ? "// +legacy\n" : "");
+    // Mode 2 on a scene without spheres (the Cornell frame): 6 waves per SIMD measured 2.5 %
+    // faster than 5, with spheres 5 % slower (profiles/r02_legacy_waves_ab.log).
+    // RVCP_JIT_LEGACY_WAVES overrides (experiments; 0 = the compiler's choice).
+    int legacy_waves = legacy && sphereless ? 6 : 0;
+    if (const char *e = std::getenv("RVCP_JIT_LEGACY_WAVES")) legacy_waves = std::atoi(e);
+    const std::string scan = jit_scan_source(tri, n) +
+        (legacy ? "// +legacy " + std::to_string(legacy_waves) + "\n" : std::string());
     const uint64_t h = fnv1a(scan);
     std::lock_guard<std::mutex> lock(g_mu);
     for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
@@ -335,7 +343,7 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         }
     }
     std::vector<char> code;
-    if (jit_compile_code(scan, code, err, legacy) != 0) return nullptr;
+    if (jit_compile_code(scan, code, err, legacy, legacy_waves) != 0) return nullptr;
     auto k = std::make_shared<JitKernels>();
     k->device = device;
     if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&k->module, code.data()) != hipSuccess) {

@@ -30,10 +30,12 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n);
 // Compile rvcp_kernels.hip with the given scan for gfx950 (hipRTC); 0 or -1 with err set.
 // `legacy` also builds the mode-2 kernel (RVCP_JIT_LEGACY).
 int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
-                     bool legacy = false);
+                     bool legacy = false, int legacy_waves = 0);
 // Compiled + loaded kernels for the scene on `device` (process-wide cache keyed by the scan
 // source and `legacy`); nullptr with err set when hipRTC is unavailable or compilation fails.
+// `sphereless`: the mode-2 kernel is built for 6 waves per SIMD.
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
-                                             std::string &err, bool legacy = false);
+                                             std::string &err, bool legacy = false,
+                                             bool sphereless = false);
 
 }  // namespace rvcp

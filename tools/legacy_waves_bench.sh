@@ -1,0 +1,13 @@
+#!/usr/bin/env bash
+# Mode 2 on the C3 frame (bench.py --workload c3m2, frames in flight as the bench picks them):
+# the sphereless 6-wave build (default) vs the compiler's choice (RVCP_JIT_LEGACY_WAVES=0),
+# interleaved repetitions on one box.
+set -e
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+for rep in 1 2 3; do
+  for w in default 0; do
+    if [ $w = default ]; then env_kv=""; else env_kv="RVCP_JIT_LEGACY_WAVES=$w"; fi
+    env $env_kv timeout -k 10 120 python bench.py --workload c3m2 --steps 40 --warmup 4 --no-cpu-baseline > /tmp/lw.log 2>&1
+    python3 -c "import json; d=json.loads(open('/tmp/lw.log').read().strip().splitlines()[-1]); print('rep=$rep waves=$w', d['value'], d['ms_per_step'])"
+  done
+done
