@@ -1163,6 +1163,9 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #ifndef RVCP_TILED_MIN_WAVES
 #define RVCP_TILED_MIN_WAVES 4
 #endif
+// RVCP_TILED_PAIR: the tiled scans issue the first pretest halves of two triangles together
+// (ILP for the latency-bound per-triangle chain; C5 -5 %).  RVCP_TILED_STEP1:
+// triangles per step of the one-slot schedule 5 (3 and 4 measured equal to 2).
 #ifndef RVCP_TILED_PAIR
 #define RVCP_TILED_PAIR 1
 #endif
