@@ -54,6 +54,45 @@ def test_bvh_moved_camera(cornell):
     _same(rvcp_amd.scene.with_random_triangles(base, 300), 64, 64, spp=2, time=1.5)
 
 
+def _translated(sc, off):
+    """The scene and its camera moved by `off` (float32): the quantised nodes' origins and
+    power-of-two scales then sit far from the coordinate origin."""
+    off = np.asarray(off, np.float32)
+    v = sc.mesh.aligned_vertices().copy()
+    v["position"][:, :3] = (v["position"][:, :3] + off).astype(np.float32)
+    cam = sc.camera
+    look = (cam.position + cam.forward * np.float32(100.0)).astype(np.float32)
+    c2 = rvcp_amd.Camera.new((cam.position + off).astype(np.float32), (look + off).astype(np.float32),
+                             cam.t_near, cam.t_far, cam.vertical_fov, cam.move_speed,
+                             cam.rotate_speed)
+    return rvcp_amd.Scene(c2, sc.materials, [], rvcp_amd.scene.ArrayMesh(v, sc.mesh.aligned_faces()))
+
+
+def test_bvh_far_from_origin(cornell):
+    """Byte-quantised nodes with the scene 3e4..5e4 units from the origin."""
+    sc = _translated(rvcp_amd.scene.with_random_triangles(cornell, 500), [3.0e4, -2.0e4, 5.0e4])
+    _same(sc, 48, 40, spp=2)
+
+
+def test_bvh_flat_mesh(cornell):
+    """Many triangles in one plane (zero extent on an axis before the build's enlargement)."""
+    rng = np.random.default_rng(7)
+    n = 400
+    c = np.stack([rng.uniform(-250, 250, n), np.full(n, 1.0), rng.uniform(-250, 250, n)], 1)
+    d = rng.uniform(-8, 8, (n, 3, 3))
+    d[:, :, 1] = 0.0
+    p = (c[:, None, :] + d).astype(np.float32)
+    bv = cornell.mesh.aligned_vertices()
+    bf = cornell.mesh.aligned_faces()
+    nv = np.zeros(3 * n, dtype=bv.dtype)
+    nv["position"][:, :3] = p.reshape(-1, 3)
+    nv["normal"][:, :3] = np.array([0.0, 1.0, 0.0], np.float32)
+    nf = np.zeros(n, dtype=bf.dtype)
+    nf["vertices"] = len(bv) + np.arange(3 * n, dtype=np.uint32).reshape(n, 3)
+    mesh = rvcp_amd.scene.ArrayMesh(np.concatenate([bv, nv]), np.concatenate([bf, nf]))
+    _same(rvcp_amd.Scene(cornell.camera, cornell.materials, [], mesh), 48, 40, spp=2)
+
+
 def test_bvh_obj_and_params(cornell):
     _same(cornell, 40, 40, spp=3, max_bounces=4, rr_probability=0.5, lum_id_std140_quirk=0)
 
