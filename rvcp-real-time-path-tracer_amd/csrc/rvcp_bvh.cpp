@@ -73,6 +73,9 @@ struct Builder {
     }
 
     int32_t leaf(uint32_t first, uint32_t count) {
+        // leaves start at even slots: the packed 10-float leaf records (rvcp_host.cpp) are then
+        // 16-B aligned; the padding slot holds kBvhPadId and is never inside a leaf's range
+        if (order.size() & 1u) order.push_back(kBvhPadId);
         const uint32_t start = (uint32_t)order.size();
         for (uint32_t i = first; i < first + count; i++) order.push_back(prims[i].id);
         return ~(int32_t)((start << 5) | (count - 1));

@@ -52,6 +52,7 @@ struct rvcp_ctx {
     TriRecord *d_bvh_tris = nullptr;
     int32_t bvh_root = 0;
     uint32_t bvh_n4 = 0;
+    uint32_t bvh_slots = 0;
     int bvh_depth = 0;
     float *d_gamma = nullptr;
     float *d_unorm = nullptr;
@@ -511,11 +512,19 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         const int depth = bvh_build(reinterpret_cast<const float (*)[3][3]>(pos.data()), n_faces,
                                     nodes, order, root);
         if (depth >= kBvhStack) return fail(ctx, RVCP_E_UNSUPPORTED, "BVH deeper than the traversal stack");
-        std::vector<TriRecord> btri(order.size());
-        for (size_t j = 0; j < order.size(); j++) {       // leaf order, face id in pad[0]
+        // leaf order, face id in pad[0]; behind the S TriRecords the same slots packed as 10
+        // floats (v0, e1, e2, face id bits) -- what the traversal reads (bvh_leaf)
+        const size_t S = order.size();
+        std::vector<TriRecord> btri(S + (10 * S * 4 + sizeof(TriRecord) - 1) / sizeof(TriRecord));
+        float *packed = reinterpret_cast<float *>(btri.data() + S);
+        for (size_t j = 0; j < S; j++) {
+            if (order[j] == kBvhPadId) { btri[j] = TriRecord{}; continue; }
             btri[j] = tri[order[j]];
             std::memcpy(&btri[j].pad[0], &order[j], 4);
+            std::memcpy(packed + 10 * j, &btri[j], 9 * sizeof(float));
+            std::memcpy(packed + 10 * j + 9, &order[j], 4);
         }
+        ctx->bvh_slots = (uint32_t)S;
         std::vector<Bvh4Node> nodes4;
         int32_t root4 = 0;
         if (bvh4_collapse(nodes, root, nodes4, root4) > kBvhStack)
@@ -630,6 +639,7 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     if (A.accel == RVCP_ACCEL_BVH) A.variant = 3;    // the BVH traversal lives in the v3 kernels
     A.bvh_root = ctx->bvh_root;
     A.bvh_n4 = ctx->bvh_n4;
+    A.bvh_slots = ctx->bvh_slots;
     const bool legacy = ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY;
     A.n_spheres = legacy ? ctx->n_spheres : 0u;
 

@@ -135,6 +135,7 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
 constexpr int kBvhLeafMax = 4;
+constexpr uint32_t kBvhPadId = 0xFFFFFFFFu;   // padding slot of the leaf order (even leaf starts)
 constexpr int kBvhStack = 32;           // traversal stack entries per lane
 
 // The traversed tree: up to 4 children per node, boxes stored per axis so one node is seven
@@ -192,6 +193,7 @@ struct FrameArgs {
     int32_t accel;           // RVCP_ACCEL_*
     int32_t bvh_root;        // root reference (see BvhNode) when accel == RVCP_ACCEL_BVH
     uint32_t bvh_n4;         // Bvh4Node count; the Bvh4QNode copy follows them in the buffer
+    uint32_t bvh_slots;      // leaf-order slots; the packed 10-float records follow the TriRecords
     // small frames (path kernels of schedules 3/6): when the surface list fits the resident
     // lanes, spread it over every resident wave, at least spread_min pixels each (0 = off),
     // and let waves with <= 32 rays split each ray's scan over R lanes from the first

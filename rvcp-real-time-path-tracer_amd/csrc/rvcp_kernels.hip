@@ -282,10 +282,44 @@ __device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, f
 // One leaf: its (at most kBvhLeafMax) triangles are loaded before any is tested, so the
 // leaf costs one memory round trip instead of one per triangle.  The original face id rides in
 // TriRecord::pad[0] of the leaf-ordered copy (rvcp_host.cpp).
+// RVCP_BVH_PACKED: the leaf's triangles are read from the packed copy behind the TriRecords
+// (10 floats per slot: v0, e1, e2, face id bits; leaves start at even slots, so 16-B aligned):
+// ceil(2.5 cnt) 16-B loads instead of 3 cnt.
+#ifndef RVCP_BVH_PACKED
+#define RVCP_BVH_PACKED 1
+#endif
 __device__ __forceinline__ void bvh_leaf(const TriRecord *__restrict__ btri, int32_t ref, f3 o, f3 d,
-                                         float tmin, float &bt, int &best) {
+                                         float tmin, float &bt, int &best, uint32_t slots = 0) {
     const uint32_t code = ~(uint32_t)ref;
     const uint32_t first = code >> 5, cnt = (code & 31u) + 1u;
+#if RVCP_BVH_PACKED
+    const float4 *base = reinterpret_cast<const float4 *>(
+        reinterpret_cast<const float *>(btri + slots) + 10u * first);
+    const uint32_t nld = (10u * cnt + 3u) >> 2;
+    float4 W[(10 * kBvhLeafMax + 3) / 4];
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)((10 * kBvhLeafMax + 3) / 4); ++k)
+        if (k < nld) W[k] = base[k];
+    const float *F = reinterpret_cast<const float *>(W);
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)kBvhLeafMax; ++k) {
+        if (k < cnt) {
+            TriRecord T;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                T.v0[c] = F[10 * k + c];
+                T.e1[c] = F[10 * k + 3 + c];
+                T.e2[c] = F[10 * k + 6 + c];
+            }
+            float t;
+            const int id = __float_as_int(F[10 * k + 9]);
+            if (tri_accept(T, o, d, tmin, bt, t) && (t < bt || id > best)) {
+                bt = t;
+                best = id;
+            }
+        }
+    }
+#else
     TriRecord L[kBvhLeafMax];
 #pragma unroll
     for (uint32_t k = 0; k < (uint32_t)kBvhLeafMax; ++k)
@@ -301,6 +335,7 @@ __device__ __forceinline__ void bvh_leaf(const TriRecord *__restrict__ btri, int
             }
         }
     }
+#endif
 }
 
 __device__ __forceinline__ f3 slab_inv(f3 d) {
@@ -358,7 +393,7 @@ template <bool LDS>
 __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
                                          const TriRecord *__restrict__ btri, int32_t root,
                                          lds_i32 *stk, f3 o, f3 d, float tmin, float &bt,
-                                         int &best, uint32_t n4 = 0) {
+                                         int &best, uint32_t n4 = 0, uint32_t slots = 0) {
     const f3 inv = slab_inv(d);
     int32_t priv[LDS ? 1 : kBvhStack];
     int sp = 0;
@@ -414,7 +449,7 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
             if (k1 < inf) { if (LDS) stk[sp * kBlock] = c1; else priv[sp] = c1; sp += 1; }
             if (k0 < inf) { ref = c0; continue; }
         } else {
-            bvh_leaf(btri, ref, o, d, tmin, bt, best);
+            bvh_leaf(btri, ref, o, d, tmin, bt, best, slots);
         }
         if (sp == 0) break;
         sp -= 1;
@@ -1091,7 +1126,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
         int best = -1;
         float bt = tmax;
         if (BVH) {
-            bvh_nearest<false>(bvh_nodes, bvh_tris, A.bvh_root, nullptr, o, d, tmin, bt, best, A.bvh_n4);
+            bvh_nearest<false>(bvh_nodes, bvh_tris, A.bvh_root, nullptr, o, d, tmin, bt, best, A.bvh_n4, A.bvh_slots);
         } else {
 #pragma unroll 2
             for (uint32_t i = 0; i < A.n_faces; ++i) {
@@ -1522,8 +1557,8 @@ __device__ __forceinline__ void path_body(
         } else if (BVH) {
             // ---- opt-in BVH: each lane traverses for its own rays ----
             lds_i32 *stk = (lds_i32 *)bvh_stack;
-            if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA, A.bvh_n4);
-            if (sB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB, A.bvh_n4);
+            if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA, A.bvh_n4, A.bvh_slots);
+            if (sB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB, A.bvh_n4, A.bvh_slots);
         } else if (tail) {
             // ---- tail: R lanes per ray, each scanning every R-th triangle ----
             // The frame queue is empty, so what is left are the serial sample chains of the
