@@ -27,18 +27,27 @@ Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
       the shader north_star names) instead of the games101 branch the current host binds.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the path-tracing kernel,
->99% of the frame's GPU time), whose bound is FP32 VALU issue: `achieved` =
-useful FLOP per launch (52 per reference-algorithm ray-triangle test, 25 per ray-sphere test,
-SURVEY.md §8(d)) / that kernel's HIP-event time on its launch stream
-(rvcp_stats_t.main_kernel_ms), `peak` = 157.3 TFLOP/s FP32 vector.  `traffic` is the same
-kernel's measured HBM bytes per launch from the rocprofv3 PMC summary committed under
-profiles/ (tools/pmc_traffic.py), when one exists for the workload and kernel schedule;
-`hbm_algorithmic` is SURVEY.md §8(d)'s HBM-read figure (36 algorithmic bytes per triangle
-test), which exceeds the HBM peak because the scene is served on-chip.  `valu_busy_pmc` /
-`valu_issue_frac_pmc` come from the committed SQ counter passes (tools/pmc_valu.py).
-`cpu_baseline` times the scalar C oracle (oracle/rvcp_oracle.c, the CPU re-execution of the
-same kernel) on every hardware thread of the host (`cores`), with the box's CPU share
-(OMP_NUM_THREADS, 16 per GPU) and one thread timed beside it, rank 0 at N=1 only.
+>99% of the frame's GPU time), whose bound is FP32 VALU issue:
+  * `achieved` / `frac`: useful FLOP per frame (52 per reference-algorithm ray-triangle test,
+    25 per ray-sphere test) / `ms_per_step` (the driver-comparable wall time
+    per frame) / `peak` = 157.3 TFLOP/s FP32 vector;
+  * `frac_executed`: the same with the traversals the kernels execute (the primary hit is
+    traced once per pixel, not once per sample);
+  * `per_launch`: useful FLOP / the path kernel's HIP-event time with ONE frame in flight, from
+    a short pass after the timed region (with frames in flight a launch's event time includes
+    the other frame's work); the rocprofv3 summary of the same command is committed under
+    profiles/ and must agree;
+  * `valu_issue_*_pmc`: VALU wave-instructions per SIMD-cycle from the committed SQ counter
+    passes (tools/pmc_valu.py), against the guide's 0.5 (2 cycles per wave64 instruction) and
+    against the measured ceiling (tools/valu_rate.hip);
+  * `traffic`: the kernel's measured HBM bytes per launch (rocprofv3 PMC, tools/pmc_traffic.py);
+    `hbm_algorithmic`: SURVEY.md §8(d)'s HBM-read figure (36 algorithmic bytes per triangle
+    test), which exceeds the HBM peak because the scene is served on-chip.
+  With --accel bvh the work is not the brute-force scan's, so `frac` is null (the traversal is
+  bound by dependent node loads).
+`cpu_baseline` times the scalar C port of the shader (oracle/rvcp_oracle.c; the image has no
+Rust toolchain for a Rust re-execution) on the CPUs this process is granted (the cgroup quota,
+16 per GPU on the box; `cores`), with one thread timed beside it, rank 0 at N=1 only.
 """
 import argparse
 import json
@@ -129,7 +138,7 @@ def cpu_model():
 
 
 def host_threads():
-    """Hardware threads this process may run on (the whole host, not OMP_NUM_THREADS)."""
+    """Hardware threads this process may run on (the whole host)."""
     try:
         return len(os.sched_getaffinity(0)) or 1
     except AttributeError:
@@ -146,10 +155,18 @@ def cgroup_cpu_quota():
         return None
 
 
-def cpu_baseline(sc, cfg_kw, W, H, threads, share_threads=0):
-    """Time the CPU oracle (scalar C re-execution) on a bounded sample of the workload:
-    `threads` (default: every hardware thread of the host) on the whole frame, the box's CPU
-    share (`share_threads`, OMP_NUM_THREADS) on the same frame, and 1 thread on a row sample."""
+def granted_cpus():
+    """The CPUs this process can actually use: the cgroup quota (rounded down) when there is
+    one, else the affinity mask."""
+    q = cgroup_cpu_quota()
+    n = host_threads()
+    return max(1, min(n, int(q))) if q else n
+
+
+def cpu_baseline(sc, cfg_kw, W, H, threads):
+    """Time the CPU port (scalar C re-execution of the shader) on a bounded sample of the
+    workload: the whole frame on `threads` threads (the granted CPUs), and 1 thread on a row
+    sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     import rvcp_amd
@@ -159,7 +176,11 @@ def cpu_baseline(sc, cfg_kw, W, H, threads, share_threads=0):
                   faces=sc.mesh.aligned_faces(), lum_face_ids=sc.luminous_face_ids(),
                   spheres=sc.aligned_spheres())
     push = sc.push_constant(123.0)
-    rows = list(range(0, H, 8))
+    common = dict(unit="Msamples/s", cores=threads, kind="port",
+                  implementation="C port of the shader (oracle/rvcp_oracle.c); the image has no "
+                                 "Rust toolchain, so not a Rust re-execution",
+                  host_threads=host_threads(), cgroup_cpu_quota=cgroup_cpu_quota(),
+                  cpu=cpu_model())
     O.render(arrays, push, cfg, W, H, rect=(0, H // 2, min(W, 64), 1), threads=threads,
              want_linear=False)                                   # warm-up (page-in, threads)
     if len(arrays["faces"]) > 1000:          # C5 on CPU: 128^2 SPP=1 frame only
@@ -167,34 +188,75 @@ def cpu_baseline(sc, cfg_kw, W, H, threads, share_threads=0):
         O.render(arrays, push, rvcp_amd.abi.make_config(**dict(cfg_kw, spp=1)), 128, 128,
                  threads=threads, want_linear=False)
         dt = time.perf_counter() - t0
-        return dict(value=128 * 128 / dt / 1e6, unit="Msamples/s", cores=threads, kind="port",
-                    sample="128x128 SPP=1 frame of the same scene", seconds=round(dt, 3),
-                    cpu=cpu_model())
+        return dict(value=round(128 * 128 / dt / 1e6, 4), sample="128x128 SPP=1 frame of the same scene",
+                    seconds=round(dt, 3), **common)
     # the whole frame on `threads` threads (a few seconds), then a single-thread figure on
     # every 64th row
     t0 = time.perf_counter()
     O.render(arrays, push, cfg, W, H, threads=threads, want_linear=False)
     dt = time.perf_counter() - t0
     samples = W * H * cfg_kw["spp"]
-    share = {}
-    if share_threads and share_threads != threads:
-        t2 = time.perf_counter()
-        O.render(arrays, push, cfg, W, H, threads=share_threads, want_linear=False)
-        dt2 = time.perf_counter() - t2
-        share = dict(share_threads=share_threads, share_value=round(samples / dt2 / 1e6, 4),
-                     share_seconds=round(dt2, 3))
     rows1 = list(range(0, H, 64 if H >= 256 else 8))
     t1 = time.perf_counter()
     for y in rows1:
         O.render(arrays, push, cfg, W, H, rect=(0, y, W, 1), threads=1, want_linear=False)
     dt1 = time.perf_counter() - t1
-    return dict(value=samples / dt / 1e6, unit="Msamples/s", cores=threads, kind="port",
+    return dict(value=round(samples / dt / 1e6, 4),
                 sample=f"the full {W}x{H} SPP={cfg_kw['spp']} frame on {threads} threads",
                 seconds=round(dt, 3),
                 single_thread_value=round(len(rows1) * W * cfg_kw["spp"] / dt1 / 1e6, 4),
                 single_thread_sample=f"every {64 if H >= 256 else 8}th row ({len(rows1)} rows), 1 thread",
-                single_thread_seconds=round(dt1, 3), cpu=cpu_model(),
-                cgroup_cpu_quota=cgroup_cpu_quota(), **share)
+                single_thread_seconds=round(dt1, 3), **common)
+
+
+def _all_ok(dist, ok, why):
+    """Agree over the control plane: (True, None) if every rank is ok, else (False, reasons)."""
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, (bool(ok), why))
+    bad = [w for o, w in got if not o]
+    return (not bad), (None if not bad else "; ".join(str(w) for w in bad))
+
+
+def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe=None):
+    """Decide, on every rank alike, whether the frame moves over RCCL or through host memory.
+
+    1. every rank creates RCCL ids (a local call that loads librccl: a rank without a usable
+       RCCL fails here, before any collective RCCL call could block the others); agreed over
+       the control plane (gloo);
+    2. rank 0's ids are broadcast and every rank joins each communicator (init_comm(i, id));
+       agreed;
+    3. `probe()` (a tiny render + gather + check) on every rank; agreed.
+    Any failure on any rank sends every rank to the host gather, with the reasons.  (A rank
+    whose ncclCommInitRank fails while the others succeed leaves them blocked inside RCCL
+    itself; such asymmetric init failures are outside what a blocking init can recover.)
+    Returns ("rccl", None) or ("host", reason)."""
+    ids, why = None, None
+    try:
+        ids = [make_id() for _ in range(n_comms)]
+    except Exception as e:              # noqa: BLE001 -- reported in the JSON line
+        why = f"rank {rank}: rccl id: {e!r}"
+    ok, reason = _all_ok(dist, why is None, why)
+    if not ok:
+        return "host", reason
+    got = [ids if rank == 0 else None]
+    dist.broadcast_object_list(got, src=0)
+    try:
+        for i, uid in enumerate(got[0]):
+            init_comm(i, uid)
+    except Exception as e:              # noqa: BLE001
+        why = f"rank {rank}: rccl init: {e!r}"
+    ok, reason = _all_ok(dist, why is None, why)
+    if not ok:
+        return "host", reason
+    if probe is not None:
+        try:
+            probe()
+        except Exception as e:          # noqa: BLE001
+            why = f"rank {rank}: gather probe: {e!r}"
+        ok, reason = _all_ok(dist, why is None, why)
+        if not ok:
+            return "host", reason
+    return "rccl", None
 
 
 def main():
@@ -206,8 +268,8 @@ def main():
                     help="default: c3 at N=1 (headline), c4 at N>1 (BASELINE's 8-GPU config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="oracle threads for cpu_baseline (default: every hardware thread "
-                         "this process may use; the OMP_NUM_THREADS share is timed beside it)")
+                    help="oracle threads for cpu_baseline (default: the CPUs this process is "
+                         "granted -- the cgroup quota, else the affinity mask)")
     ap.add_argument("--save-frame", default="")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="contexts rendering consecutive frames concurrently (1 = one frame "
@@ -216,16 +278,18 @@ def main():
                          "N>1 rehearsals always use 1)")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
+    ap.add_argument("--launch-pass", type=int, default=10,
+                    help="frames of the post-timing one-frame-in-flight pass that measures the "
+                         "path kernel's isolated launch time (roofline.per_launch; 0 = skip)")
     args = ap.parse_args()
 
     # Hardware queues per process: HIP's default is 4; with 4 frames in flight on small frames
     # (C2) the contexts' streams then share queues and serialise.  8 queues let C2 take a fourth
-    # frame: 0.284 -> 0.269 ms (profiles/r02_hwq_fif_sweep.log).  Set before HIP initialises.
-    try:
-        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
-    except ValueError:
-        hwq = 4
-    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, hwq)))
+    # frame: 0.284 -> 0.269 ms (profiles/r02_hwq_fif_sweep.log).  Only when the variable is unset
+    # (an explicit value is the user's), before HIP initialises; the value used is in the line.
+    if "GPU_MAX_HW_QUEUES" not in os.environ:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    hw_queues = os.environ["GPU_MAX_HW_QUEUES"]
 
     import torch
     import torch.distributed as dist
@@ -245,8 +309,9 @@ def main():
         local_rank = 0
     torch.cuda.set_device(local_rank)
     if world > 1:
-        # control plane only (barriers, the max-over-ranks time, the RCCL id); the frame
-        # itself moves over RCCL inside librvcp (rvcp_gather_frame_async)
+        # control plane only (barriers, the max-over-ranks time, the RCCL ids, agreement on
+        # the gather mode); the frame itself moves over RCCL inside librvcp
+        # (rvcp_gather_frame_async)
         dist.init_process_group("gloo")
 
     wname = args.workload or ("c3" if world == 1 else "c4")
@@ -275,25 +340,6 @@ def main():
     rank_samples = W * spp * rvcp_amd.shard_rows(H, rank, world)
     auto_fif = 4 if rank_samples < (4 << 20) else (3 if legacy else 2)
     fif = 1 if rehearsal else (args.frames_in_flight or auto_fif)
-    # RCCL communicator ids (one per context), made on rank 0 and shared over the control
-    # plane.  If rank 0 cannot make them (no usable librccl) every rank learns it from the
-    # broadcast and the frame is gathered through host memory over gloo instead, labelled as
-    # such in the JSON line ("gather"), so that a scaling run still yields a measured line.
-    rccl_ids, rccl_error = None, None
-    if world > 1 and not rehearsal:
-        got = [None]
-        if rank == 0:
-            try:
-                got = [[rvcp_amd.rccl_unique_id() for _ in range(fif)]]
-            except Exception as e:          # noqa: BLE001 -- reported in the JSON line
-                got = [repr(e)]
-        dist.broadcast_object_list(got, src=0)
-        if isinstance(got[0], list):
-            rccl_ids = got[0]
-        else:
-            rccl_error = got[0]
-            fif = 1
-    host_gather = rehearsal or rccl_error is not None
     rts = [rvcp_amd.RayTracer(**cfg_kw) for _ in range(fif)]
     t_up = time.perf_counter()
     rts[0].upload_scene(sc)              # includes the scene-specialised compile (§4.7)
@@ -304,9 +350,6 @@ def main():
     push = sc.push_constant(123.0)
     n_faces = len(sc.mesh.aligned_faces())
     n_spheres = len(sc.spheres) if legacy else 0
-    if rccl_ids is not None:
-        for r, uid in zip(rts, rccl_ids):    # one communicator per context, created in order
-            r.rccl_init(uid, world, rank)
 
     rows = rvcp_amd.shard_rows(H, rank, world)
     slot = rvcp_amd.shard_rows(H, 0, world)          # shard 0 has the most rows
@@ -316,8 +359,42 @@ def main():
               for _ in range(fif)]
     gat_flats = [torch.zeros((world, slot, W), dtype=torch.int32, device=dev)
                  if (world > 1 and rank == 0) else None for _ in range(fif)]
+
+    # The gather mode, agreed by every rank (negotiate_gather): RCCL (one communicator per
+    # context) when every rank can load RCCL, join the communicators and pass a probe gather;
+    # otherwise every rank gathers through host memory over gloo, labelled in the JSON line.
+    gather_mode, gather_error = ("none", None) if world == 1 else ("host", "rehearsal")
+    if world > 1 and not rehearsal:
+        def probe():
+            # a tiny frame (8 rows per rank) rendered, gathered and checked against rank 0's own
+            # render of it, on every context
+            pW, pH = 16, 8 * world
+            p_slot = rvcp_amd.shard_rows(pH, 0, world)
+            p_shard = torch.zeros((p_slot, pW), dtype=torch.int32, device=dev)
+            p_gat = torch.zeros((world, p_slot, pW), dtype=torch.int32, device=dev) if rank == 0 else None
+            p_frame = torch.zeros((pH, pW), dtype=torch.int32, device=dev) if rank == 0 else None
+            for r in rts:
+                r.render_shard_async(push, pW, pH, rank, world, p_shard.data_ptr())
+                r.gather_frame_async(p_shard.data_ptr(), pW, pH,
+                                     p_gat.data_ptr() if rank == 0 else 0,
+                                     p_frame.data_ptr() if rank == 0 else 0)
+                r.sync_stats()
+                r.gather_wait()
+                if rank == 0:
+                    ref = torch.zeros((pH, pW), dtype=torch.int32, device=dev)
+                    r.render_shard_async(push, pW, pH, 0, 1, ref.data_ptr())
+                    r.sync_stats()
+                    torch.cuda.synchronize()
+                    if not torch.equal(ref, p_frame):
+                        raise RuntimeError("probe frame differs from the 1-rank render")
+            torch.cuda.synchronize()
+        gather_mode, gather_error = negotiate_gather(
+            dist, rank, fif, rvcp_amd.rccl_unique_id,
+            lambda i, uid: rts[i].rccl_init(uid, world, rank), probe)
+    host_gather = world > 1 and gather_mode != "rccl"
     torch.cuda.synchronize()
     pending = [False] * fif
+    gather_ms = []
 
     def enqueue(i):
         """Enqueue one frame on context i's own stream (stream 0 = the context's stream)."""
@@ -337,6 +414,8 @@ def main():
         """Wait for context i's frame; return its stats."""
         st = rts[i].sync_stats()
         pending[i] = False
+        if world > 1 and not host_gather:
+            gather_ms.append(rts[i].gather_wait()[0])
         if host_gather:    # gloo gather through host memory (rehearsal / no usable RCCL)
             got = rvcp_amd.frame.gather_shards(shard_bufs[i].cpu(), rank, world, dst=0)
             if rank == 0:
@@ -360,6 +439,7 @@ def main():
     for f in range(args.warmup):
         step(f)
     drain()
+    gather_ms.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -374,18 +454,18 @@ def main():
         if st is not None:
             stats.append(st)
     stats += drain()
-    kernel_ms = [float(st["kernel_ms"]) for st in stats]
-    main_ms = [float(st["main_kernel_ms"]) for st in stats]
-    trav = sum(int(st["traversals"]) for st in stats)
-    trav_exec = sum(int(st["traversals_executed"]) for st in stats)
-    variant = int(stats[-1]["kernel_variant"])
-    assert len(stats) == args.steps
     frame = frames[0]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    kernel_ms = [float(st["kernel_ms"]) for st in stats]
+    main_ms = [float(st["main_kernel_ms"]) for st in stats]
+    trav = sum(int(st["traversals"]) for st in stats)
+    trav_exec = sum(int(st["traversals_executed"]) for st in stats)
+    variant = int(stats[-1]["kernel_variant"])
+    assert len(stats) == args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -395,6 +475,15 @@ def main():
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed * 1000.0 / args.steps
 
+    # Isolated launch time (after the timed region): the path kernel with ONE frame in flight,
+    # so its HIP-event time is its own (roofline.per_launch).
+    iso_ms = []
+    if args.launch_pass > 0:
+        for _ in range(args.launch_pass):
+            rt.render_shard_async(push, W, H, rank, world,
+                                  (frames[0] if world == 1 else shard_bufs[0]).data_ptr())
+            iso_ms.append(float(rt.sync_stats()["main_kernel_ms"]))
+
     # roofline of the dominant kernel (this rank's launches).  The pre-pass (schedules 3-6,
     # games101 only) traces each pixel's primary ray once; every other reference-algorithm
     # traversal -- including the reused primary hits of samples 2..SPP -- belongs to the
@@ -403,33 +492,58 @@ def main():
     avg_kernel_s = (sum(main_ms) / len(main_ms)) / 1000.0
     prepass = 0 if legacy else rows * W
     units = trav / args.steps - prepass                     # traversals per path-kernel launch
+    units_exec = trav_exec / args.steps - prepass
     tri_tests = units * n_faces
     flop_per_launch = tri_tests * FLOP_PER_TEST + units * n_spheres * FLOP_PER_SPHERE_TEST
-    achieved_tflops = flop_per_launch / avg_kernel_s / 1e12
+    flop_exec = units_exec * (n_faces * FLOP_PER_TEST + n_spheres * FLOP_PER_SPHERE_TEST)
+    wall_s = ms_per_step / 1000.0
+    # (at N>1 each rank's FLOP over the max-over-ranks wall time per frame)
+    achieved_tflops = flop_per_launch / wall_s / 1e12
     # 36 algorithmic bytes per triangle test (16 per sphere test)
     bytes_per_launch = units * (n_faces * 36 + n_spheres * 16)
-    algo_gbs = bytes_per_launch / avg_kernel_s / 1e9
-    exec_tests_per_s = (trav_exec / args.steps - prepass) * (n_faces + n_spheres) / avg_kernel_s
+    algo_gbs = bytes_per_launch / wall_s / 1e9
     kname = rvcp_amd.abi.KERNEL_NAMES.get(variant, "?")
     traffic, traffic_src = load_traffic(wl["workload"], kname)
     valu_busy, valu_issue_frac = load_valu_busy(wl["workload"], kname)
+    bvh = args.accel == "bvh"
+    iso_s = (float(np.mean(iso_ms)) / 1000.0) if iso_ms else None
 
     frame_check, one_gpu_ms = None, None
     if world > 1 and rank == 0:
         # the assembled N-rank frame must be bit-identical to a 1-rank render of the same frame
-        # (outside timing); its time is the same-frame single-GPU reference for the speedup
-        single = torch.zeros((H, W), dtype=torch.int32, device=dev)
-        times = []
-        for _ in range(3):
-            torch.cuda.synchronize()
-            ts = time.perf_counter()
-            rt.render_shard_async(push, W, H, 0, 1, single.data_ptr())
-            rt.sync_stats()
-            torch.cuda.synchronize()
-            times.append((time.perf_counter() - ts) * 1000.0)
-        one_gpu_ms = float(np.median(times))
-        frame_check = bool(torch.equal(single, frame))
+        # (outside timing); the same frame rendered by this GPU alone, with the same frames in
+        # flight as the N-rank run, is the single-GPU reference for the speedup
+        singles = [torch.zeros((H, W), dtype=torch.int32, device=dev) for _ in range(fif)]
+        n1 = 3 * fif
+        for i in range(fif):                               # warm-up, one per context
+            rts[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
+        for i in range(fif):
+            rts[i].sync_stats()
+        torch.cuda.synchronize()
+        busy = [False] * fif
+        ts = time.perf_counter()
+        for f in range(n1):
+            i = f % fif
+            if busy[i]:
+                rts[i].sync_stats()
+            rts[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
+            busy[i] = True
+        for i in range(fif):
+            if busy[i]:
+                rts[i].sync_stats()
+        torch.cuda.synchronize()
+        one_gpu_ms = (time.perf_counter() - ts) * 1000.0 / n1
+        frame_check = bool(torch.equal(singles[0], frame))
+
+    per_rank = None
     if world > 1:
+        mine = dict(rank=rank, path_kernel_ms=round(avg_kernel_s * 1000.0, 4),
+                    frame_kernels_ms=round(avg_frame_s * 1000.0, 4),
+                    isolated_path_kernel_ms=None if iso_s is None else round(iso_s * 1000.0, 4),
+                    gather_ms=round(float(np.mean(gather_ms)), 4) if gather_ms else None,
+                    rows=rows)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         dist.barrier()
 
     if args.save_frame and rank == 0:
@@ -464,58 +578,66 @@ def main():
                                 if variant & rvcp_amd.abi.VARIANT_SPECIALIZED else "generic"),
                        "upload_s": round(upload_s, 3),
                        "frames_in_flight": fif,
-                       "gather": ("gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
-                                  f"gloo through host memory (RCCL unavailable: {rccl_error})"
-                                  if rccl_error is not None else
-                                  "rccl ncclGather via rvcp_gather_frame_async") if world > 1 else "none"},
-            "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 2),
+                       "gpu_max_hw_queues": hw_queues,
+                       "gather": ("none" if world == 1 else
+                                  "gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
+                                  "rccl ncclGather via rvcp_gather_frame_async" if not host_gather
+                                  else f"gloo through host memory (RCCL not usable: {gather_error})")},
+            "roofline": {"bound": "latency (dependent BVH node loads)" if bvh else "valu",
+                         "achieved": None if bvh else round(achieved_tflops, 2),
                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
-                         # the same useful FLOP over the wall time per frame: with frames in
-                         # flight a launch's event time includes the other frame's overlap
-                         "achieved_wall": round(flop_per_launch / (ms_per_step / 1000.0) / 1e12, 2),
-                         "frac_wall": round(flop_per_launch / (ms_per_step / 1000.0) / 1e12
-                                            / FP32_PEAK_TFLOPS, 4),
+                         "frac": None if bvh else round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
+                         "definition": (
+                             "BVH: the brute-force scan's FLOP are not executed; no FLOP roofline "
+                             "(DESIGN.md §4.6)" if bvh else
+                             f"useful FP32 FLOP per frame ({FLOP_PER_TEST} per reference-"
+                             f"algorithm ray-triangle test, {FLOP_PER_SPHERE_TEST} per ray-sphere "
+                             "test) / ms_per_step / peak"),
+                         "frac_executed": None if bvh else round(flop_exec / wall_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+                         "frac_executed_definition": "FLOP of the traversals the kernels execute "
+                                                     "(primary hit once per pixel) / ms_per_step / peak",
+                         "per_launch": None if (bvh or iso_s is None) else {
+                             "kernel_ms": round(iso_s * 1000.0, 4),
+                             "kernel_ms_min": round(min(iso_ms), 4),
+                             "achieved": round(flop_per_launch / iso_s / 1e12, 2),
+                             "frac": round(flop_per_launch / iso_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+                             "frames": len(iso_ms),
+                             "definition": "useful FLOP / the path kernel's HIP-event time with "
+                                           "one frame in flight (post-timing pass)"},
+                         "kernel": kname,
+                         "kernel_ms_in_flight": round(avg_kernel_s * 1000.0, 4),
+                         "frame_kernels_ms_in_flight": round(avg_frame_s * 1000.0, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
-                         "traffic_hbm_frac": None if traffic is None else
-                         round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 5),
-                         "kernel": kname,
-                         "kernel_ms": round(avg_kernel_s * 1000.0, 4),
-                         "frame_kernels_ms": round(avg_frame_s * 1000.0, 4),
-                         "definition": f"useful FP32 FLOP per launch ({FLOP_PER_TEST} per reference-"
-                                       f"algorithm ray-triangle test, {FLOP_PER_SPHERE_TEST} per "
-                                       "ray-sphere test) / the dominant kernel's HIP-event time"
-                                       + (" (BVH: brute-force-equivalent tests; work avoided)"
-                                          if args.accel == "bvh" else ""),
+                         "traffic_hbm_frac": None if (traffic is None or iso_s is None) else
+                         round(traffic / iso_s / 1e9 / HBM_PEAK_GBS, 5),
                          "tests_per_launch": round(tri_tests),
                          "hbm_algorithmic": {
                              "bytes_per_launch": round(bytes_per_launch),
                              "achieved_gbs": round(algo_gbs, 1),
                              "frac_of_peak": round(algo_gbs / HBM_PEAK_GBS, 4),
                              "definition": "SURVEY.md §8(d): reference-algorithm traversals x "
-                                           "(F x 36 B + S x 16 B) per launch / kernel time; > 1 "
+                                           "(F x 36 B + S x 16 B) per frame / ms_per_step; > 1 "
                                            "= on-chip reuse (scene in scalar cache / LDS)"},
                          "traversals_per_sample": round(trav / args.steps / (W * H * spp / world), 4)
                          if world == 1 else None,
                          "executed_traversal_frac": round(trav_exec / max(trav, 1), 4),
-                         "executed_tests_per_s": round(exec_tests_per_s, 1),
-                         "valu_busy_pmc": valu_busy,
-                         "valu_issue_frac_pmc": valu_issue_frac},
+                         "valu_issue_frac_pmc_guide": valu_busy,
+                         "valu_issue_frac_pmc_measured_ceiling": valu_issue_frac},
             "cpu_baseline": None,
         }
+        if world > 1:
+            out["config"]["per_rank"] = per_rank
         if frame_check is not None:
             out["config"]["assembled_frame_bitexact_vs_1gpu"] = frame_check
             out["config"]["one_gpu_ms"] = round(one_gpu_ms, 4)
+            out["config"]["one_gpu_frames_in_flight"] = fif
             out["config"]["speedup_vs_one_gpu_same_frame"] = round(one_gpu_ms / ms_per_step, 3)
             if rehearsal:
                 out["config"]["physical_gpus"] = 1
         if world == 1 and not args.no_cpu_baseline:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import oracle as O
-            threads = args.cpu_threads or host_threads()
-            out["cpu_baseline"] = cpu_baseline(sc, cfg_kw, W, H, threads,
-                                               share_threads=O.default_threads())
+            threads = args.cpu_threads or granted_cpus()
+            out["cpu_baseline"] = cpu_baseline(sc, cfg_kw, W, H, threads)
         print(json.dumps(out), flush=True)
 
     for r in rts:

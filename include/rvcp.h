@@ -392,9 +392,16 @@ int rvcp_rccl_attach(rvcp_ctx_t *ctx, void *nccl_comm, uint32_t world, uint32_t 
  * assemble the W x H RGBA8 frame into d_frame.  d_shard_rgba8: rvcp_shard_rows(H, 0, world)
  * * W * 4 bytes on every rank; d_gathered (world times that) and d_frame (W*H*4 bytes) are
  * needed on rank 0 only (NULL elsewhere).  Enqueued on `stream` (NULL: ctx's stream); the
- * frame is bit-identical to a single-GPU render. */
+ * frame is bit-identical to a single-GPU render.  The preceding render on ctx must have been
+ * shard_index = rank, shard_count = world of the same W x H frame (else RVCP_E_INVALID). */
 int rvcp_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, uint32_t width,
                             uint32_t height, void *d_gathered, void *d_frame, void *stream);
+
+/* Wait for ctx's last rvcp_gather_frame_async and report its device time (ncclGather plus, on
+ * rank 0, the assembly) in *gather_ms and, if frame_ms is not NULL, the time from the start of
+ * the preceding render to the end of the gather in *frame_ms (HIP events on the gather's
+ * stream).  RVCP_E_INVALID when no gather was enqueued since the last call. */
+int rvcp_gather_wait(rvcp_ctx_t *ctx, float *gather_ms, float *frame_ms);
 
 #ifdef __cplusplus
 }

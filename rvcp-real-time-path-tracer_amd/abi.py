@@ -48,7 +48,8 @@ EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "r
             "rvcp_destroy", "rvcp_last_error", "rvcp_upload_scene", "rvcp_render", "rvcp_render_shard_async",
             "rvcp_sync_stats", "rvcp_shard_rows", "rvcp_assemble_frame_async",
             "rvcp_upload_scene_file", "rvcp_mandelbrot", "rvcp_render_async", "rvcp_wait",
-            "rvcp_rccl_unique_id", "rvcp_rccl_init", "rvcp_rccl_attach", "rvcp_gather_frame_async"]
+            "rvcp_rccl_unique_id", "rvcp_rccl_init", "rvcp_rccl_attach", "rvcp_gather_frame_async",
+            "rvcp_gather_wait"]
 
 
 # Integrator mode 2 (ray_tracer.comp ray_trace): its own #defines (ray_tracer.comp:5-13).
@@ -134,11 +135,12 @@ def load():
     L.rvcp_rccl_init.argtypes = [P, P, u32, u32]
     L.rvcp_rccl_attach.argtypes = [P, P, u32, u32]
     L.rvcp_gather_frame_async.argtypes = [P, P, u32, u32, P, P, P]
+    L.rvcp_gather_wait.argtypes = [P, P, P]
     for name in ("rvcp_config_default", "rvcp_config_default_for", "rvcp_create", "rvcp_destroy", "rvcp_upload_scene",
                  "rvcp_render", "rvcp_render_shard_async", "rvcp_sync_stats",
                  "rvcp_assemble_frame_async", "rvcp_upload_scene_file", "rvcp_mandelbrot",
                  "rvcp_render_async", "rvcp_wait", "rvcp_rccl_unique_id", "rvcp_rccl_init",
-                 "rvcp_rccl_attach", "rvcp_gather_frame_async"):
+                 "rvcp_rccl_attach", "rvcp_gather_frame_async", "rvcp_gather_wait"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -28,11 +28,23 @@
 
 using namespace rvcp;
 
+// Experiment knobs (grid caps, fixed queue grabs, small-frame spreading, per-wave timelines,
+// generic-scan forcing) are read from the environment only in the debug build of the library
+// (make debug -> build/librvcp_debug.so, -DRVCP_DEBUG_KNOBS, used by tools/).  The product
+// library's behaviour depends on rvcp_config_t alone: here the names are not even compiled in.
+#ifdef RVCP_DEBUG_KNOBS
+#define RVCP_KNOB(name) std::getenv(name)
+#else
+#define RVCP_KNOB(name) ((const char *)nullptr)
+#endif
+
 struct rvcp_ctx {
     rvcp_config_t cfg{};
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;   // start, main kernel, end
+    hipEvent_t evg0 = nullptr, evg1 = nullptr;                // gather start / end
+    bool gather_pending = false;
     int grid_capacity[kMaxVariant + 1] = {};   // resident workgroups per kernel variant
     int legacy_capacity = 0;                   // ... of the RVCP_INTEGRATOR_LEGACY kernel
     int bvh_capacity = 0;                      // ... of the RVCP_ACCEL_BVH path kernel
@@ -77,7 +89,7 @@ struct rvcp_ctx {
     float *d_pack_lin = nullptr;
     size_t cap_surf_pack = 0;
 
-    // RVCP_DEBUG_TIMELINE=<file>: per-wave timeline of the path kernel appended per render
+    // debug build: per-wave timeline of the path kernel appended per render
     unsigned long long *d_timeline = nullptr;
     size_t cap_timeline = 0, last_timeline_waves = 0;
 
@@ -100,6 +112,8 @@ struct rvcp_ctx {
     int32_t last_variant = 0;
     uint64_t last_pixels = 0;
     uint32_t last_spp = 0;
+    uint32_t last_shard_index = 0, last_shard_count = 0;   // of the last rvcp_render_shard_async
+    uint32_t last_width = 0, last_height = 0;
 
     std::string err;
 };
@@ -320,7 +334,8 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     if (hipSetDevice(ctx->device) != hipSuccess) return bail(fail(ctx, RVCP_E_HIP, "hipSetDevice"));
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->evm) != hipSuccess ||
-        hipEventCreate(&ctx->ev1) != hipSuccess)
+        hipEventCreate(&ctx->ev1) != hipSuccess || hipEventCreate(&ctx->evg0) != hipSuccess ||
+        hipEventCreate(&ctx->evg1) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "stream/event creation failed"));
 
     // UNORM8 thresholds on the stored value g: u8 >= k  <=>  g >= G[k].
@@ -345,8 +360,8 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
         cus = 256;
-    // RVCP_DEBUG_BLOCKS_PER_CU caps the persistent grid (occupancy experiments only)
-    const char *cap_env = std::getenv("RVCP_DEBUG_BLOCKS_PER_CU");
+    // debug build: cap on the persistent grid (occupancy experiments only)
+    const char *cap_env = RVCP_KNOB("RVCP_DEBUG_BLOCKS_PER_CU");
     const int cap = cap_env ? std::atoi(cap_env) : 0;
     ctx->n_simds = (uint32_t)cus * 4u;
     for (int v = 1; v <= kMaxVariant; v++) {
@@ -414,6 +429,7 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     (void)hipSetDevice(ctx->device);
     // a frame still in flight (possibly on the caller's stream) reads the buffers freed below
     if (ctx->pending && ctx->ev1) (void)hipEventSynchronize(ctx->ev1);
+    if (ctx->gather_pending && ctx->evg1) (void)hipEventSynchronize(ctx->evg1);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm && ctx->comm_owned) (void)rccl_api().comm_destroy(ctx->comm);
     ctx->comm = nullptr;
@@ -430,6 +446,8 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->evm) (void)hipEventDestroy(ctx->evm);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->evg0) (void)hipEventDestroy(ctx->evg0);
+    if (ctx->evg1) (void)hipEventDestroy(ctx->evg1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return RVCP_OK;
@@ -512,19 +530,20 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         const int depth = bvh_build(reinterpret_cast<const float (*)[3][3]>(pos.data()), n_faces,
                                     nodes, order, root);
         if (depth >= kBvhStack) return fail(ctx, RVCP_E_UNSUPPORTED, "BVH deeper than the traversal stack");
-        // leaf order, face id in pad[0]; behind the S TriRecords the same slots packed as 10
-        // floats (v0, e1, e2, face id bits) -- what the traversal reads (bvh_leaf)
+        // the leaf-ordered triangles packed as 10 floats per slot (v0, e1, e2, face id bits),
+        // what the traversal reads (bvh_leaf); leaves start at even slots, so 16-B aligned.
+        // A leaf reference is ~((start << 5) | (count - 1)) in an int32: start < 2^26.
         const size_t S = order.size();
-        std::vector<TriRecord> btri(S + (10 * S * 4 + sizeof(TriRecord) - 1) / sizeof(TriRecord));
-        float *packed = reinterpret_cast<float *>(btri.data() + S);
+        if (S >= (size_t(1) << 26))
+            return fail(ctx, RVCP_E_UNSUPPORTED, "BVH leaf slots exceed 2^26 (mesh too large for the leaf encoding)");
+        std::vector<TriRecord> btri((10 * S * 4 + sizeof(TriRecord) - 1) / sizeof(TriRecord) + 1);
+        float *packed = reinterpret_cast<float *>(btri.data());
         for (size_t j = 0; j < S; j++) {
-            if (order[j] == kBvhPadId) { btri[j] = TriRecord{}; continue; }
-            btri[j] = tri[order[j]];
-            std::memcpy(&btri[j].pad[0], &order[j], 4);
-            std::memcpy(packed + 10 * j, &btri[j], 9 * sizeof(float));
+            if (order[j] == kBvhPadId) continue;        // padding slot: never referenced
+            std::memcpy(packed + 10 * j, &tri[order[j]], 9 * sizeof(float));
             std::memcpy(packed + 10 * j + 9, &order[j], 4);
         }
-        ctx->bvh_slots = (uint32_t)S;
+        ctx->bvh_slots = 0;     // the packed records start the buffer
         std::vector<Bvh4Node> nodes4;
         int32_t root4 = 0;
         if (bvh4_collapse(nodes, root, nodes4, root4) > kBvhStack)
@@ -546,7 +565,8 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     ctx->jit.reset();
     ctx->jit_err.clear();
     if (ctx->cfg.specialize == RVCP_SPECIALIZE_AUTO && ctx->cfg.accel == RVCP_ACCEL_NONE &&
-        n_faces >= 1 && n_faces <= kJitMaxFaces && !std::getenv("RVCP_NO_SPECIALIZE")) {
+        n_faces >= 1 && n_faces <= kJitMaxFaces && jit_scene_in_range(tri.data(), n_faces) &&
+        !RVCP_KNOB("RVCP_NO_SPECIALIZE")) {
         ctx->jit = jit_path_kernels(ctx->device, tri.data(), n_faces, ctx->jit_err,
                                     ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY,
                                     n_spheres == 0);
@@ -682,28 +702,28 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             A.dyn_chunk = kDynChunk;
             A.chunk_min = kMinChunk;
             A.chunk_window = kChunkWindow;
-            if (const char *c = std::getenv("RVCP_DEBUG_CHUNK")) {   // fixed grab (experiments)
+            if (const char *c = RVCP_KNOB("RVCP_DEBUG_CHUNK")) {   // fixed grab (experiments)
                 const int v = std::atoi(c);
                 if (v >= 1 && v <= 4096) A.dyn_chunk = A.chunk_min = (uint32_t)v;
             }
-            if (const char *c = std::getenv("RVCP_DEBUG_CHUNK_WINDOW")) {
+            if (const char *c = RVCP_KNOB("RVCP_DEBUG_CHUNK_WINDOW")) {
                 const int v = std::atoi(c);
                 if (v >= 1) A.chunk_window = (uint32_t)v;
             }
             A.spread_min = 0;
             A.early_tail = 0;
-            if (const char *c = std::getenv("RVCP_DEBUG_SPREAD")) A.spread_min = (uint32_t)std::atoi(c);
-            if (const char *c = std::getenv("RVCP_DEBUG_EARLY_TAIL")) A.early_tail = (uint32_t)std::atoi(c);
+            if (const char *c = RVCP_KNOB("RVCP_DEBUG_SPREAD")) A.spread_min = (uint32_t)std::atoi(c);
+            if (const char *c = RVCP_KNOB("RVCP_DEBUG_EARLY_TAIL")) A.early_tail = (uint32_t)std::atoi(c);
             // schedules 3/6 spreading a small surface list run the full resident grid
             if (A.spread_min && !legacy && !A.accel && (A.variant == 3 || A.variant == 6)) blocks = cap;
             ctx->last_timeline_waves = 0;
-            if (std::getenv("RVCP_DEBUG_TIMELINE") && !legacy && A.variant >= 3) {
+            if (RVCP_KNOB("RVCP_DEBUG_TIMELINE") && !legacy && A.variant >= 3) {
                 const size_t waves = (size_t)blocks * (kBlock / kWave);
                 if (ctx->cap_timeline < waves) {
                     (void)hipFree(ctx->d_timeline);
                     ctx->d_timeline = nullptr;
                     ctx->cap_timeline = 0;
-                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_timeline, waves * 32));
+                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_timeline, waves * 48));
                     ctx->cap_timeline = waves;
                 }
                 A.timeline = ctx->d_timeline;
@@ -752,6 +772,10 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     if (ctx->last_spec && ctx->last_variant != 0) ctx->last_variant |= RVCP_VARIANT_SPECIALIZED;
     ctx->last_pixels = A.n_pixels;
     ctx->last_spp = A.spp;
+    ctx->last_shard_index = shard_index;
+    ctx->last_shard_count = shard_count;
+    ctx->last_width = width;
+    ctx->last_height = height;
     return RVCP_OK;
 }
 
@@ -794,9 +818,10 @@ static int impl_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         stats->wave_iterations = c[2];
     }
     if (ctx->last_timeline_waves) {
-        std::vector<unsigned long long> t(4 * ctx->last_timeline_waves);
+        std::vector<unsigned long long> t(6 * ctx->last_timeline_waves);
         HIP_TRY(ctx, hipMemcpy(t.data(), ctx->d_timeline, t.size() * 8, hipMemcpyDeviceToHost));
-        if (FILE *f = std::fopen(std::getenv("RVCP_DEBUG_TIMELINE"), "ab")) {
+        const char *path = RVCP_KNOB("RVCP_DEBUG_TIMELINE");
+        if (FILE *f = path ? std::fopen(path, "ab") : nullptr) {
             std::fwrite(t.data(), 8, t.size(), f);
             std::fclose(f);
         }
@@ -1064,16 +1089,44 @@ static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, u
         return fail(ctx, RVCP_E_INVALID, "invalid gather arguments");
     if ((uint64_t)width * height >= (1ull << 31))
         return fail(ctx, RVCP_E_INVALID, "frame too large (W*H must be < 2^31)");
+    // the gather assumes this rank rendered shard comm_rank of comm_world of this frame size;
+    // anything else would assemble a scrambled frame on rank 0
+    if (ctx->last_shard_count != ctx->comm_world || ctx->last_shard_index != ctx->comm_rank ||
+        ctx->last_width != width || ctx->last_height != height)
+        return fail(ctx, RVCP_E_INVALID, "gather after a render of another shard / frame size "
+                    "(rvcp_render_shard_async must use shard_index = rank, shard_count = world)");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     const uint32_t N = ctx->comm_world;
     const uint32_t slot = rvcp_shard_rows(height, 0, N);      // shard 0 has the most rows
+    HIP_TRY(ctx, hipEventRecord(ctx->evg0, s));
     const ncclResult_t r = rccl_api().gather(d_shard_rgba8, root ? d_gathered : nullptr,
                                              (size_t)slot * width, ncclUint32, 0, ctx->comm, s);
     if (r != ncclSuccess) return fail(ctx, RVCP_E_HIP, std::string("ncclGather: ") + rccl_api().error_string(r));
     if (root && rvcp_launch_assemble((const uint32_t *)d_gathered, slot, width, height, N,
                                      (uint32_t *)d_frame, s) != 0)
         return fail(ctx, RVCP_E_HIP, "assemble launch failed");
+    HIP_TRY(ctx, hipEventRecord(ctx->evg1, s));
+    ctx->gather_pending = true;
+    return RVCP_OK;
+}
+
+static int impl_gather_wait(rvcp_ctx_t *ctx, float *gather_ms, float *frame_ms)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    if (!ctx->gather_pending) return fail(ctx, RVCP_E_INVALID, "no gather in flight");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipEventSynchronize(ctx->evg1));
+    ctx->gather_pending = false;
+    float ms = 0.0f;
+    if (gather_ms) {
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->evg0, ctx->evg1));
+        *gather_ms = ms;
+    }
+    if (frame_ms) {
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->evg1));
+        *frame_ms = ms;
+    }
     return RVCP_OK;
 }
 
@@ -1187,6 +1240,11 @@ int rvcp_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, uint32_t
 {
     return barrier(ctx, [&] { return impl_gather_frame_async(ctx, d_shard_rgba8, width, height,
         d_gathered, d_frame, stream); });
+}
+
+int rvcp_gather_wait(rvcp_ctx_t *ctx, float *gather_ms, float *frame_ms)
+{
+    return barrier(ctx, [&] { return impl_gather_wait(ctx, gather_ms, frame_ms); });
 }
 
 }  // extern "C"

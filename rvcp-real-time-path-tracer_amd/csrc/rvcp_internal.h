@@ -193,14 +193,15 @@ struct FrameArgs {
     int32_t accel;           // RVCP_ACCEL_*
     int32_t bvh_root;        // root reference (see BvhNode) when accel == RVCP_ACCEL_BVH
     uint32_t bvh_n4;         // Bvh4Node count; the Bvh4QNode copy follows them in the buffer
-    uint32_t bvh_slots;      // leaf-order slots; the packed 10-float records follow the TriRecords
+    uint32_t bvh_slots;      // TriRecord offset of the packed 10-float leaf records (0: buffer start)
     // small frames (path kernels of schedules 3/6): when the surface list fits the resident
     // lanes, spread it over every resident wave, at least spread_min pixels each (0 = off),
     // and let waves with <= 32 rays split each ray's scan over R lanes from the first
     // iteration (early_tail), not only once the queue is empty
     uint32_t spread_min;
     uint32_t early_tail;
-    // debug (RVCP_DEBUG_TIMELINE): per-wave {start, queue exhausted, end, iterations}
+    // debug build of the library only: per-wave {start, queue exhausted, end, iterations,
+    // shader-clock start, shader-clock end}
     // of the path kernel, s_memrealtime ticks (100 MHz); nullptr otherwise
     unsigned long long *timeline;
 };

@@ -9,10 +9,12 @@
 // faces have a third of their edge components zero), compiles rvcp_kernels.hip around it with
 // hipRTC for gfx950, and hands the host the two kernels.
 //
-// Why the result is bit-identical to the generic scan (for finite rays and t_min > 0; the
-// kernel falls back to the generic loop for a wave holding a non-finite ray, and the host uses
-// the generic kernels when ray_t_min <= 0):
-//  * a dropped term is a product c * x with c = +0 or -0 and x finite, i.e. a zero; removing a
+// Why the result is bit-identical to the generic scan (for rays within ray_in_range and
+// t_min > 0; the kernel falls back to the generic loop for a wave holding any other ray, and
+// the host uses the generic kernels when ray_t_min <= 0 or a coordinate is out of range):
+//  * a dropped term is a product c * x with c = +0 or -0 and x finite, i.e. a zero (x is
+//    finite because nothing overflows: the scene is specialised only within jit_scene_in_range's
+//    bounds and a wave uses the scan only when its rays pass ray_in_range); removing a
 //    zero addend from a correctly rounded sum or fma changes at most the sign of a zero result;
 //  * so every intermediate equals the generic one up to the sign of zero, and the values that
 //    reach a decision are: f = 1/den (den = +-0 gives f = +-inf, and then t = +-inf or NaN is
@@ -211,6 +213,18 @@ bool emit_triangle(std::string &out, const TriRecord &T, uint32_t index, const c
 
 }  // namespace
 
+bool jit_scene_in_range(const TriRecord *tri, uint32_t n)
+{
+    // the premise of the zero-dropping (header): with |v0| <= 2^40, |e1|, |e2| <= 2^41 and the
+    // kernel's per-wave ray check (|o|_1 <= 2^41, |d|_1 <= 16) no intermediate overflows
+    for (uint32_t i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++)
+            if (!(std::fabs(tri[i].v0[k]) <= 0x1p40f) || !(std::fabs(tri[i].e1[k]) <= 0x1p41f) ||
+                !(std::fabs(tri[i].e2[k]) <= 0x1p41f))
+                return false;
+    return true;
+}
+
 std::string jit_scan_source(const TriRecord *tri, uint32_t n)
 {
     // RVCP_F32(bits): the triangle's float by its bit pattern; RVCP_SPEC_COMMIT(t, i): the
@@ -234,6 +248,42 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n)
 }
 
 // ------------------------------------------------------------------ compile + cache -----
+namespace {
+
+}  // namespace
+
+// Extra hipRTC options: only the debug build of the library (-DRVCP_DEBUG_KNOBS, tools/) reads
+// them, from RVCP_JIT_FLAGS (separated by spaces or commas).  Options that would change the
+// numeric contract (contraction, fast math) are refused; the options are part of the module
+// cache key (jit_path_kernels), so changing them within a process recompiles.
+std::vector<std::string> jit_extra_flags()
+{
+    std::vector<std::string> extra;
+#ifdef RVCP_DEBUG_KNOBS
+    if (const char *e = std::getenv("RVCP_JIT_FLAGS")) {
+        std::string cur;
+        for (const char *c = e;; c++) {
+            if (*c == ' ' || *c == ',' || *c == '\0') {
+                if (!cur.empty()) {
+                    if (cur.find("fp-contract") == std::string::npos &&
+                        cur.find("fast-math") == std::string::npos &&
+                        cur.find("ffast") == std::string::npos &&
+                        cur.find("unsafe") == std::string::npos)
+                        extra.push_back(cur);
+                    else
+                        std::fprintf(stderr, "rvcp: ignoring JIT option %s (numeric contract)\n", cur.c_str());
+                }
+                cur.clear();
+                if (!*c) break;
+            } else {
+                cur += *c;
+            }
+        }
+    }
+#endif
+    return extra;
+}
+
 namespace {
 
 uint64_t fnv1a(const std::string &s)
@@ -285,19 +335,7 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
         return -1;
     }
     // the flags of the static build (Makefile): the numeric contract depends on them
-    std::vector<std::string> extra;            // RVCP_JIT_FLAGS: experiment options,
-    if (const char *e = std::getenv("RVCP_JIT_FLAGS")) {   // separated by spaces or commas
-        std::string cur;
-        for (const char *c = e;; c++) {
-            if (*c == ' ' || *c == ',' || *c == '\0') {
-                if (!cur.empty()) extra.push_back(cur);
-                cur.clear();
-                if (!*c) break;
-            } else {
-                cur += *c;
-            }
-        }
-    }
+    const std::vector<std::string> extra = jit_extra_flags();
     std::vector<const char *> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17",
                                       "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
                                       "-fno-fast-math", "-fno-slp-vectorize", "-DRVCP_JIT",
@@ -329,11 +367,16 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
 {
     // Mode 2 on a scene without spheres (the Cornell frame): 6 waves per SIMD measured 2.5 %
     // faster than 5, with spheres 5 % slower (profiles/r02_legacy_waves_ab.log).
-    // RVCP_JIT_LEGACY_WAVES overrides (experiments; 0 = the compiler's choice).
+    // (debug build: RVCP_JIT_LEGACY_WAVES overrides; 0 = the compiler's choice)
     int legacy_waves = legacy && sphereless ? 6 : 0;
+#ifdef RVCP_DEBUG_KNOBS
     if (const char *e = std::getenv("RVCP_JIT_LEGACY_WAVES")) legacy_waves = std::atoi(e);
+#endif
+    std::string key_flags;
+    for (const std::string &x : jit_extra_flags()) key_flags += " " + x;
     const std::string scan = jit_scan_source(tri, n) +
-        (legacy ? "// +legacy " + std::to_string(legacy_waves) + "\n" : std::string());
+        (legacy ? "// +legacy " + std::to_string(legacy_waves) + "\n" : std::string()) +
+        (key_flags.empty() ? std::string() : "// +flags" + key_flags + "\n");
     const uint64_t h = fnv1a(scan);
     std::lock_guard<std::mutex> lock(g_mu);
     for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
@@ -373,6 +416,12 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
 }
 
 }  // namespace rvcp
+
+// Self-test hook: would upload specialise a scene with these n triangle records (1 / 0)?
+extern "C" int rvcp_internal_jit_scene_in_range(const void *tri_records, uint32_t n)
+{
+    return rvcp::jit_scene_in_range(static_cast<const rvcp::TriRecord *>(tri_records), n) ? 1 : 0;
+}
 
 // Self-test hooks for the CPU test suite (not part of rvcp.h): generate and compile the
 // specialised module for n triangle records without a GPU (`legacy`: with the mode-2 kernel).

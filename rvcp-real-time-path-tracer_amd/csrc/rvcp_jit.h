@@ -25,6 +25,11 @@ struct JitKernels {
     ~JitKernels();
 };
 
+// Every |v0| <= 2^40 and |e1|, |e2| <= 2^41 (finite): the range in which dropping the products
+// with exact-zero components cannot turn the generic test's inf * 0 = NaN into a finite value.
+bool jit_scene_in_range(const TriRecord *tri, uint32_t n);
+// Extra hipRTC options (debug build only; empty in the product library).
+std::vector<std::string> jit_extra_flags();
 // The generated scan (spec_scan1 / spec_scan2) for n triangle records.
 std::string jit_scan_source(const TriRecord *tri, uint32_t n);
 // Compile rvcp_kernels.hip with the given scan for gfx950 (hipRTC); 0 or -1 with err set.

@@ -135,9 +135,6 @@ __device__ __forceinline__ float rcp_ieee(float den) {
 // (The denominator's class is tested inside the rare branch, so the fast path costs what
 // rcp_ieee's does; a class test outside it measured 2 % slower.)
 __device__ __forceinline__ float rcp_scan(float den) {
-#ifdef RVCP_SCAN_RCP_IEEE         // A/B experiment: the plain rcp_ieee
-    return rcp_ieee(den);
-#endif
     const float r = __builtin_amdgcn_rcpf(den);
     float f = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
     if (__builtin_expect(!__builtin_amdgcn_classf(f, (1 << 8) | (1 << 3)), 0)) {
@@ -218,12 +215,16 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
 // DESIGN.md §4.7.)
 #define RVCP_SPEC_RCP(den) rcp_scan(den)
 #include RVCP_SPEC_SCAN
-// The specialised scan drops products with exact-zero triangle components, which is exact
-// only for finite rays; a wave holding any non-finite ray uses the generic loop instead.
-// (One sum: it is non-finite if any component is, and an overflowing sum of finite values
-// only sends a wave to the generic loop.)
-__device__ __forceinline__ bool ray_finite(f3 o, f3 d) {
-    return __builtin_isfinite(((o.x + o.y) + (o.z + d.x)) + (d.y + d.z));
+// The specialised scan drops products with exact-zero triangle components.  That is exact
+// when no intermediate of the generic test overflows (inf * 0 = NaN rejects there, while the
+// dropped term leaves a finite value): the host specialises a scene only when every |v0| <=
+// 2^40 and |e1|, |e2| <= 2^41 (jit_scene_in_range), and a wave uses the unrolled scan only when
+// every ray has |o|_1 <= 2^41 and |d|_1 <= 16.  Then |s| < 2^42, |s1| <= 2^46, |s2| <= 2^84,
+// |den|, |n1| < 2^90, |n2| < 2^91 and |s2.e2| < 2^127: all finite.  A NaN or infinite component
+// fails the compares, so non-finite rays take the generic loop too.  
+__device__ __forceinline__ bool ray_in_range(f3 o, f3 d) {
+    return (((__builtin_fabsf(o.x) + __builtin_fabsf(o.y)) + __builtin_fabsf(o.z)) <= 0x1p41f) &
+           (((__builtin_fabsf(d.x) + __builtin_fabsf(d.y)) + __builtin_fabsf(d.z)) <= 16.0f);
 }
 #endif
 // A necessary condition for tri_stage2 to accept, from stage 1 alone: |n1| and |n2| at most
@@ -280,19 +281,13 @@ __device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, f
 }
 
 // One leaf: its (at most kBvhLeafMax) triangles are loaded before any is tested, so the
-// leaf costs one memory round trip instead of one per triangle.  The original face id rides in
-// TriRecord::pad[0] of the leaf-ordered copy (rvcp_host.cpp).
-// RVCP_BVH_PACKED: the leaf's triangles are read from the packed copy behind the TriRecords
-// (10 floats per slot: v0, e1, e2, face id bits; leaves start at even slots, so 16-B aligned):
-// ceil(2.5 cnt) 16-B loads instead of 3 cnt.
-#ifndef RVCP_BVH_PACKED
-#define RVCP_BVH_PACKED 1
-#endif
+// leaf costs one memory round trip instead of one per triangle.  The leaf-ordered triangles
+// are packed as 10 floats per slot (v0, e1, e2, face id bits; leaves start at even slots, so
+// 16-B aligned, rvcp_host.cpp): ceil(2.5 cnt) 16-B loads.
 __device__ __forceinline__ void bvh_leaf(const TriRecord *__restrict__ btri, int32_t ref, f3 o, f3 d,
                                          float tmin, float &bt, int &best, uint32_t slots = 0) {
     const uint32_t code = ~(uint32_t)ref;
     const uint32_t first = code >> 5, cnt = (code & 31u) + 1u;
-#if RVCP_BVH_PACKED
     const float4 *base = reinterpret_cast<const float4 *>(
         reinterpret_cast<const float *>(btri + slots) + 10u * first);
     const uint32_t nld = (10u * cnt + 3u) >> 2;
@@ -319,23 +314,6 @@ __device__ __forceinline__ void bvh_leaf(const TriRecord *__restrict__ btri, int
             }
         }
     }
-#else
-    TriRecord L[kBvhLeafMax];
-#pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)kBvhLeafMax; ++k)
-        if (k < cnt) L[k] = btri[first + k];
-#pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)kBvhLeafMax; ++k) {
-        if (k < cnt) {
-            float t;
-            const int id = __float_as_int(L[k].pad[0]);
-            if (tri_accept(L[k], o, d, tmin, bt, t) && (t < bt || id > best)) {
-                bt = t;
-                best = id;
-            }
-        }
-    }
-#endif
 }
 
 __device__ __forceinline__ f3 slab_inv(f3 d) {
@@ -1237,6 +1215,7 @@ __device__ __forceinline__ void path_body(
     // this wave's index in the block, made wave-uniform (an SGPR) for the LDS row bases
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long c_start = A.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long t_exhausted = 0ull;
     // the queue runs over the pre-pass's compact list; its length is in counters[3]
     FrameArgs Q = A;
@@ -1263,9 +1242,6 @@ __device__ __forceinline__ void path_body(
     // each sample start instead of being held in 10 VGPRs for the whole pixel
     uint32_t pslot = 0, k = 0, depth = 0;
     uint32_t trav_wave = 0, iters = 0;      // wave-uniform: traversals of all lanes, iterations
-#ifdef RVCP_DEBUG_NR_HIST
-    unsigned long long nr_hist = 0;
-#endif
     float seed = 0.0f, ridx = 0.0f;
     f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
     f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0), S_alb = mk(0, 0, 0);
@@ -1322,15 +1298,6 @@ __device__ __forceinline__ void path_body(
             if (surf_ev) {                                          // :431-462
                 surf_ev = false;
                 f3 ws;
-#if RVCP_EXP_REPEAT_NEE
-                {
-                    float sd = seed, ri = ridx, dd;
-                    f3 cc, ww, ps = S_pos;
-                    asm volatile("" : "+v"(sd), "+v"(ri), "+v"(ps.x));
-                    const bool ok = nee_sample(A, lights, S_alb, ps, S_nrm, att, sd, ri, cc, dd, ww);
-                    asm volatile("" :: "v"(cc.x), "v"(cc.y), "v"(cc.z), "v"(dd), "v"(ww.x), "v"(ri), "v"(ok ? 1 : 0));
-                }
-#endif
                 if (nee_sample(A, lights, S_alb, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist,
                                ws)) {
                     a_o = add(S_pos, muls(ws, A.eps));
@@ -1347,25 +1314,8 @@ __device__ __forceinline__ void path_body(
                 if (!need_dir && !hasA) ended = true;
             }
             f3 p = mk(0, 0, 0);
-#if RVCP_EXP_REPEAT_COOP
-            {
-                float sd = seed, ri = ridx;
-                f3 pp = mk(0, 0, 0);
-                asm volatile("" : "+v"(sd), "+v"(ri));
-                coop_unit_sphere(need_dir, sd, ri, pp, lane, tail_tab[wv]);
-                asm volatile("" :: "v"(pp.x), "v"(pp.y), "v"(pp.z), "v"(ri));
-            }
-#endif
             coop_unit_sphere(need_dir, seed, ridx, p, lane, tail_tab[wv]);
             if (need_dir) {                                         // :464-478
-#if RVCP_EXP_REPEAT_BRDF
-                {
-                    f3 at2 = att, wi2, p2 = p;
-                    asm volatile("" : "+v"(p2.x), "+v"(at2.x));
-                    brdf_finish(A, S_alb, S_nrm, p2, at2, wi2);
-                    asm volatile("" :: "v"(at2.x), "v"(at2.y), "v"(at2.z), "v"(wi2.x), "v"(wi2.y), "v"(wi2.z));
-                }
-#endif
                 f3 wi;
                 brdf_finish(A, S_alb, S_nrm, p, att, wi);
                 depth += 1;
@@ -1394,12 +1344,6 @@ __device__ __forceinline__ void path_body(
             break;
         }
         if (wave_active) iters += 1;
-#ifdef RVCP_DEBUG_NR_HIST
-        {
-            const uint32_t n_r = (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
-            if (wave_active) nr_hist += n_r <= 64u ? (1ull << 42) : n_r <= 96u ? (1ull << 21) : 1ull;
-        }
-#endif
         trav_wave += (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
         if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
 
@@ -1635,7 +1579,7 @@ __device__ __forceinline__ void path_body(
             float bt = A.t_max;
             int best = -1;
 #ifdef RVCP_SPEC_SCAN
-            if (!__any(lane_r < nr && !ray_finite(o, d))) {
+            if (!__any(lane_r < nr && !ray_in_range(o, d))) {
                 spec_scan1(o, d, A.t_min, bt, best);
             } else
 #endif
@@ -1667,38 +1611,18 @@ __device__ __forceinline__ void path_body(
             }
         } else {
             // ---- scan: both rays against every triangle (wave-uniform face index) ----
-            // (RVCP_EXP_SCAN_REPEAT > 1 re-runs the scan -- same result, since a repeat
-            // re-accepts exactly the kept face -- to measure the scan's share of the frame)
-#ifndef RVCP_EXP_SCAN_REPEAT
-#define RVCP_EXP_SCAN_REPEAT 1
-#endif
 #ifdef RVCP_SPEC_SCAN
-            if (!__any((hasA && !ray_finite(a_o, a_d)) || (hasB && !ray_finite(b_o, b_d)))) {
+            if (!__any((hasA && !ray_in_range(a_o, a_d)) || (hasB && !ray_in_range(b_o, b_d)))) {
                 spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
-#if defined(RVCP_EXP_SCAN_REPEAT) && RVCP_EXP_SCAN_REPEAT > 1
-                // experiment: the scan again on laundered copies of the rays,
-                // results discarded -- its marginal cost is the scan's share of the frame
-                for (int rep = 1; rep < RVCP_EXP_SCAN_REPEAT; ++rep) {
-                    f3 ao = a_o, ad = a_d, bo = b_o, bd = b_d;
-                    asm volatile("" : "+v"(ao.x), "+v"(ao.y), "+v"(ao.z), "+v"(ad.x), "+v"(ad.y), "+v"(ad.z));
-                    asm volatile("" : "+v"(bo.x), "+v"(bo.y), "+v"(bo.z), "+v"(bd.x), "+v"(bd.y), "+v"(bd.z));
-                    float t1 = A.t_max, t2 = A.t_max;
-                    int i1 = -1, i2 = -1;
-                    spec_scan2(ao, ad, bo, bd, A.t_min, t1, i1, t2, i2);
-                    asm volatile("" :: "v"(t1), "v"(i1), "v"(t2), "v"(i2));
-                }
-#endif
             } else
 #endif
             {
-            for (int rep = 0; rep < RVCP_EXP_SCAN_REPEAT; ++rep) {
 #pragma unroll RVCP_SCAN_UNROLL
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
                 float tA, tB;
                 if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
                 if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
-            }
             }
             }
         }
@@ -1729,15 +1653,6 @@ __device__ __forceinline__ void path_body(
             } else {
                 f3 hpos, hn;
                 FaceShade fs;
-#if RVCP_EXP_REPEAT_HIT
-                {
-                    f3 hp2, hn2, bo2 = b_o;
-                    FaceShade fs2;
-                    asm volatile("" : "+v"(bo2.x));
-                    hit_shade(tri, shade, bestB, bo2, b_d, btB, hp2, hn2, fs2);
-                    asm volatile("" :: "v"(hp2.x), "v"(hn2.x), "v"(hn2.y), "v"(hn2.z), "v"(fs2.ty));
-                }
-#endif
                 hit_shade(tri, shade, bestB, b_o, b_d, btB, hpos, hn, fs);
                 if (fs.ty == kLight) {
                     ended = true;       // depth >= 1: no emission term (:426)
@@ -1752,22 +1667,16 @@ __device__ __forceinline__ void path_body(
         hasA = false;
         if (!defer_B) hasB = false;
     }
-#ifdef RVCP_DEBUG_NR_HIST
-    // experiment: wave-iterations by rays per wave, in the wave-iteration counter's place
-    // (bits 0-20: > 96 rays, 21-41: 65-96, 42-62: <= 64)
-    iters = 0;
-    flush_wave_counters(counters, lane, trav_wave, 0u);
-    if (lane == 0) atomicAdd(&counters[2], nr_hist);
-#else
     flush_wave_counters(counters, lane, trav_wave, iters);
-#endif
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;
-        unsigned long long *rec = A.timeline + 4ull * w;
+        unsigned long long *rec = A.timeline + 6ull * w;
         rec[0] = t_start;
         rec[1] = t_exhausted;
         rec[2] = __builtin_amdgcn_s_memrealtime();
         rec[3] = iters;
+        rec[4] = c_start;                              // shader-clock ticks (s_memtime)
+        rec[5] = __builtin_amdgcn_s_memtime();
     }
 }
 
@@ -2079,7 +1988,7 @@ __device__ __forceinline__ void legacy_body(
                           __all(st != L_TRACE || ((two_a >= 0x1p-30f) & (two_a <= 0x1p30f) &
                                                   (rtmin >= 0x1p-29f)));
 #ifdef RVCP_SPEC_SCAN
-        const bool spec = __all(st != L_TRACE || (ray_finite(ro, rd) && rtmin > 0.0f));
+        const bool spec = __all(st != L_TRACE || (ray_in_range(ro, rd) && rtmin > 0.0f));
 #endif
         if (st == L_TRACE) {
             trav += 1;

@@ -195,6 +195,13 @@ class RayTracer:
             ctypes.c_void_p(d_frame) if d_frame else None,
             ctypes.c_void_p(stream) if stream else None))
 
+    def gather_wait(self):
+        """rvcp_gather_wait: block until the last gather is done; returns (gather_ms,
+        render-start-to-gather-end ms) from HIP events on the gather's stream."""
+        g, f = ctypes.c_float(0.0), ctypes.c_float(0.0)
+        self._check(self._lib.rvcp_gather_wait(self._ctx, ctypes.byref(g), ctypes.byref(f)))
+        return float(g.value), float(f.value)
+
 
 def rccl_unique_id() -> bytes:
     """rvcp_rccl_unique_id (rank 0): the 128-byte RCCL communicator id."""

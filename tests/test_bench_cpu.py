@@ -46,3 +46,68 @@ def test_committed_pmc_summaries_load():
         assert traffic and traffic > 0 and src.startswith("profiles/")
         busy, frac = bench.load_valu_busy(wl, kname)
         assert 0 < busy <= 1 and 0 < frac <= 1
+
+
+def _negotiate_worker(rank, world, port, outdir):
+    """One rank of bench.py's N>1 control flow (negotiate_gather) over gloo, with the RCCL
+    calls replaced by stand-ins that fail on chosen ranks."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    results = {}
+    try:
+        for case, bad_rank, stage in [("ok", -1, ""), ("id", 3, "id"), ("init", 5, "init"),
+                                      ("probe", 7, "probe"), ("init_all", -2, "init")]:
+            inited = []
+
+            def fails(st):
+                return stage == st and (bad_rank == rank or bad_rank == -2)
+
+            def make_id():
+                if fails("id"):
+                    raise RuntimeError("cannot load librccl.so.1")
+                return bytes([rank]) * 128
+
+            def init_comm(i, uid):
+                if fails("init"):
+                    raise RuntimeError("ncclCommInitRank: unhandled system error")
+                assert uid == bytes([0]) * 128          # every rank joins rank 0's ids
+                inited.append(i)
+
+            def probe():
+                if fails("probe"):
+                    raise RuntimeError("ncclGather: internal error")
+
+            mode, why = bench.negotiate_gather(dist, rank, 2, make_id, init_comm, probe)
+            results[case] = (mode, why, inited)
+        import pickle
+        with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+            pickle.dump(results, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_negotiate_gather_world8_injected_failures(tmp_path):
+    """bench.py at N=8: a failure on ANY rank (no loadable RCCL, communicator init, the probe
+    gather) sends EVERY rank to the same host-memory gather, with the failing rank named; with
+    no failure every rank takes RCCL.  (gloo, world size 8, on CPU)"""
+    import pickle
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_negotiate_worker, args=(8, port, str(tmp_path)), nprocs=8, join=True)
+    res = []
+    for r in range(8):
+        with open(tmp_path / f"r{r}.pkl", "rb") as f:
+            res.append(pickle.load(f))
+    for r in range(8):
+        assert res[r]["ok"][0] == "rccl" and res[r]["ok"][1] is None and res[r]["ok"][2] == [0, 1]
+        for case, bad in [("id", "rank 3"), ("init", "rank 5"), ("probe", "rank 7")]:
+            mode, why, _ = res[r][case]
+            assert mode == "host" and bad in why, (r, case, why)
+        mode, why, _ = res[r]["init_all"]
+        assert mode == "host" and all(f"rank {k}" in why for k in range(8))
+    # the id failure stops before any communicator is joined
+    assert all(res[r]["id"][2] == [] for r in range(8))

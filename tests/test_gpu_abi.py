@@ -132,6 +132,42 @@ def test_gather_without_communicator(cornell):
         assert e.value.code == rvcp_amd.abi.RVCP_E_INVALID
 
 
+def test_gather_checks_the_rendered_shard(cornell):
+    """rvcp_gather_frame_async refuses to gather after a render of another shard or frame
+    size (rank 0 would assemble a scrambled frame); rvcp_gather_wait reports the gather's
+    device time and fails when no gather is in flight."""
+    torch = pytest.importorskip("torch")
+    W, H = 64, 40
+    slot = rvcp_amd.shard_rows(H, 0, 1)
+    shard = torch.zeros((slot, W), dtype=torch.int32, device="cuda")
+    gathered = torch.zeros((1, slot, W), dtype=torch.int32, device="cuda")
+    frame = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+    push = cornell.push_constant(TIME)
+    with rvcp_amd.RayTracer(spp=1) as rt:
+        rt.upload_scene(cornell)
+        rt.rccl_init(rvcp_amd.rccl_unique_id(), 1, 0)
+        with pytest.raises(rvcp_amd.abi.RvcpError) as e:
+            rt.gather_wait()
+        assert e.value.code == rvcp_amd.abi.RVCP_E_INVALID
+        rt.render_shard_async(push, W, H, 0, 2, shard.data_ptr())        # shard 0 of 2
+        rt.sync_stats()
+        with pytest.raises(rvcp_amd.abi.RvcpError) as e:
+            rt.gather_frame_async(shard.data_ptr(), W, H, gathered.data_ptr(), frame.data_ptr())
+        assert e.value.code == rvcp_amd.abi.RVCP_E_INVALID
+        big = torch.zeros((H + 8, W), dtype=torch.int32, device="cuda")
+        rt.render_shard_async(push, W, H + 8, 0, 1, big.data_ptr())      # another frame size
+        rt.sync_stats()
+        with pytest.raises(rvcp_amd.abi.RvcpError):
+            rt.gather_frame_async(shard.data_ptr(), W, H, gathered.data_ptr(), frame.data_ptr())
+        rt.render_shard_async(push, W, H, 0, 1, shard.data_ptr())
+        rt.gather_frame_async(shard.data_ptr(), W, H, gathered.data_ptr(), frame.data_ptr())
+        rt.sync_stats()
+        g_ms, f_ms = rt.gather_wait()
+        assert 0.0 <= g_ms <= f_ms
+        ref = rt.render(W, H, TIME)
+    assert np.array_equal(frame.cpu().numpy().view(np.uint8).reshape(H, W, 4), ref)
+
+
 def test_stats_report_schedule(cornell):
     """rvcp_stats_t.kernel_variant names the schedule that ran (bench.py picks the rocprof
     kernel name from it)."""

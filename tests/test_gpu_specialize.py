@@ -125,3 +125,46 @@ def test_specialised_mode2_t_min_zero_vs_oracle():
     o_lin, o_rgba, o_trav = O.render(scene_arrays(sc), sc.push_constant(TIME), cfg, 48, 40)
     assert np.array_equal(s[1].view(np.uint32), o_lin.view(np.uint32))
     assert np.array_equal(s[0], o_rgba)
+
+
+def _with_huge_wall(base, scale=1e20):
+    """The Cornell box plus a wall behind the camera (z = -1100, facing +z) whose two triangles
+    reach +-scale in x and y: paths leaving through the open side hit it at t ~ 1e3, and its
+    coordinates are far outside the specialised scan's range."""
+    ArrayMesh, VERTEX_DTYPE, FACE_DTYPE = (rvcp_amd.scene.ArrayMesh, rvcp_amd.scene.VERTEX_DTYPE,
+                                           rvcp_amd.scene.FACE_DTYPE)
+    bv = base.mesh.aligned_vertices()
+    bf = base.mesh.aligned_faces()
+    s = np.float32(scale)
+    nv = np.zeros(4, dtype=VERTEX_DTYPE)
+    nv["position"][:, :3] = np.array([[-s, -s, -1100.0], [s, -s, -1100.0], [s, s, -1100.0],
+                                      [-s, s, -1100.0]], np.float32)
+    nv["normal"][:, :3] = [0.0, 0.0, 1.0]
+    nf = np.zeros(2, dtype=FACE_DTYPE)
+    nf["vertices"] = len(bv) + np.array([[0, 1, 2], [0, 2, 3]], np.uint32)
+    nf["material_id"] = 0
+    mesh = ArrayMesh(np.concatenate([bv, nv]), np.concatenate([bf, nf]))
+    return rvcp_amd.Scene(base.camera, list(base.materials), list(base.spheres), mesh)
+
+
+@pytest.mark.parametrize("integrator", [0, 1])
+def test_out_of_range_scene_uses_generic_vs_oracle(cornell, integrator):
+    """A scene with coordinates around 1e20 (where the generic test's intermediates overflow
+    and inf * 0 = NaN decides) is not specialised (jit_scene_in_range), and its frame equals
+    the oracle's bit for bit."""
+    sc = _with_huge_wall(cornell)
+    kw = dict(spp=3, integrator=integrator)
+    W, H = 64, 48
+    s = _render(sc, W, H, **kw)
+    assert not int(s[2]["kernel_variant"]) & SPEC
+    cfg = rvcp_amd.abi.make_config(**kw)
+    o_lin, o_rgba, o_trav = O.render(scene_arrays(sc), sc.push_constant(TIME), cfg, W, H)
+    assert np.array_equal(s[1].view(np.uint32), o_lin.view(np.uint32))
+    assert np.array_equal(s[0], o_rgba) and int(s[2]["traversals"]) == int(o_trav)
+    # the same wall at 2^38 is in range: specialised, and still the oracle's frame
+    sc2 = _with_huge_wall(cornell, 2.0 ** 38)
+    s2 = _render(sc2, W, H, **kw)
+    assert int(s2[2]["kernel_variant"]) & SPEC
+    o_lin2, o_rgba2, _ = O.render(scene_arrays(sc2), sc2.push_constant(TIME), cfg, W, H)
+    assert np.array_equal(s2[1].view(np.uint32), o_lin2.view(np.uint32))
+    assert np.array_equal(s2[0], o_rgba2)

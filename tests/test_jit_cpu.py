@@ -232,3 +232,49 @@ def test_hiprtc_compiles_specialised_mode2_module():
         pytest.skip("hipRTC not installed")
     assert rc == 0, err.value.decode()
     assert size.value > 10000
+
+
+def _in_range(rec):
+    L = rvcp_amd.abi.load()
+    fn = L.rvcp_internal_jit_scene_in_range
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    return bool(fn(rec.ctypes.data, len(rec)))
+
+
+def _huge_box(scale):
+    """An axis-aligned box of side 2*scale around the origin (12 triangles, a third of their
+    edge components exact zeros), the camera inside it."""
+    s = np.float32(scale)
+    c = np.array([[x, y, z] for x in (-s, s) for y in (-s, s) for z in (-s, s)], np.float32)
+    quads = [(0, 1, 3, 2), (4, 6, 7, 5), (0, 4, 5, 1), (2, 3, 7, 6), (0, 2, 6, 4), (1, 5, 7, 3)]
+    tris = []
+    for a, b, cc, d in quads:
+        tris += [[c[a], c[b], c[cc]], [c[a], c[cc], c[d]]]
+    return np.array(tris, np.float32)
+
+
+def test_specialisation_range_guard(tmp_path):
+    """The zero-dropping premise: no intermediate of the generic test may
+    overflow, else the generic inf * 0 = NaN rejects where the dropped term does not.  Upload
+    specialises only scenes with |v0| <= 2^40 and |e1|, |e2| <= 2^41 (jit_scene_in_range); the
+    Cornell box is in range, a 1e20-scale box is routed to the generic kernels.  Inside the
+    range the generated scan stays bit-exact vs the oracle on that box scaled to 2^39."""
+    assert _in_range(_tri_records(_cornell_positions()))
+    big = _huge_box(1e20)
+    assert not _in_range(_tri_records(big))
+    assert not _in_range(_tri_records(_huge_box(2.0 ** 40.5)))
+    edge = _huge_box(2.0 ** 39)
+    assert _in_range(_tri_records(edge))
+    rng = np.random.default_rng(5)
+    rays = _adversarial_rays(edge, rng, 600)
+    lib = _build(tmp_path, _tri_records(edge), "edge")
+    _check(lib, edge, rays, tmin=0.01, tmax=1e30)
+    # outside the range the premise fails: from a point inside the 1e20 box the generic
+    # test's s2 = s x e1 overflows to inf (and inf * 0 = NaN would meet a dropped zero term)
+    T = _tri_records(big)[0]
+    o = np.float32([1.0, 2.0, -1e20 + 1e14])
+    sv = (o - T["v0"]).astype(np.float32)
+    with np.errstate(over="ignore", invalid="ignore"):
+        s2 = np.cross(sv, T["e1"]).astype(np.float32)
+    assert not np.isfinite(s2).all()

@@ -3,6 +3,8 @@
 # passes):  tools/env_ab.sh "VAR=value" ["frames.py args"]...
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# environment knobs exist only in the debug build of the library (csrc: make debug)
+export RVCP_LIB=${RVCP_LIB:-rvcp-real-time-path-tracer_amd/csrc/build/librvcp_debug.so}
 SETTING=$1; shift
 [ $# -gt 0 ] || set -- ""
 for pass in 1 2; do

@@ -4,6 +4,8 @@
 # interleaved repetitions on one box.
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# environment knobs exist only in the debug build of the library (csrc: make debug)
+export RVCP_LIB=${RVCP_LIB:-rvcp-real-time-path-tracer_amd/csrc/build/librvcp_debug.so}
 for rep in 1 2 3; do
   for w in default 0; do
     if [ $w = default ]; then env_kv=""; else env_kv="RVCP_JIT_LEGACY_WAVES=$w"; fi

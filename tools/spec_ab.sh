@@ -2,6 +2,8 @@
 # Specialised-kernel A/B: schedule 3 (5 waves) vs 6 (6 waves), generic vs specialised (§4.7).
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# environment knobs exist only in the debug build of the library (csrc: make debug)
+export RVCP_LIB=${RVCP_LIB:-rvcp-real-time-path-tracer_amd/csrc/build/librvcp_debug.so}
 for sz in "1024 30" "2048 64 6" "384 10"; do
   set -- $sz
   fr=${3:-20}

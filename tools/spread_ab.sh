@@ -4,6 +4,8 @@
 # Prints the median kernel ms of 20 frames (last 15) per setting.
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# environment knobs exist only in the debug build of the library (csrc: make debug)
+export RVCP_LIB=${RVCP_LIB:-rvcp-real-time-path-tracer_amd/csrc/build/librvcp_debug.so}
 for sz in "384 10" "256 10" "512 10" "768 10" "128 30" "1024 30"; do
   set -- $sz
   for cfg in "0 0" "0 1" "8 0" "8 1" "16 1" "24 1"; do

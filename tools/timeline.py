@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Summarise RVCP_DEBUG_TIMELINE dumps (per-wave {start, queue-exhausted, end, iterations} of
-the path kernel, s_memrealtime ticks at 100 MHz):
+"""Summarise per-wave timeline dumps of the path kernel (debug build of the library,
+RVCP_DEBUG_TIMELINE): {start, queue-exhausted, end, iterations} in s_memrealtime ticks (100 MHz)
+and {start, end} in s_memtime ticks (shader clock), so `clock_ghz` = the in-kernel clock:
 
-  RVCP_DEBUG_TIMELINE=/tmp/tl.bin python tools/frames.py --frames 3
+  RVCP_LIB=rvcp-real-time-path-tracer_amd/csrc/build/librvcp_debug.so \
+      RVCP_DEBUG_TIMELINE=/tmp/tl.bin python tools/frames.py --frames 3
   python tools/timeline.py /tmp/tl.bin --waves N
 """
 import argparse
@@ -14,11 +16,13 @@ import numpy as np
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
-    ap.add_argument("--waves", type=int, required=True, help="waves per launch")
+    ap.add_argument("--waves", type=int, required=True, help="waves per launch (file size / 48 / frames)")
     a = ap.parse_args()
-    t = np.fromfile(a.path, dtype=np.uint64).reshape(-1, a.waves, 4).astype(np.float64)
+    t = np.fromfile(a.path, dtype=np.uint64).reshape(-1, a.waves, 6).astype(np.float64)
     for k, fr in enumerate(t):
         st, ex, en, it = fr[:, 0], fr[:, 1], fr[:, 2], fr[:, 3]
+        ok = (en > st) & (fr[:, 5] > fr[:, 4])
+        ghz = (fr[ok, 5] - fr[ok, 4]) / (en[ok] - st[ok]) * 0.1
         t0 = st.min()
         span = en.max() - t0
         ex = np.where(ex > 0, ex, en)
@@ -28,7 +32,10 @@ def main():
                           "mean_residency": round(float(np.mean((en - st) / span)), 4),
                           "iters_p50": float(np.median(it)), "iters_max": float(it.max()),
                           "us_per_iter_p50": round(float(np.median((en - st)[it > 0] / it[it > 0])) / 100.0, 3),
-                          "waves_with_work": int((it > 0).sum())}))
+                          "waves_with_work": int((it > 0).sum()),
+                          "clock_ghz_p50": round(float(np.median(ghz)), 4) if ghz.size else None,
+                          "clock_ghz_p10_p90": [round(float(np.percentile(ghz, p)), 4) for p in (10, 90)]
+                          if ghz.size else None}))
 
 
 if __name__ == "__main__":

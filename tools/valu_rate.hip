@@ -79,6 +79,38 @@ __global__ void k_mov(float *out, float seed, int kIters) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
 }
 
+// In-kernel clock (MI355X_MICROARCH.md "DVFS give-back" item 6): the same streams with one
+// s_memtime / s_memrealtime stamp pair around the loop per wave; shader clock = d(memtime) /
+// d(memrealtime) x 100 MHz.  Run after the other kernels (>= 2 s of back-to-back launches).
+__global__ void k_fma_clk(float *out, float seed, int kIters, unsigned long long *st) {
+    float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+          a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const float m = 0.999f, c = 1e-3f;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < kIters; i++) { FMA8("v_fma_f32"); }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    if ((threadIdx.x & 63) == 0) {
+        const size_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+        st[2 * w] = t1 - t0;
+        st[2 * w + 1] = r1 - r0;
+    }
+}
+
+__global__ void k_fma_ic_clk(float *out, float seed, int kIters, unsigned long long *st) {
+    float a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+          a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < kIters; i++) { FMA8IC; }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    if ((threadIdx.x & 63) == 0) {
+        const size_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+        st[2 * w] = t1 - t0;
+        st[2 * w + 1] = r1 - r0;
+    }
+}
+
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 __global__ void k_pkfma(float *out, float seed, int kIters) {
@@ -148,6 +180,47 @@ static void run(const char *name, K kern, int lanes_per_instr, int flops_per_lan
                 winstr * 64 * lanes_per_instr * flops_per_lane / s * 1e-12);
 }
 
+template <typename K>
+static void run_clk(const char *name, K kern, float *out, int blocks, int threads, int kIters) {
+    const size_t waves = (size_t)blocks * threads / 64;
+    unsigned long long *st = nullptr;
+    if (hipMalloc(&st, waves * 16) != hipSuccess) return;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int r = 0; r < 20; r++) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, out, 1.0f, kIters, st);
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, out, 1.0f, kIters, st);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    unsigned long long *h = (unsigned long long *)std::malloc(waves * 16);
+    (void)hipMemcpy(h, st, waves * 16, hipMemcpyDeviceToHost);
+    double *ghz = (double *)std::malloc(waves * sizeof(double));
+    double cyc_sum = 0;
+    for (size_t w = 0; w < waves; w++) {
+        ghz[w] = h[2 * w + 1] ? (double)h[2 * w] / (double)h[2 * w + 1] * 0.1 : 0.0;
+        cyc_sum += (double)h[2 * w];
+    }
+    std::qsort(ghz, waves, sizeof(double), [](const void *x, const void *y) {
+        const double d = *(const double *)x - *(const double *)y;
+        return d < 0 ? -1 : d > 0 ? 1 : 0;
+    });
+    const double clk = ghz[waves / 2] * 1e9;
+    const double s = ms * 1e-3;
+    const double winstr = (double)waves * kIters * 8;
+    const double simds = 256.0 * 4;
+    // per SIMD: the instructions issued / the shader cycles of the kernel at the in-kernel clock
+    std::printf("%-14s %8.3f ms  in-kernel clock %.3f GHz (p10 %.3f, p90 %.3f)  "
+                "wave-instr/SIMD/shader-clk %.3f  cycles/instr %.2f\n",
+                name, s * 1e3, clk * 1e-9, ghz[waves / 10], ghz[waves * 9 / 10],
+                winstr / simds / (s * clk), simds * s * clk / winstr);
+    std::free(h);
+    std::free(ghz);
+    (void)hipFree(st);
+}
+
 int main(int argc, char **argv) {
     const int iters = argc > 1 ? std::atoi(argv[1]) : 65536;
     const int threads = 256, blocks = 256 * 8;   // 8 waves per SIMD
@@ -161,5 +234,7 @@ int main(int argc, char **argv) {
     run("v_fma_f32 ic", k_fma_ic, 1, 2, out, blocks, threads, iters);
     run("v_fma_f32 x16", k_fma16, 1, 2, out, blocks, threads, iters);
     run("v_mov_b32", k_mov, 1, 0, out, blocks, threads, iters);
+    run_clk("v_fma_f32 clk", k_fma_clk, out, blocks, threads, iters);
+    run_clk("v_fma_f32 ic clk", k_fma_ic_clk, out, blocks, threads, iters);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 2;
 }
