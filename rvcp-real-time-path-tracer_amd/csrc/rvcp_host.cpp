@@ -300,7 +300,8 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     if (cfg->integrator != RVCP_INTEGRATOR_GAMES101 && cfg->integrator != RVCP_INTEGRATOR_LEGACY)
         return fail(nullptr, RVCP_E_UNSUPPORTED, "unsupported integrator");
     if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
-    if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant)
+    if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant || cfg->kernel_variant == 7 ||
+        cfg->kernel_variant == 8)
         return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
     if (cfg->n_gpus < 0 || cfg->n_gpus > 64)
         return fail(nullptr, RVCP_E_INVALID, "n_gpus must be in [0, 64]");
@@ -365,6 +366,7 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     const int cap = cap_env ? std::atoi(cap_env) : 0;
     ctx->n_simds = (uint32_t)cus * 4u;
     for (int v = 1; v <= kMaxVariant; v++) {
+        if (v == 7 || v == 8) continue;
         int per_cu = 0;
         if (rvcp_games101_occupancy(v, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
         if (cap > 0 && cap < per_cu) per_cu = cap;
@@ -681,7 +683,8 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             // upload compiled one; its exactness argument needs t_min > 0
             const JitKernels *jk = ctx->jit.get();
             const int jit_per_cu = !jk ? 0 : A.variant == 6 ? jk->blocks_per_cu6
-                                 : A.variant == 3 ? jk->blocks_per_cu5 : 0;
+                                 : A.variant == 3 ? jk->blocks_per_cu5
+                                 : A.variant == kPoolVariant ? jk->blocks_per_cu_pool : 0;
             const bool spec = !legacy && !A.accel && jit_per_cu > 0 && A.t_min > 0.0f;
             // mode 2 with the specialised triangle scan (its kernel also checks per wave
             // that every ray is finite and has t_min > 0)
@@ -693,8 +696,9 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             if (spec_legacy) cap = (uint32_t)jk->blocks_per_cu_legacy * (ctx->n_simds / 4u);
             A.n_simds = ctx->n_simds;
             uint32_t waves = 0, chunk = 0;
-            rvcp_static_split(A.n_pixels, cap * (kBlock / kWave), A.n_simds, &waves, &chunk);
-            uint32_t blocks = (waves + (kBlock / kWave) - 1) / (kBlock / kWave);
+            const uint32_t wpb = (uint32_t)((legacy || A.accel ? kBlock : variant_block(A.variant)) / kWave);
+            rvcp_static_split(A.n_pixels, cap * wpb, A.n_simds, &waves, &chunk);
+            uint32_t blocks = (waves + wpb - 1) / wpb;
             if (blocks > cap) blocks = cap;
             if (blocks == 0) blocks = 1;
             A.static_chunk = chunk;
@@ -718,7 +722,7 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             if (A.spread_min && !legacy && !A.accel && (A.variant == 3 || A.variant == 6)) blocks = cap;
             ctx->last_timeline_waves = 0;
             if (RVCP_KNOB("RVCP_DEBUG_TIMELINE") && !legacy && A.variant >= 3) {
-                const size_t waves = (size_t)blocks * (kBlock / kWave);
+                const size_t waves = (size_t)blocks * wpb;
                 if (ctx->cap_timeline < waves) {
                     (void)hipFree(ctx->d_timeline);
                     ctx->d_timeline = nullptr;
@@ -750,7 +754,9 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                                              ctx->d_counters, ctx->d_surf, ctx->d_shade,
                                              ctx->d_bvh_nodes, ctx->d_bvh_tris,
                                              blocks, s, ctx->evm,
-                                             spec ? (void *)(A.variant == 6 ? jk->path6 : jk->path5)
+                                             spec ? (void *)(A.variant == 6 ? jk->path6
+                                                             : A.variant == kPoolVariant ? jk->pool
+                                                             : jk->path5)
                                                   : nullptr);
                 if (spec) ctx->last_spec = true;
             } else {

@@ -675,7 +675,7 @@ struct Queue {
 
 __device__ __forceinline__ Queue queue_init(const FrameArgs &A) {
     const uint32_t wave_global =
-        __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) / kWave);
+        __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) / kWave);
     Queue q;
     q.next = wave_global * A.static_chunk;
     q.end = q.next + A.static_chunk;
@@ -1197,8 +1197,11 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 #endif
 // LDS_STATE: the light sample's pending state (a_p, nee_C, nee_dist: written at the surface
 // event, read when the shadow ray resolves) and the pixel's running sum `acc` live in this
-// lane's column of an LDS block (SoA, stride kBlock) instead of 10 VGPRs across the scan.
-template <bool TILED, bool BVH, bool SINGLE = false, bool LDS_STATE = false>
+// lane's column of an LDS block (SoA, stride = the block size) instead of 10 VGPRs across the
+// scan.
+// POOL_W > 0 (schedule 9): the workgroup of POOL_W waves pools its rays in LDS every iteration
+// and scans them in full 64-ray passes shared out over its waves (see the POOL_W branch).
+template <bool TILED, bool BVH, bool SINGLE = false, bool LDS_STATE = false, int POOL_W = 0>
 __device__ __forceinline__ void path_body(
     const FrameArgs &A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
@@ -1206,11 +1209,13 @@ __device__ __forceinline__ void path_body(
     unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
     const FaceShade *__restrict__ shade, uint8_t (*tail_tab)[kWave], TriRecord *tile,
     const Bvh4Node *__restrict__ bvh_nodes = nullptr, const TriRecord *__restrict__ bvh_tris = nullptr,
-    int32_t *bvh_stack = nullptr, float4 *compact_lds = nullptr, float *state_lds = nullptr)
+    int32_t *bvh_stack = nullptr, float4 *compact_lds = nullptr, float *state_lds = nullptr,
+    float4 *pool = nullptr, uint32_t *pool_count = nullptr)
 {
-    float *const st = LDS_STATE ? state_lds + threadIdx.x : nullptr;   // st[f * kBlock]
-    auto st_put3 = [&](int f, f3 v) { st[f * kBlock] = v.x; st[(f + 1) * kBlock] = v.y; st[(f + 2) * kBlock] = v.z; };
-    auto st_get3 = [&](int f) { return mk(st[f * kBlock], st[(f + 1) * kBlock], st[(f + 2) * kBlock]); };
+    constexpr int BLK = POOL_W ? POOL_W * kWave : kBlock;     // threads per workgroup
+    float *const st = LDS_STATE ? state_lds + threadIdx.x : nullptr;   // st[f * BLK]
+    auto st_put3 = [&](int f, f3 v) { st[f * BLK] = v.x; st[(f + 1) * BLK] = v.y; st[(f + 2) * BLK] = v.z; };
+    auto st_get3 = [&](int f) { return mk(st[f * BLK], st[(f + 1) * BLK], st[(f + 2) * BLK]); };
     const uint32_t lane = lane_id();
     // this wave's index in the block, made wave-uniform (an SGPR) for the LDS row bases
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1222,7 +1227,7 @@ __device__ __forceinline__ void path_body(
     Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
     {   // static chunks over the surface list, same rule as the host's (static_split)
         uint32_t waves, c;
-        const uint32_t grid_waves = gridDim.x * (kBlock / kWave);
+        const uint32_t grid_waves = gridDim.x * (BLK / kWave);
         static_split(Q.n_pixels, grid_waves, A.n_simds, waves, c);
         if (A.spread_min && Q.n_pixels <= grid_waves * kChunk) {
             // small frame: every resident wave gets a share (latency hiding over lane count)
@@ -1307,7 +1312,7 @@ __device__ __forceinline__ void path_body(
                     if (LDS_STATE) {
                         st_put3(0, a_p);
                         st_put3(3, nee_C);
-                        st[6 * kBlock] = nee_dist;
+                        st[6 * BLK] = nee_dist;
                     }
                 }
                 need_dir = !(rnd(seed, ridx) > A.rr);               // Russian roulette :462
@@ -1337,7 +1342,23 @@ __device__ __forceinline__ void path_body(
         const f3 s_ad = (SINGLE && !hasA) ? b_d : a_d;
         const uint64_t mA = __ballot(sA), mB = __ballot(sB);
         const bool wave_active = (mA | mB) != 0ull;
-        if (TILED) {
+        // POOL_W: this wave's first slot in the workgroup's ray pool and the pool's size R
+        uint32_t pool_base = 0, pool_R = 0;
+        if (POOL_W) {
+            // every wave of the workgroup takes part in every iteration until the whole group
+            // has no ray left (the pool is filled and scanned between workgroup barriers)
+            if (lane == 0) pool_count[wv] = (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
+            __syncthreads();
+#pragma unroll
+            for (int v = 0; v < POOL_W; ++v) {
+                const uint32_t c = pool_count[v];
+                pool_base += (uint32_t)v < wv ? c : 0u;
+                pool_R += c;
+            }
+            pool_base = __builtin_amdgcn_readfirstlane(pool_base);
+            pool_R = __builtin_amdgcn_readfirstlane(pool_R);
+            if (pool_R == 0u) break;
+        } else if (TILED) {
             // every wave of the workgroup keeps loading tiles until the whole group is done
             if (!__syncthreads_or(wave_active ? 1 : 0)) break;
         } else if (!wave_active) {
@@ -1351,8 +1372,120 @@ __device__ __forceinline__ void path_body(
         float btA = A.t_max, btB = A.t_max;
         const uint32_t na = (uint32_t)__builtin_popcountll(mA);
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
-        const bool tail = wave_active && (q.exhausted || A.early_tail) && nr <= kWave / 2 && !BVH;
-        if (TILED) {
+        const bool tail = wave_active && (q.exhausted || A.early_tail) && nr <= kWave / 2 && !BVH &&
+                          !POOL_W;
+        if (POOL_W) {
+            // ---- workgroup ray pool (schedule 9) ----
+            // Ray j of the pool: the waves' A rays (lane order), then their B rays, wave by wave.
+            // Each slot is two float4s: (o, t) and (d, face).  The R rays are scanned in
+            // ceil(R / 64) full passes of 64, pass p by wave p mod POOL_W (a wave with two
+            // passes scans them as the two rays of the dual scan), so a workgroup scans what it
+            // holds instead of two slots per lane whether or not they hold a ray; when R is at
+            // most half the workgroup's lanes, every ray gets K >= 2 lanes that scan every K-th
+            // triangle (the tail partition, combined with the scan's order rule).  Each ray
+            // meets the same triangles with the same test wherever it is scanned, so every
+            // nearest hit is unchanged.
+            const uint32_t jA = pool_base + rank_in(mA), jB = pool_base + na + rank_in(mB);
+            if (sA) {
+                pool[2 * jA] = make_float4(s_ao.x, s_ao.y, s_ao.z, 0.0f);
+                pool[2 * jA + 1] = make_float4(s_ad.x, s_ad.y, s_ad.z, 0.0f);
+            }
+            if (sB) {
+                pool[2 * jB] = make_float4(b_o.x, b_o.y, b_o.z, 0.0f);
+                pool[2 * jB + 1] = make_float4(b_d.x, b_d.y, b_d.z, 0.0f);
+            }
+            __syncthreads();
+            float *const poolf = reinterpret_cast<float *>(pool);
+            if (pool_R * 2u <= (uint32_t)(POOL_W * kWave)) {
+                // tail partition over the whole workgroup: K lanes per ray (power of two <= 64)
+                uint32_t lgK = 1;
+                while (lgK < 6u && (pool_R << (lgK + 1)) <= (uint32_t)(POOL_W * kWave)) lgK += 1;
+                const uint32_t K = 1u << lgK;
+                const uint32_t g = wv * kWave + lane;
+                const uint32_t j = g >> lgK, part = g & (K - 1u);
+                const bool worker = j < pool_R;
+                float bt = A.t_max;
+                int best = -1;
+                if (worker) {
+                    const float4 ro = pool[2 * j], rd = pool[2 * j + 1];
+                    const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
+                    for (uint32_t i = part; i < A.n_faces; i += K) {
+                        float t;
+                        if (tri_accept(tri[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
+                    }
+                }
+                for (uint32_t off = K >> 1; off >= 1; off >>= 1) {
+                    const float ot = __shfl_xor(bt, (int)off);
+                    const int ob = __shfl_xor(best, (int)off);
+                    if (ot < bt || (ot == bt && ob > best)) { bt = ot; best = ob; }
+                }
+                if (worker && part == 0u) {
+                    poolf[8 * j + 3] = bt;
+                    poolf[8 * j + 7] = __int_as_float(best);
+                }
+            } else {
+                const uint32_t P = (pool_R + (uint32_t)kWave - 1u) / (uint32_t)kWave;
+                const uint32_t p0 = wv, p1 = wv + POOL_W;          // this wave's passes
+                if (p0 < P) {
+                    const bool two = p1 < P;
+                    const uint32_t j0 = p0 * kWave + lane, j1 = p1 * kWave + lane;
+                    const bool v0 = j0 < pool_R, v1 = two && j1 < pool_R;
+                    // (slots beyond R hold stale rays: scanned, never read back)
+                    const float4 o0r = pool[2 * j0], d0r = pool[2 * j0 + 1];
+                    const float4 o1r = two ? pool[2 * j1] : o0r, d1r = two ? pool[2 * j1 + 1] : d0r;
+                    const f3 o0 = mk(o0r.x, o0r.y, o0r.z), d0 = mk(d0r.x, d0r.y, d0r.z);
+                    const f3 o1 = mk(o1r.x, o1r.y, o1r.z), d1 = mk(d1r.x, d1r.y, d1r.z);
+                    float bt0 = A.t_max, bt1 = A.t_max;
+                    int best0 = -1, best1 = -1;
+#ifdef RVCP_SPEC_SCAN
+                    if (!__any((v0 && !ray_in_range(o0, d0)) || (v1 && !ray_in_range(o1, d1)))) {
+                        if (two) spec_scan2(o0, d0, o1, d1, A.t_min, bt0, best0, bt1, best1);
+                        else spec_scan1(o0, d0, A.t_min, bt0, best0);
+                    } else
+#endif
+                    if (two) {
+#pragma unroll RVCP_SCAN_UNROLL
+                        for (uint32_t i = 0; i < A.n_faces; ++i) {
+                            const TriRecord T = tri[i];
+                            float t0, t1;
+                            if (tri_accept(T, o0, d0, A.t_min, bt0, t0)) { bt0 = t0; best0 = (int)i; }
+                            if (tri_accept(T, o1, d1, A.t_min, bt1, t1)) { bt1 = t1; best1 = (int)i; }
+                        }
+                    } else {
+#pragma unroll RVCP_SCAN_UNROLL
+                        for (uint32_t i = 0; i < A.n_faces; ++i) {
+                            float t0;
+                            if (tri_accept(tri[i], o0, d0, A.t_min, bt0, t0)) { bt0 = t0; best0 = (int)i; }
+                        }
+                    }
+                    if (v0) {
+                        poolf[8 * j0 + 3] = bt0;
+                        poolf[8 * j0 + 7] = __int_as_float(best0);
+                    }
+                    if (v1) {
+                        poolf[8 * j1 + 3] = bt1;
+                        poolf[8 * j1 + 7] = __int_as_float(best1);
+                    }
+                }
+            }
+            __syncthreads();
+            // read back this lane's rays with their results: the rays come from LDS rather
+            // than being held in registers across the scan, so they are loaded by every lane
+            // (a lane without the ray reads an in-bounds slot it never uses) -- a conditional
+            // load would keep the old registers live through the scan
+            {
+                const uint32_t cap = (uint32_t)(POOL_W * 2 * kWave) - 1u;
+                const uint32_t ia = jA < cap ? jA : cap, ib = jB < cap ? jB : cap;
+                const float4 ra = pool[2 * ia], rda = pool[2 * ia + 1];
+                const float4 rb = pool[2 * ib], rdb = pool[2 * ib + 1];
+                a_o = mk(ra.x, ra.y, ra.z);
+                a_d = mk(rda.x, rda.y, rda.z);
+                b_o = mk(rb.x, rb.y, rb.z);
+                b_d = mk(rdb.x, rdb.y, rdb.z);
+                if (sA) { btA = ra.w; bestA = __float_as_int(rda.w); }
+                if (sB) { btB = rb.w; bestB = __float_as_int(rdb.w); }
+            }
+        } else if (TILED) {
             // ---- LDS-tiled scan (optionally with the tail partition below) ----
             uint32_t R = 1, part = 0;
             bool worker = false;
@@ -1637,7 +1770,7 @@ __device__ __forceinline__ void path_body(
             if (LDS_STATE) {
                 a_p = st_get3(0);
                 nee_C = st_get3(3);
-                nee_dist = st[6 * kBlock];
+                nee_dist = st[6 * BLK];
             }
             const f3 hp = bestA >= 0 ? add(a_o, muls(a_d, btA))
                                      : mk(__builtin_inff(), __builtin_inff(), __builtin_inff());
@@ -1669,7 +1802,7 @@ __device__ __forceinline__ void path_body(
     }
     flush_wave_counters(counters, lane, trav_wave, iters);
     if (A.timeline && lane == 0) {
-        const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;
+        const uint32_t w = (blockIdx.x * BLK + threadIdx.x) / kWave;
         unsigned long long *rec = A.timeline + 6ull * w;
         rec[0] = t_start;
         rec[1] = t_exhausted;
@@ -1698,6 +1831,24 @@ __global__ __launch_bounds__(kBlock, MIN_WAVES) void games101_path_kernel(
     path_body<false, false, false, RVCP_STATE_LDS != 0>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+}
+
+// Schedule 9: schedule 3 with the workgroup ray pool (path_body POOL_W): workgroups of
+// kPoolWaves waves, 5 waves per SIMD.
+__global__ __launch_bounds__(kPoolWaves * kWave, RVCP_PATH_MIN_WAVES) void games101_pool_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade)
+{
+    __shared__ uint8_t tail_tab[kPoolWaves][kWave];
+    __shared__ float state_lds[10 * kPoolWaves * kWave];
+    __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
+    __shared__ uint32_t pool_count[kPoolWaves];
+    path_body<false, false, false, true, kPoolWaves>(
+        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
+        nullptr, nullptr, nullptr, nullptr, nullptr, state_lds, pool, pool_count);
 }
 
 // Opt-in BVH (RVCP_ACCEL_BVH): the variant-3 machine with per-lane BVH traversal in place of
@@ -2128,6 +2279,21 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void rvcp_s
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
 }
+extern "C" __global__ __launch_bounds__(kPoolWaves * kWave, RVCP_PATH_MIN_WAVES) void rvcp_spec_pool_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade)
+{
+    __shared__ uint8_t tail_tab[kPoolWaves][kWave];
+    __shared__ float state_lds[10 * kPoolWaves * kWave];
+    __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
+    __shared__ uint32_t pool_count[kPoolWaves];
+    path_body<false, false, false, true, kPoolWaves>(
+        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
+        nullptr, nullptr, nullptr, nullptr, nullptr, state_lds, pool, pool_count);
+}
 extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
@@ -2186,13 +2352,18 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
         rvcp::FrameArgs a = *args;
         void *params[] = {&a, &tri, &mats, &lights, &gamma_t, &out_rgba, &out_lin, &counters,
                           &surf, &shade};
-        if (hipModuleLaunchKernel((hipFunction_t)spec_path_fn, grid_blocks, 1, 1, rvcp::kBlock,
+        const unsigned bs = args->variant == 9 ? rvcp::kPoolWaves * rvcp::kWave : rvcp::kBlock;
+        if (hipModuleLaunchKernel((hipFunction_t)spec_path_fn, grid_blocks, 1, 1, bs,
                                   1, 1, 0, (hipStream_t)stream, params, nullptr) != hipSuccess)
             return -2;
     } else if (args->accel)
         hipLaunchKernelGGL(rvcp::games101_bvh_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade, bvh_nodes, bvh_tris);
+    else if (args->variant == 9)
+        hipLaunchKernelGGL(rvcp::games101_pool_kernel, dim3(grid_blocks), dim3(rvcp::kPoolWaves * rvcp::kWave), 0,
+                           (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
+                           out_lin, counters, surf, shade);
     else if (args->variant == 5)
         hipLaunchKernelGGL(rvcp::games101_tiled_single_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
@@ -2244,6 +2415,8 @@ extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_single_kernel, rvcp::kBlock, 0)
         : variant == 4
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_kernel, rvcp::kBlock, 0)
+        : variant == 9
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_pool_kernel, rvcp::kPoolWaves * rvcp::kWave, 0)
         : variant == 6
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel<6>, rvcp::kBlock, 0)
         : variant == 3
