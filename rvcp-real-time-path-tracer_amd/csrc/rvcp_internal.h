@@ -21,7 +21,7 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 // schedule 9 (workgroup ray pool): waves per workgroup
 #ifndef RVCP_POOL_WAVES
-#define RVCP_POOL_WAVES 5
+#define RVCP_POOL_WAVES 4
 #endif
 constexpr int kPoolWaves = RVCP_POOL_WAVES;
 // Pixels a wave takes from the frame queue per atomic.

@@ -1255,6 +1255,7 @@ __device__ __forceinline__ void path_body(
     float nee_dist = 0.0f;
     bool hasB = false;
     f3 b_o = mk(0, 0, 0), b_d = mk(0, 0, 1);
+    uint32_t pool_iter = 0;              // POOL_W: the workgroup's iteration (wave-uniform)
 
     for (;;) {
         // ---- settle: end samples, take pixels, emit surface events ----
@@ -1342,22 +1343,44 @@ __device__ __forceinline__ void path_body(
         const f3 s_ad = (SINGLE && !hasA) ? b_d : a_d;
         const uint64_t mA = __ballot(sA), mB = __ballot(sB);
         const bool wave_active = (mA | mB) != 0ull;
-        // POOL_W: this wave's first slot in the workgroup's ray pool and the pool's size R
-        uint32_t pool_base = 0, pool_R = 0;
+        // POOL_W: this wave's first A and B slots in the workgroup's ray pool, the pool's size
+        // R, its A rays RA, and the pool slots scanned this iteration (pool_cut; the B rays
+        // beyond it wait for the next iteration)
+        uint32_t pool_baseA = 0, pool_baseB = 0, pool_R = 0, pool_RA = 0, pool_cut = 0;
         if (POOL_W) {
             // every wave of the workgroup takes part in every iteration until the whole group
             // has no ray left (the pool is filled and scanned between workgroup barriers)
-            if (lane == 0) pool_count[wv] = (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
+            if (lane == 0) {
+                pool_count[2 * wv] = (uint32_t)__builtin_popcountll(mA);
+                pool_count[2 * wv + 1] = (uint32_t)__builtin_popcountll(mB);
+            }
             __syncthreads();
+            // A rays wave by wave, then B rays wave by wave starting at wave pool_iter mod W
+            // (the rotation spreads the deferred B rays over the waves)
+            const uint32_t rot = pool_iter % (uint32_t)POOL_W;
+            const uint32_t my_pos = (wv + (uint32_t)POOL_W - rot) % (uint32_t)POOL_W;
+            uint32_t RB = 0;
 #pragma unroll
             for (int v = 0; v < POOL_W; ++v) {
-                const uint32_t c = pool_count[v];
-                pool_base += (uint32_t)v < wv ? c : 0u;
-                pool_R += c;
+                const uint32_t ca = pool_count[2 * v], cb = pool_count[2 * v + 1];
+                const uint32_t pos = ((uint32_t)v + (uint32_t)POOL_W - rot) % (uint32_t)POOL_W;
+                pool_baseA += (uint32_t)v < wv ? ca : 0u;
+                pool_baseB += pos < my_pos ? cb : 0u;
+                pool_RA += ca;
+                RB += cb;
             }
-            pool_base = __builtin_amdgcn_readfirstlane(pool_base);
-            pool_R = __builtin_amdgcn_readfirstlane(pool_R);
+            pool_R = __builtin_amdgcn_readfirstlane(pool_RA + RB);
+            pool_RA = __builtin_amdgcn_readfirstlane(pool_RA);
+            pool_baseA = __builtin_amdgcn_readfirstlane(pool_baseA);
+            pool_baseB = __builtin_amdgcn_readfirstlane(pool_baseB + pool_RA);
             if (pool_R == 0u) break;
+            pool_iter += 1u;
+            // full passes only: floor(R / 64) passes (but every A ray), the rest waits; a
+            // small pool (the tail partition below) is scanned whole
+            const bool part_mode = pool_R * 2u <= (uint32_t)(POOL_W * kWave);
+            const uint32_t pf = pool_R / (uint32_t)kWave, pa = (pool_RA + (uint32_t)kWave - 1u) / (uint32_t)kWave;
+            pool_cut = part_mode ? pool_R : (pf > pa ? pf : pa) * (uint32_t)kWave;
+            if (pool_cut > pool_R) pool_cut = pool_R;
         } else if (TILED) {
             // every wave of the workgroup keeps loading tiles until the whole group is done
             if (!__syncthreads_or(wave_active ? 1 : 0)) break;
@@ -1365,27 +1388,35 @@ __device__ __forceinline__ void path_body(
             break;
         }
         if (wave_active) iters += 1;
-        trav_wave += (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
+        if (POOL_W)   // a deferred B ray is counted when it is scanned
+            trav_wave += (uint32_t)__builtin_popcountll(mA) +
+                         (uint32_t)__builtin_popcountll(__ballot(sB && pool_baseB + rank_in(mB) < pool_cut));
+        else
+            trav_wave += (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
         if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
 
         int bestA = -1, bestB = -1;
         float btA = A.t_max, btB = A.t_max;
+        bool pool_deferB = false;
         const uint32_t na = (uint32_t)__builtin_popcountll(mA);
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
         const bool tail = wave_active && (q.exhausted || A.early_tail) && nr <= kWave / 2 && !BVH &&
                           !POOL_W;
         if (POOL_W) {
             // ---- workgroup ray pool (schedule 9) ----
-            // Ray j of the pool: the waves' A rays (lane order), then their B rays, wave by wave.
-            // Each slot is two float4s: (o, t) and (d, face).  The R rays are scanned in
-            // ceil(R / 64) full passes of 64, pass p by wave p mod POOL_W (a wave with two
-            // passes scans them as the two rays of the dual scan), so a workgroup scans what it
-            // holds instead of two slots per lane whether or not they hold a ray; when R is at
-            // most half the workgroup's lanes, every ray gets K >= 2 lanes that scan every K-th
-            // triangle (the tail partition, combined with the scan's order rule).  Each ray
-            // meets the same triangles with the same test wherever it is scanned, so every
-            // nearest hit is unchanged.
-            const uint32_t jA = pool_base + rank_in(mA), jB = pool_base + na + rank_in(mB);
+            // Ray j of the pool: the waves' A (shadow) rays, wave by wave in lane order, then
+            // their B (path) rays.  Each slot is two float4s: (o, t) and (d, face).  The first
+            // pool_cut rays -- floor(R / 64) full passes of 64, at least every A ray -- are
+            // scanned, pass p by wave p mod POOL_W (a wave with two passes scans them as the two
+            // rays of the dual scan); the B rays beyond the cut wait for the next iteration
+            // (their lanes resolve the shadow ray and start no new event meanwhile).  So the
+            // workgroup scans full passes instead of two slots per lane whether or not they
+            // hold a ray.  When R is at most half the workgroup's lanes, every ray gets K >= 2
+            // lanes that scan every K-th triangle (the tail partition, combined with the scan's
+            // order rule).  Each ray meets the same triangles with the same test wherever and
+            // whenever it is scanned, so every nearest hit is unchanged.
+            const uint32_t jA = pool_baseA + rank_in(mA), jB = pool_baseB + rank_in(mB);
+            pool_deferB = jB >= pool_cut;
             if (sA) {
                 pool[2 * jA] = make_float4(s_ao.x, s_ao.y, s_ao.z, 0.0f);
                 pool[2 * jA + 1] = make_float4(s_ad.x, s_ad.y, s_ad.z, 0.0f);
@@ -1396,7 +1427,7 @@ __device__ __forceinline__ void path_body(
             }
             __syncthreads();
             float *const poolf = reinterpret_cast<float *>(pool);
-            if (pool_R * 2u <= (uint32_t)(POOL_W * kWave)) {
+            if (pool_cut == pool_R && pool_R * 2u <= (uint32_t)(POOL_W * kWave)) {
                 // tail partition over the whole workgroup: K lanes per ray (power of two <= 64)
                 uint32_t lgK = 1;
                 while (lgK < 6u && (pool_R << (lgK + 1)) <= (uint32_t)(POOL_W * kWave)) lgK += 1;
@@ -1424,13 +1455,13 @@ __device__ __forceinline__ void path_body(
                     poolf[8 * j + 7] = __int_as_float(best);
                 }
             } else {
-                const uint32_t P = (pool_R + (uint32_t)kWave - 1u) / (uint32_t)kWave;
+                const uint32_t P = pool_cut / (uint32_t)kWave + (pool_cut % (uint32_t)kWave != 0u);
                 const uint32_t p0 = wv, p1 = wv + POOL_W;          // this wave's passes
                 if (p0 < P) {
                     const bool two = p1 < P;
                     const uint32_t j0 = p0 * kWave + lane, j1 = p1 * kWave + lane;
-                    const bool v0 = j0 < pool_R, v1 = two && j1 < pool_R;
-                    // (slots beyond R hold stale rays: scanned, never read back)
+                    const bool v0 = j0 < pool_cut, v1 = two && j1 < pool_cut;
+                    // (slots beyond the cut hold stale or waiting rays: scanned, never read back)
                     const float4 o0r = pool[2 * j0], d0r = pool[2 * j0 + 1];
                     const float4 o1r = two ? pool[2 * j1] : o0r, d1r = two ? pool[2 * j1 + 1] : d0r;
                     const f3 o0 = mk(o0r.x, o0r.y, o0r.z), d0 = mk(d0r.x, d0r.y, d0r.z);
@@ -1778,7 +1809,9 @@ __device__ __forceinline__ void path_body(
             if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) col = add(col, nee_C);
         }
         // ---- resolve B: next bounce (:421-429) ----
-        const bool defer_B = SINGLE && hasA && hasB;    // B was not traced this iteration
+        // B was not traced this iteration: SINGLE traces A first; POOL_W defers the B rays
+        // beyond the pool's cut
+        const bool defer_B = (SINGLE && hasA && hasB) || (POOL_W && hasB && pool_deferB);
         if (hasB && !defer_B) {
             if (bestB < 0) {
                 col = add(col, mk(0.1f, 0.1f, 0.1f));

@@ -22,12 +22,13 @@ def main():
     ap.add_argument("--integrator", type=int, default=0)
     ap.add_argument("--accel", type=int, default=0)
     ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres"])
+    ap.add_argument("--generic", action="store_true", help="specialize = OFF (generic scan)")
     a = ap.parse_args()
     sc = rvcp_amd.Scene.default() if a.scene == "cornell" else rvcp_amd.scene.sphere_scene()
     if a.tris:
         sc = rvcp_amd.scene.with_random_triangles(sc, a.tris)
     with rvcp_amd.RayTracer(spp=a.spp, kernel_variant=a.variant, integrator=a.integrator,
-                            accel=a.accel) as rt:
+                            accel=a.accel, specialize=1 if a.generic else 0) as rt:
         rt.upload_scene(sc)
         for _ in range(a.frames):
             rt.render(a.size, a.size, 123.0)
