@@ -24,6 +24,9 @@ constexpr int kBlock = 256;
 #define RVCP_POOL_WAVES 4
 #endif
 constexpr int kPoolWaves = RVCP_POOL_WAVES;
+// LDS state columns of the path kernels (path_body LDS_STATE): a_p 0-2, nee_C 3-5, nee_dist 6,
+// acc 7-9, att 10-12, col 13-15
+constexpr int kStateCols = 16;
 // Pixels a wave takes from the frame queue per atomic.
 constexpr uint32_t kChunk = 64;
 // Small frames: the grid is sized so that a wave starts with at least kMinStatic pixels, and

@@ -1272,7 +1272,9 @@ __device__ __forceinline__ void path_body(
                 } else {
                     depth = 0;
                     att = mk(1, 1, 1);
+                    if (LDS_STATE) st_put3(10, att);
                     col = mk(0, 0, 0);
+                    if (LDS_STATE) st_put3(13, col);
                     const SurfRecord r = surf[pslot];
                     S_pos = ld3(r.pos); S_nrm = ld3(r.nrm); S_alb = ld3(r.alb_pi);
                     surf_ev = true;
@@ -1292,7 +1294,9 @@ __device__ __forceinline__ void path_body(
                     if (LDS_STATE) st_put3(7, acc);
                     depth = 0;
                     att = mk(1, 1, 1);
+                    if (LDS_STATE) st_put3(10, att);
                     col = mk(0, 0, 0);
+                    if (LDS_STATE) st_put3(13, col);
                     S_pos = ld3(r.pos); S_nrm = ld3(r.nrm); S_alb = ld3(r.alb_pi);
                     need_pixel = false;
                     surf_ev = true;
@@ -1303,6 +1307,7 @@ __device__ __forceinline__ void path_body(
             bool need_dir = false;
             if (surf_ev) {                                          // :431-462
                 surf_ev = false;
+                if (LDS_STATE) att = st_get3(10);
                 f3 ws;
                 if (nee_sample(A, lights, S_alb, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist,
                                ws)) {
@@ -1324,6 +1329,7 @@ __device__ __forceinline__ void path_body(
             if (need_dir) {                                         // :464-478
                 f3 wi;
                 brdf_finish(A, S_alb, S_nrm, p, att, wi);
+                if (LDS_STATE) st_put3(10, att);
                 depth += 1;
                 if (!(depth >= A.max_bounces || att_stop(A, att))) {
                     b_o = add(S_pos, muls(wi, A.eps));
@@ -1333,6 +1339,15 @@ __device__ __forceinline__ void path_body(
                 if (!hasA && !hasB) ended = true;
             }
             if (!__any(ended)) break;
+        }
+        // The shading point is dead until the next surface event sets it again (resolve B, or
+        // a sample / pixel start): say so, so that it is not held in 9 VGPRs across the scan.
+        S_pos = mk(0, 0, 0);
+        S_nrm = mk(0, 0, 0);
+        S_alb = mk(0, 0, 0);
+        if (LDS_STATE) {       // likewise the attenuation and the sample's colour (LDS columns)
+            att = mk(0, 0, 0);
+            col = mk(0, 0, 0);
         }
         // The scan's view of the lane's rays.  SINGLE (variant 5): one ray per lane per
         // iteration -- the shadow ray A while it is pending, else the path ray B; a B left
@@ -1797,6 +1812,7 @@ __device__ __forceinline__ void path_body(
         }
 
         // ---- resolve A: visibility of the light sample (:447-459) ----
+        if (LDS_STATE) col = st_get3(13);
         if (hasA) {
             if (LDS_STATE) {
                 a_p = st_get3(0);
@@ -1806,7 +1822,10 @@ __device__ __forceinline__ void path_body(
             const f3 hp = bestA >= 0 ? add(a_o, muls(a_d, btA))
                                      : mk(__builtin_inff(), __builtin_inff(), __builtin_inff());
             const float dist_blocked = len(sub(hp, a_p));
-            if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) col = add(col, nee_C);
+            if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) {
+                col = add(col, nee_C);
+                if (LDS_STATE) st_put3(13, col);
+            }
         }
         // ---- resolve B: next bounce (:421-429) ----
         // B was not traced this iteration: SINGLE traces A first; POOL_W defers the B rays
@@ -1815,6 +1834,7 @@ __device__ __forceinline__ void path_body(
         if (hasB && !defer_B) {
             if (bestB < 0) {
                 col = add(col, mk(0.1f, 0.1f, 0.1f));
+                if (LDS_STATE) st_put3(13, col);
                 ended = true;
             } else {
                 f3 hpos, hn;
@@ -1860,7 +1880,7 @@ __global__ __launch_bounds__(kBlock, MIN_WAVES) void games101_path_kernel(
 #ifndef RVCP_STATE_LDS
 #define RVCP_STATE_LDS 1
 #endif
-    __shared__ float state_lds[RVCP_STATE_LDS ? 10 * kBlock : 1];   // LDS_STATE columns
+    __shared__ float state_lds[RVCP_STATE_LDS ? kStateCols * kBlock : 1];   // LDS_STATE columns
     path_body<false, false, false, RVCP_STATE_LDS != 0>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
@@ -1876,7 +1896,7 @@ __global__ __launch_bounds__(kPoolWaves * kWave, RVCP_PATH_MIN_WAVES) void games
     const FaceShade *__restrict__ shade)
 {
     __shared__ uint8_t tail_tab[kPoolWaves][kWave];
-    __shared__ float state_lds[10 * kPoolWaves * kWave];
+    __shared__ float state_lds[kStateCols * kPoolWaves * kWave];
     __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
     __shared__ uint32_t pool_count[kPoolWaves];
     path_body<false, false, false, true, kPoolWaves>(
@@ -2307,7 +2327,7 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void rvcp_s
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];
-    __shared__ float state_lds[10 * kBlock];
+    __shared__ float state_lds[kStateCols * kBlock];
     path_body<false, false, false, true>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
@@ -2320,7 +2340,7 @@ extern "C" __global__ __launch_bounds__(kPoolWaves * kWave, RVCP_PATH_MIN_WAVES)
     const FaceShade *__restrict__ shade)
 {
     __shared__ uint8_t tail_tab[kPoolWaves][kWave];
-    __shared__ float state_lds[10 * kPoolWaves * kWave];
+    __shared__ float state_lds[kStateCols * kPoolWaves * kWave];
     __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
     __shared__ uint32_t pool_count[kPoolWaves];
     path_body<false, false, false, true, kPoolWaves>(
@@ -2336,7 +2356,7 @@ extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];
-    __shared__ float state_lds[10 * kBlock];
+    __shared__ float state_lds[kStateCols * kBlock];
     path_body<false, false, false, true>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
