@@ -339,6 +339,11 @@ def main():
     # profiles/r02_hwq_fif_sweep.log; C3 2 and 3 equal)
     rank_samples = W * spp * rvcp_amd.shard_rows(H, rank, world)
     auto_fif = 4 if rank_samples < (4 << 20) else (3 if legacy else 2)
+    # contexts beyond the hardware queues minus one contend for queues
+    try:
+        auto_fif = max(1, min(auto_fif, int(hw_queues) - 1))
+    except ValueError:
+        pass
     fif = 1 if rehearsal else (args.frames_in_flight or auto_fif)
     rts = [rvcp_amd.RayTracer(**cfg_kw) for _ in range(fif)]
     t_up = time.perf_counter()

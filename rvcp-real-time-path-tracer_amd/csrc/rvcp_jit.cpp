@@ -125,10 +125,11 @@ struct Gen {
     std::string out;
     int n = 0;
 
+    std::string prefix;
     std::string text(const Val &v) const { return v.kind == Val::kLit ? lit_text(v.lit) : v.name; }
     Val tmp(const std::string &expr)
     {
-        const std::string name = "r" + std::to_string(n++);
+        const std::string name = prefix + "r" + std::to_string(n++);
         out += "        const float " + name + " = " + expr + ";\n";
         return var(name);
     }
@@ -164,10 +165,15 @@ struct Gen {
     }
 };
 
-// One triangle's test for ray `r` ("" / "A" / "B"); false when it can never accept.
-bool emit_triangle(std::string &out, const TriRecord &T, uint32_t index, const char *r)
+// One triangle's test for ray `r` ("" / "A" / "B"), split into its arithmetic (`decl`: every
+// value that does not depend on the running nearest hit, temporaries named <prefix>r<k>) and
+// its acceptance (`accept`: the compares with `t <= bt` and the update); false when it can
+// never accept.
+bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, uint32_t index,
+                   const char *r)
 {
     Gen g;
+    g.prefix = "t" + std::to_string(index) + r + "_";
     const std::string R(r);
     Val o[3] = {var("o" + R + ".x"), var("o" + R + ".y"), var("o" + R + ".z")};
     Val d[3] = {var("d" + R + ".x"), var("d" + R + ".y"), var("d" + R + ".z")};
@@ -201,14 +207,41 @@ bool emit_triangle(std::string &out, const TriRecord &T, uint32_t index, const c
     else if (!b1.empty()) add("(" + b1 + " <= 1.0f)");
     else if (!b2.empty()) add("(" + b2 + " <= 1.0f)");
     add("(" + t + " >= tmin)");
-    add("(" + t + " <= bt" + R + ")");
-    out += "    {\n" + g.out;
-    out += "        if (" + cond + ") { bt" + R + " = " + t + "; best" + R + " = " +
-           std::to_string(index) + "; }\n    }\n";
-    // commit the triangle's result before the next one: keeps the unrolled scan one test
-    // deep in registers (without it the compiler interleaves all tests and spills)
-    out += "    RVCP_SPEC_COMMIT(bt" + R + ", best" + R + ");\n";
+    decl += g.out;
+    accept += "        if (" + cond + " & (" + t + " <= bt" + R + ")) { bt" + R + " = " + t + "; best" + R +
+              " = " + std::to_string(index) + "; }\n";
     return true;
+}
+
+// Tests per commit group.  RVCP_SPEC_COMMIT(t, i) after a group makes its result final before
+// the next group starts: without it the compiler interleaves all unrolled tests and spills
+// hundreds of registers.  Within a group the arithmetic of every test comes first (it does not
+// depend on the running nearest hit) and the acceptances follow in triangle order, so the
+// tests of a group are independent chains (ILP) and the order rule is the loop's.
+#ifndef RVCP_SPEC_GROUP1
+#define RVCP_SPEC_GROUP1 1        // single-ray scan (mode 2, the compact scan): tests per group
+#endif
+#ifndef RVCP_SPEC_GROUP2
+#define RVCP_SPEC_GROUP2 1        // dual-ray scan: (triangle, ray) tests per group, in the order
+#endif                            // (0, A), (0, B), (1, A), ...
+
+void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *const *rays,
+               int n_rays, uint32_t group)
+{
+    const uint32_t units = n * (uint32_t)n_rays;
+    for (uint32_t u0 = 0; u0 < units; u0 += group) {
+        std::string decl, accept;
+        bool used[2] = {false, false};
+        for (uint32_t u = u0; u < units && u < u0 + group; u++) {
+            const int r = (int)(u % (uint32_t)n_rays);
+            if (emit_triangle(decl, accept, tri[u / (uint32_t)n_rays], u / (uint32_t)n_rays, rays[r]))
+                used[r] = true;
+        }
+        if (accept.empty()) continue;
+        out += "    {\n" + decl + accept + "    }\n";
+        for (int r = 0; r < n_rays; r++)
+            if (used[r]) out += "    RVCP_SPEC_COMMIT(bt" + std::string(rays[r]) + ", best" + std::string(rays[r]) + ");\n";
+    }
 }
 
 }  // namespace
@@ -235,14 +268,12 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n)
                       std::to_string(n) + " triangles\n";
     out += "__device__ __forceinline__ void spec_scan1(f3 o, f3 d, float tmin, float &bt, "
            "int &best) {\n";
-    for (uint32_t i = 0; i < n; i++) emit_triangle(out, tri[i], i, "");
+    static const char *const one[] = {""}, *const two[] = {"A", "B"};
+    emit_scan(out, tri, n, one, 1, RVCP_SPEC_GROUP1);
     out += "}\n";
     out += "__device__ __forceinline__ void spec_scan2(f3 oA, f3 dA, f3 oB, f3 dB, float tmin, "
            "float &btA, int &bestA, float &btB, int &bestB) {\n";
-    for (uint32_t i = 0; i < n; i++) {
-        emit_triangle(out, tri[i], i, "A");
-        emit_triangle(out, tri[i], i, "B");
-    }
+    emit_scan(out, tri, n, two, 2, RVCP_SPEC_GROUP2);
     out += "}\n";
     return out;
 }

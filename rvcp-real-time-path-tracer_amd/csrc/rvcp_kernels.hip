@@ -1075,7 +1075,10 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
 // never touch the RNG, :424-428), and appends every other pixel with its primary hit record to
 // a compact list for the path kernel (one atomic per wave).
 // ======================================================================================
-constexpr uint32_t kPrimaryBlock = 1024;   // one list append (global atomic) per 1024 pixels
+#ifndef RVCP_PRIMARY_BLOCK
+#define RVCP_PRIMARY_BLOCK 256
+#endif
+constexpr uint32_t kPrimaryBlock = RVCP_PRIMARY_BLOCK;   // one list append (global atomic) per block
 
 template <bool BVH>
 __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(

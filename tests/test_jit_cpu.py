@@ -173,7 +173,7 @@ def test_generated_scan_cornell_bitexact(tmp_path):
     # zero components are dropped: 2544 arithmetic temporaries against 3552 for 32 triangles
     # with no zero component (-28 %)
     dense = _scan_source(_tri_records(np.random.default_rng(0).uniform(-5, 5, pos.shape)))
-    assert src.count("const float r") < 0.75 * dense.count("const float r")
+    assert src.count("const float ") < 0.75 * dense.count("const float ")
     lib = _build(tmp_path, rec, "cornell")
     hits = _check(lib, pos, _adversarial_rays(pos, np.random.default_rng(1), 2500))
     assert hits > 1500
