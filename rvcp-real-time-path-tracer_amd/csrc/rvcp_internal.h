@@ -52,9 +52,10 @@ constexpr uint32_t kChunkWindow = 10000;    // 100 us
 // kWideMinSamples pixel-samples per frame).
 // 9 = variant 3 with the workgroup ray pool: a workgroup's rays are scanned in full 64-ray
 // passes shared out over its waves (no empty ray slots in the scan).
+// 10 = variant 4 with the workgroup ray pool (full passes against each LDS tile).
 // (7 and 8 are the stats codes of the BVH and mode-2 kernels, not schedules.)
 constexpr int kDefaultVariant = 3;
-constexpr int kMaxVariant = 9;
+constexpr int kMaxVariant = 10;
 constexpr int kPoolVariant = 9;
 constexpr int variant_block(int v) { return v == kPoolVariant ? kPoolWaves * kWave : kBlock; }
 constexpr uint64_t kWideMinSamples = 8ull << 20;   // auto: variant 6 from 8 Msamples per frame

@@ -1420,7 +1420,7 @@ __device__ __forceinline__ void path_body(
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
         const bool tail = wave_active && (q.exhausted || A.early_tail) && nr <= kWave / 2 && !BVH &&
                           !POOL_W;
-        if (POOL_W) {
+        if (POOL_W && !TILED) {
             // ---- workgroup ray pool (schedule 9) ----
             // Ray j of the pool: the waves' A (shadow) rays, wave by wave in lane order, then
             // their B (path) rays.  Each slot is two float4s: (o, t) and (d, face).  The first
@@ -1536,10 +1536,63 @@ __device__ __forceinline__ void path_body(
             }
         } else if (TILED) {
             // ---- LDS-tiled scan (optionally with the tail partition below) ----
+            // The scan's operands: slot 0 (so0, sd0; lanes m0) and slot 1 (so1, sd1; lanes m1)
+            // are the lane's A and B rays, or with POOL_W the wave's passes of the workgroup
+            // ray pool; `ttail`: R lanes per ray (o, d), each scanning every R-th triangle.
+            f3 so0 = s_ao, sd0 = s_ad, so1 = b_o, sd1 = b_d;
+            uint64_t m0 = mA, m1 = mB;
+            bool ttail = tail;
             uint32_t R = 1, part = 0;
             bool worker = false;
             f3 o = s_ao, d = s_ad;
-            if (tail) {
+            uint32_t jA = 0, jB = 0, pj0 = 0, pj1 = 0;
+            if (POOL_W) {
+                // push the rays (as in the non-tiled pool above); the pool's passes become
+                // this wave's slots, or every ray gets R lanes when the pool is small
+                jA = pool_baseA + rank_in(mA);
+                jB = pool_baseB + rank_in(mB);
+                pool_deferB = jB >= pool_cut;
+                if (sA) {
+                    pool[2 * jA] = make_float4(s_ao.x, s_ao.y, s_ao.z, 0.0f);
+                    pool[2 * jA + 1] = make_float4(s_ad.x, s_ad.y, s_ad.z, 0.0f);
+                }
+                if (sB) {
+                    pool[2 * jB] = make_float4(b_o.x, b_o.y, b_o.z, 0.0f);
+                    pool[2 * jB + 1] = make_float4(b_d.x, b_d.y, b_d.z, 0.0f);
+                }
+                __syncthreads();
+                if (pool_cut == pool_R && pool_R * 2u <= (uint32_t)(POOL_W * kWave)) {
+                    uint32_t lgK = 1;
+                    while (lgK < 6u && (pool_R << (lgK + 1)) <= (uint32_t)(POOL_W * kWave)) lgK += 1;
+                    R = 1u << lgK;
+                    const uint32_t g = wv * kWave + lane;
+                    pj0 = g >> lgK;
+                    part = g & (R - 1u);
+                    worker = pj0 < pool_R;
+                    const uint32_t jj = worker ? pj0 : 0u;
+                    const float4 ro = pool[2 * jj], rd = pool[2 * jj + 1];
+                    o = mk(ro.x, ro.y, ro.z);
+                    d = mk(rd.x, rd.y, rd.z);
+                    ttail = true;
+                    m0 = m1 = 0ull;
+                } else {
+                    ttail = false;
+                    const uint32_t P = pool_cut / (uint32_t)kWave + (pool_cut % (uint32_t)kWave != 0u);
+                    pj0 = wv * kWave + lane;
+                    pj1 = (wv + POOL_W) * kWave + lane;
+                    const bool v0 = wv < P && pj0 < pool_cut;
+                    const bool v1 = wv + POOL_W < P && pj1 < pool_cut;
+                    const uint32_t i0 = v0 ? pj0 : 0u, i1 = v1 ? pj1 : 0u;
+                    const float4 o0r = pool[2 * i0], d0r = pool[2 * i0 + 1];
+                    const float4 o1r = pool[2 * i1], d1r = pool[2 * i1 + 1];
+                    so0 = mk(o0r.x, o0r.y, o0r.z);
+                    sd0 = mk(d0r.x, d0r.y, d0r.z);
+                    so1 = mk(o1r.x, o1r.y, o1r.z);
+                    sd1 = mk(d1r.x, d1r.y, d1r.z);
+                    m0 = __ballot(v0);
+                    m1 = __ballot(v1);
+                }
+            } else if (tail) {
                 R = 2;
                 while (nr * R * 2 <= (uint32_t)kWave) R *= 2;
                 uint8_t *tab = tail_tab[wv];
@@ -1562,20 +1615,24 @@ __device__ __forceinline__ void path_body(
             }
             float bt = A.t_max;
             int best = -1;
+            if (POOL_W) {        // slot results accumulate in btA/bestA (slot 0), btB/bestB (1)
+                btA = btB = A.t_max;
+                bestA = bestB = -1;
+            }
             for (uint32_t base = 0; base < A.n_faces; base += kTile) {
                 const uint32_t n = A.n_faces - base < kTile ? A.n_faces - base : kTile;
                 const float4 *src = reinterpret_cast<const float4 *>(tri + base);
                 float4 *dst = reinterpret_cast<float4 *>(tile);
-                for (uint32_t e = threadIdx.x; e < 3 * n; e += kBlock) dst[e] = src[e];
+                for (uint32_t e = threadIdx.x; e < 3 * n; e += BLK) dst[e] = src[e];
                 __syncthreads();
-                if (tail) {
+                if (ttail) {
                     if (worker) {
                         for (uint32_t i = part; i < n; i += R) {
                             float t;
                             if (tri_accept(tile[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)(base + i); }
                         }
                     }
-                } else if (wave_active) {
+                } else if ((m0 | m1) != 0ull) {
                     // Two-stage exact test: stage 2 (1/den, t, b1, b2, the
                     // compares) only when some lane may accept.  (A software-pipelined read of
                     // the next triangle costs 12 VGPRs and was slower at 4 waves/SIMD.)
@@ -1594,25 +1651,25 @@ __device__ __forceinline__ void path_body(
                         for (uint32_t h = 0; h < kStep; ++h) { Tp[h] = tile[i + h]; gb[h] = 0ull; }
 #pragma unroll
                         for (uint32_t h = 0; h < kStep; ++h) {
-                            Pa[h] = tri_stage1a(Tp[h], s_ao, s_ad);
-                            ga[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pa[h])) & mA;
+                            Pa[h] = tri_stage1a(Tp[h], so0, sd0);
+                            ga[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pa[h])) & m0;
                             if (!SINGLE) {
-                                Pb[h] = tri_stage1a(Tp[h], b_o, b_d);
-                                gb[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pb[h])) & mB;
+                                Pb[h] = tri_stage1a(Tp[h], so1, sd1);
+                                gb[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pb[h])) & m1;
                             }
                         }
 #pragma unroll
                         for (uint32_t h = 0; h < kStep; ++h) {
                             const TriRecord &T = Tp[h];
                             if (ga[h] != 0ull) {
-                                const TriPart PA = tri_stage1b(T, Pa[h], s_ad);
+                                const TriPart PA = tri_stage1b(T, Pa[h], sd0);
                                 if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PA.n2) <= Pa[h].m) & ga[h]) != 0ull) {
                                     float tA;
                                     if (tri_stage2(T, PA, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i + h); }
                                 }
                             }
                             if (!SINGLE && gb[h] != 0ull) {
-                                const TriPart PB = tri_stage1b(T, Pb[h], b_d);
+                                const TriPart PB = tri_stage1b(T, Pb[h], sd1);
                                 if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PB.n2) <= Pb[h].m) & gb[h]) != 0ull) {
                                     float tB;
                                     if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i + h); }
@@ -1629,20 +1686,20 @@ __device__ __forceinline__ void path_body(
                         // the gates are lane masks ANDed in scalar registers (ballot of one
                         // compare each): __any(sA && p) materialised the predicate in a VGPR
                         // and compared it again, 2 VALU per gate (C5 schedule 4: -7 %)
-                        const TriPartA PaA = tri_stage1a(T, s_ao, s_ad);
-                        const uint64_t gA = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaA)) & mA;
+                        const TriPartA PaA = tri_stage1a(T, so0, sd0);
+                        const uint64_t gA = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaA)) & m0;
                         if (gA != 0ull) {
-                            const TriPart PA = tri_stage1b(T, PaA, s_ad);
+                            const TriPart PA = tri_stage1b(T, PaA, sd0);
                             if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PA.n2) <= PaA.m) & gA) != 0ull) {
                                 float tA;
                                 if (tri_stage2(T, PA, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
                             }
                         }
                         if (!SINGLE) {
-                            const TriPartA PaB = tri_stage1a(T, b_o, b_d);
-                            const uint64_t gB = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaB)) & mB;
+                            const TriPartA PaB = tri_stage1a(T, so1, sd1);
+                            const uint64_t gB = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaB)) & m1;
                             if (gB != 0ull) {
-                                const TriPart PB = tri_stage1b(T, PaB, b_d);
+                                const TriPart PB = tri_stage1b(T, PaB, sd1);
                                 if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PB.n2) <= PaB.m) & gB) != 0ull) {
                                     float tB;
                                     if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
@@ -1650,14 +1707,14 @@ __device__ __forceinline__ void path_body(
                             }
                         }
 #else
-                        const TriPart PA = tri_stage1(T, s_ao, s_ad);
-                        if (__any(sA && tri_maybe(PA))) {
+                        const TriPart PA = tri_stage1(T, so0, sd0);
+                        if (__any(((m0 >> lane) & 1ull) && tri_maybe(PA))) {
                             float tA;
                             if (tri_stage2(T, PA, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
                         }
                         if (!SINGLE) {
-                            const TriPart PB = tri_stage1(T, b_o, b_d);
-                            if (__any(sB && tri_maybe(PB))) {
+                            const TriPart PB = tri_stage1(T, so1, sd1);
+                            if (__any(((m1 >> lane) & 1ull) && tri_maybe(PB))) {
                                 float tB;
                                 if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
                             }
@@ -1667,12 +1724,40 @@ __device__ __forceinline__ void path_body(
                 }
                 __syncthreads();
             }
-            if (tail) {
+            if (ttail) {
                 for (uint32_t off = R >> 1; off >= 1; off >>= 1) {
                     const float ot = __shfl_xor(bt, (int)off);
                     const int ob = __shfl_xor(best, (int)off);
                     if (ot < bt || (ot == bt && ob > best)) { bt = ot; best = ob; }
                 }
+            }
+            if (POOL_W) {
+                float *const poolf = reinterpret_cast<float *>(pool);
+                if (ttail) {
+                    if (worker && part == 0u) {
+                        poolf[8 * pj0 + 3] = bt;
+                        poolf[8 * pj0 + 7] = __int_as_float(best);
+                    }
+                } else {
+                    if ((m0 >> lane) & 1ull) {
+                        poolf[8 * pj0 + 3] = btA;
+                        poolf[8 * pj0 + 7] = __int_as_float(bestA);
+                    }
+                    if ((m1 >> lane) & 1ull) {
+                        poolf[8 * pj1 + 3] = btB;
+                        poolf[8 * pj1 + 7] = __int_as_float(bestB);
+                    }
+                }
+                __syncthreads();
+                // this lane's own results (its rays stay in registers: the tiled kernel's
+                // budget is not the limit here)
+                const uint32_t cap = (uint32_t)(POOL_W * 2 * kWave) - 1u;
+                const uint32_t ia = jA < cap ? jA : cap, ib = jB < cap ? jB : cap;
+                const float ta = poolf[8 * ia + 3], tb = poolf[8 * ib + 3];
+                const int ba = __float_as_int(poolf[8 * ia + 7]), bb = __float_as_int(poolf[8 * ib + 7]);
+                btA = ta; bestA = ba;
+                btB = tb; bestB = bb;
+            } else if (tail) {
                 const int srcA = sA ? (int)(rank_in(mA) * R) : (int)lane;
                 const int srcB = sB ? (int)((na + rank_in(mB)) * R) : (int)lane;
                 const float tA_ = __shfl(bt, srcA), tB_ = __shfl(bt, srcB);
@@ -1901,7 +1986,7 @@ __global__ __launch_bounds__(kPoolWaves * kWave, RVCP_PATH_MIN_WAVES) void games
     __shared__ uint8_t tail_tab[kPoolWaves][kWave];
     __shared__ float state_lds[kStateCols * kPoolWaves * kWave];
     __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
-    __shared__ uint32_t pool_count[kPoolWaves];
+    __shared__ uint32_t pool_count[2 * kPoolWaves];   // A and B rays per wave
     path_body<false, false, false, true, kPoolWaves>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, nullptr, state_lds, pool, pool_count);
@@ -1935,6 +2020,25 @@ __global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_k
     __shared__ TriRecord tile[kTile];
     path_body<true, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
                            shade, tail_tab, tile);
+}
+
+// Schedule 10: schedule 4 with the workgroup ray pool (path_body POOL_W): the workgroup's rays
+// are scanned against each LDS tile in full 64-ray passes shared out over its 4 waves.
+static_assert(kPoolWaves * kWave == kBlock, "the tiled pool kernel keeps the tiled block size");
+__global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_pool_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    __shared__ TriRecord tile[kTile];
+    __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
+    __shared__ uint32_t pool_count[2 * kPoolWaves];
+    path_body<true, false, false, false, kPoolWaves>(
+        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
+        tile, nullptr, nullptr, nullptr, nullptr, nullptr, pool, pool_count);
 }
 
 // Variant 5: the LDS-tiled scan with one ray per lane per iteration (no empty ray slots).
@@ -2345,7 +2449,7 @@ extern "C" __global__ __launch_bounds__(kPoolWaves * kWave, RVCP_PATH_MIN_WAVES)
     __shared__ uint8_t tail_tab[kPoolWaves][kWave];
     __shared__ float state_lds[kStateCols * kPoolWaves * kWave];
     __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
-    __shared__ uint32_t pool_count[kPoolWaves];
+    __shared__ uint32_t pool_count[2 * kPoolWaves];   // A and B rays per wave
     path_body<false, false, false, true, kPoolWaves>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, nullptr, state_lds, pool, pool_count);
@@ -2416,6 +2520,10 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
         hipLaunchKernelGGL(rvcp::games101_bvh_path_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade, bvh_nodes, bvh_tris);
+    else if (args->variant == 10)
+        hipLaunchKernelGGL(rvcp::games101_tiled_pool_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+                           (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
+                           out_lin, counters, surf, shade);
     else if (args->variant == 9)
         hipLaunchKernelGGL(rvcp::games101_pool_kernel, dim3(grid_blocks), dim3(rvcp::kPoolWaves * rvcp::kWave), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
@@ -2473,6 +2581,8 @@ extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_kernel, rvcp::kBlock, 0)
         : variant == 9
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_pool_kernel, rvcp::kPoolWaves * rvcp::kWave, 0)
+        : variant == 10
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_pool_kernel, rvcp::kBlock, 0)
         : variant == 6
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel<6>, rvcp::kBlock, 0)
         : variant == 3

@@ -119,8 +119,9 @@ def c5_small_oracle(c5_scene):
     return cfg, _oracle(c5_scene, cfg, 64, 64)
 
 
-@pytest.mark.parametrize("kw", [dict(), dict(kernel_variant=4), dict(kernel_variant=3),
-                                dict(accel=1)], ids=["default", "tiled4", "scalar3", "bvh"])
+@pytest.mark.parametrize("kw", [dict(), dict(kernel_variant=4), dict(kernel_variant=10),
+                                dict(kernel_variant=3), dict(accel=1)],
+                         ids=["default", "tiled4", "tiledpool10", "scalar3", "bvh"])
 def test_c5_small_bitexact(c5_scene, c5_small_oracle, kw):
     """64^2 SPP=1 of the C5 mesh, whole frame: the default schedule for 100k faces is the
     LDS-tiled single-ray kernel (5); the BVH is compared with the oracle directly, not with
@@ -133,11 +134,12 @@ def test_c5_small_bitexact(c5_scene, c5_small_oracle, kw):
 C5_RECTS = [(384, 512, 256, 1), (640, 200, 256, 1)]
 
 
-@pytest.mark.parametrize("accel", [0, 1], ids=["tiled", "bvh"])
-def test_c5_full_size_segments(c5_scene, accel):
+@pytest.mark.parametrize("kw", [dict(), dict(kernel_variant=10), dict(accel=1)],
+                         ids=["tiled", "tiledpool10", "bvh"])
+def test_c5_full_size_segments(c5_scene, kw):
     """The C5 frame at its own size (1024^2 SPP=30): two 256-pixel row segments through the
     middle of the room (floor, boxes, back wall) against the oracle."""
-    cfg = rvcp_amd.abi.make_config(spp=30, accel=accel)
+    cfg = rvcp_amd.abi.make_config(spp=30, **kw)
     g = _gpu(c5_scene, cfg, 1024, 1024)
     for rect in C5_RECTS:
         _assert_rect(g, _oracle(c5_scene, rvcp_amd.abi.make_config(spp=30), 1024, 1024, rect=rect), rect)

@@ -39,7 +39,7 @@ def _assert_same(gpu, orc):
     assert int(stats["traversals"]) == o_trav
 
 
-VARIANTS = [1, 2, 3, 4, 5, 6, 9]  # kernel schedules (rvcp_config_t::kernel_variant); 0 = default
+VARIANTS = [1, 2, 3, 4, 5, 6, 9, 10]  # kernel schedules (rvcp_config_t::kernel_variant); 0 = default
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -70,7 +70,7 @@ def test_variants_bitexact(cornell, variant, case):
     _assert_same(_gpu(sc, cfg, 40, 36), _oracle(sc, cfg, 40, 36))
 
 
-@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("variant", [4, 5, 10])
 def test_multi_tile_bitexact(cornell, variant):
     """LDS-tiled schedules over several triangle tiles (732 faces = 2 full tiles of 256 and a
     partial one), nearest hits spread across tiles."""
@@ -79,7 +79,7 @@ def test_multi_tile_bitexact(cornell, variant):
     _assert_same(_gpu(sc, cfg, 48, 40), _oracle(sc, cfg, 48, 40))
 
 
-@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("variant", [4, 5, 10])
 @pytest.mark.parametrize("extra", [201, 225, 259])
 def test_tiled_odd_remainder_bitexact(cornell, variant, extra):
     """The tiled scans take two triangles per step and the last one of an
