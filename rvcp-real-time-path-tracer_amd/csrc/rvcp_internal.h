@@ -24,6 +24,11 @@ constexpr int kBlock = 256;
 #define RVCP_POOL_WAVES 4
 #endif
 constexpr int kPoolWaves = RVCP_POOL_WAVES;
+// schedule 10 (LDS-tiled scan with the workgroup ray pool): waves per workgroup
+#ifndef RVCP_TILED_POOL_WAVES
+#define RVCP_TILED_POOL_WAVES 8
+#endif
+constexpr int kTiledPoolWaves = RVCP_TILED_POOL_WAVES;
 // LDS state columns of the path kernels (path_body LDS_STATE): a_p 0-2, nee_C 3-5, nee_dist 6,
 // acc 7-9, att 10-12, col 13-15
 constexpr int kStateCols = 16;
@@ -57,7 +62,10 @@ constexpr uint32_t kChunkWindow = 10000;    // 100 us
 constexpr int kDefaultVariant = 3;
 constexpr int kMaxVariant = 10;
 constexpr int kPoolVariant = 9;
-constexpr int variant_block(int v) { return v == kPoolVariant ? kPoolWaves * kWave : kBlock; }
+constexpr int variant_block(int v)
+{
+    return v == kPoolVariant ? kPoolWaves * kWave : v == 10 ? kTiledPoolWaves * kWave : kBlock;
+}
 constexpr uint64_t kWideMinSamples = 8ull << 20;   // auto: variant 6 from 8 Msamples per frame
 constexpr int kOccupancyBvh = 100;          // rvcp_games101_occupancy code of the BVH kernel
 #ifndef RVCP_TILE

@@ -1398,7 +1398,9 @@ __device__ __forceinline__ void path_body(
             const bool part_mode = pool_R * 2u <= (uint32_t)(POOL_W * kWave);
             const uint32_t pf = pool_R / (uint32_t)kWave, pa = (pool_RA + (uint32_t)kWave - 1u) / (uint32_t)kWave;
             pool_cut = part_mode ? pool_R : (pf > pa ? pf : pa) * (uint32_t)kWave;
-            if (pool_cut > pool_R) pool_cut = pool_R;
+            // the tiled scan streams every triangle tile once per iteration, so an iteration
+            // added by waiting rays costs a whole tile stream: scan every ray (ceil passes)
+            if (pool_cut > pool_R || TILED) pool_cut = pool_R;
         } else if (TILED) {
             // every wave of the workgroup keeps loading tiles until the whole group is done
             if (!__syncthreads_or(wave_active ? 1 : 0)) break;
@@ -2024,19 +2026,18 @@ __global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_k
 
 // Schedule 10: schedule 4 with the workgroup ray pool (path_body POOL_W): the workgroup's rays
 // are scanned against each LDS tile in full 64-ray passes shared out over its 4 waves.
-static_assert(kPoolWaves * kWave == kBlock, "the tiled pool kernel keeps the tiled block size");
-__global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_pool_kernel(
+__global__ __launch_bounds__(kTiledPoolWaves * kWave, RVCP_TILED_MIN_WAVES) void games101_tiled_pool_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
     unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
     const FaceShade *__restrict__ shade)
 {
-    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    __shared__ uint8_t tail_tab[kTiledPoolWaves][kWave];
     __shared__ TriRecord tile[kTile];
-    __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
-    __shared__ uint32_t pool_count[2 * kPoolWaves];
-    path_body<true, false, false, false, kPoolWaves>(
+    __shared__ float4 pool[2 * kTiledPoolWaves * 2 * kWave];
+    __shared__ uint32_t pool_count[2 * kTiledPoolWaves];
+    path_body<true, false, false, false, kTiledPoolWaves>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         tile, nullptr, nullptr, nullptr, nullptr, nullptr, pool, pool_count);
 }
@@ -2521,7 +2522,7 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade, bvh_nodes, bvh_tris);
     else if (args->variant == 10)
-        hipLaunchKernelGGL(rvcp::games101_tiled_pool_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+        hipLaunchKernelGGL(rvcp::games101_tiled_pool_kernel, dim3(grid_blocks), dim3(rvcp::kTiledPoolWaves * rvcp::kWave), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade);
     else if (args->variant == 9)
@@ -2582,7 +2583,7 @@ extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
         : variant == 9
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_pool_kernel, rvcp::kPoolWaves * rvcp::kWave, 0)
         : variant == 10
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_pool_kernel, rvcp::kBlock, 0)
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_pool_kernel, rvcp::kTiledPoolWaves * rvcp::kWave, 0)
         : variant == 6
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel<6>, rvcp::kBlock, 0)
         : variant == 3

@@ -64,7 +64,7 @@ for s in $STEPS; do
         rehearse2) run rehearse2 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
         frames) run frames 300 python tools/frames.py --frames 20 ;;
         poolab) run poolab 600 bash tools/sched_ab.sh "3 9" "--frames 20" "--size 384 --spp 10 --frames 40" "--size 2048 --spp 64 --frames 6" "--size 128 --spp 30 --frames 40" ;;
-        c5pool) run c5pool 900 bash tools/sched_ab.sh "4 10" "--tris 100000 --size 512 --spp 4 --frames 5" "--tris 2000 --size 1024 --spp 8 --frames 6" "--tris 300 --size 1024 --spp 8 --frames 8" ;;
+        c5pool) run c5pool 900 bash tools/sched_ab.sh "${VARS:-4 10}" "--tris 100000 --size 512 --spp 4 --frames 5" "--tris 2000 --size 1024 --spp 8 --frames 6" "--tris 300 --size 1024 --spp 8 --frames 8" ;;
         c5tests) run c5tests 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "c5 or multi_tile or odd_remainder or variants or bitexact_cornell" ;;
         pooltests) run pooltests 600 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         *) echo "unknown step $s"; exit 2 ;;
