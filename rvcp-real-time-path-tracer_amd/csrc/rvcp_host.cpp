@@ -301,7 +301,7 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         return fail(nullptr, RVCP_E_UNSUPPORTED, "unsupported integrator");
     if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
     if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant || cfg->kernel_variant == 7 ||
-        cfg->kernel_variant == 8)
+        cfg->kernel_variant == 8 || cfg->kernel_variant == 9)
         return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
     if (cfg->n_gpus < 0 || cfg->n_gpus > 64)
         return fail(nullptr, RVCP_E_INVALID, "n_gpus must be in [0, 64]");
@@ -366,7 +366,7 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     const int cap = cap_env ? std::atoi(cap_env) : 0;
     ctx->n_simds = (uint32_t)cus * 4u;
     for (int v = 1; v <= kMaxVariant; v++) {
-        if (v == 7 || v == 8) continue;
+        if (v == 7 || v == 8 || v == 9) continue;
         int per_cu = 0;
         if (rvcp_games101_occupancy(v, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
         if (cap > 0 && cap < per_cu) per_cu = cap;
@@ -647,15 +647,16 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     A.light_total = ctx->light_total;
     A.light_pdf = ctx->light_pdf;
     A.want_linear = d_linear_rgb ? 1u : 0u;
-    // automatic schedule: 4 / 5 (LDS tiles; two rays per lane on large frames, one on small
-    // ones) for large meshes, 4 also for mid-size meshes on large frames, else 3, or 6 (6 waves/SIMD) for
+    // automatic schedule: 10 / 5 (LDS tiles; the workgroup's rays pooled into full passes on
+    // large frames, one ray per lane on small ones) for large meshes, 10 also for mid-size
+    // meshes on large frames, else 3, or 6 (6 waves/SIMD) for
     // large frames -- except with the scene-specialised scan, whose 6-wave build spills and
     // measures slower than its 5-wave one at every size
     const bool jit_ok = ctx->jit && ctx->cfg.ray_t_min > 0.0f;
     const bool big_frame = (uint64_t)A.n_pixels * A.spp >= kTiledDualMinSamples;
     A.variant = ctx->cfg.kernel_variant != 0 ? ctx->cfg.kernel_variant
-              : ctx->n_faces >= kTiledMinFaces ? (big_frame ? 4 : 5)
-              : (!jit_ok && ctx->n_faces > kTiledWideMinFaces && big_frame) ? 4
+              : ctx->n_faces >= kTiledMinFaces ? (big_frame ? kTiledPoolVariant : 5)
+              : (!jit_ok && ctx->n_faces > kTiledWideMinFaces && big_frame) ? kTiledPoolVariant
               : (!jit_ok && (uint64_t)A.n_pixels * A.spp >= kWideMinSamples) ? 6 : kDefaultVariant;
     A.accel = (ctx->cfg.accel == RVCP_ACCEL_BVH && ctx->n_faces > 0) ? RVCP_ACCEL_BVH : RVCP_ACCEL_NONE;
     if (A.accel == RVCP_ACCEL_BVH) A.variant = 3;    // the BVH traversal lives in the v3 kernels
@@ -683,8 +684,7 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             // upload compiled one; its exactness argument needs t_min > 0
             const JitKernels *jk = ctx->jit.get();
             const int jit_per_cu = !jk ? 0 : A.variant == 6 ? jk->blocks_per_cu6
-                                 : A.variant == 3 ? jk->blocks_per_cu5
-                                 : A.variant == kPoolVariant ? jk->blocks_per_cu_pool : 0;
+                                 : A.variant == 3 ? jk->blocks_per_cu5 : 0;
             const bool spec = !legacy && !A.accel && jit_per_cu > 0 && A.t_min > 0.0f;
             // mode 2 with the specialised triangle scan (its kernel also checks per wave
             // that every ray is finite and has t_min > 0)
@@ -754,9 +754,7 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                                              ctx->d_counters, ctx->d_surf, ctx->d_shade,
                                              ctx->d_bvh_nodes, ctx->d_bvh_tris,
                                              blocks, s, ctx->evm,
-                                             spec ? (void *)(A.variant == 6 ? jk->path6
-                                                             : A.variant == kPoolVariant ? jk->pool
-                                                             : jk->path5)
+                                             spec ? (void *)(A.variant == 6 ? jk->path6 : jk->path5)
                                                   : nullptr);
                 if (spec) ctx->last_spec = true;
             } else {

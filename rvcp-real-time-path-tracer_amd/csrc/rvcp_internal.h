@@ -19,11 +19,6 @@ namespace rvcp {
 constexpr int kWave = 64;
 // Threads per workgroup of the path-tracing kernel (4 independent waves).
 constexpr int kBlock = 256;
-// schedule 9 (workgroup ray pool): waves per workgroup
-#ifndef RVCP_POOL_WAVES
-#define RVCP_POOL_WAVES 4
-#endif
-constexpr int kPoolWaves = RVCP_POOL_WAVES;
 // schedule 10 (LDS-tiled scan with the workgroup ray pool): waves per workgroup
 #ifndef RVCP_TILED_POOL_WAVES
 #define RVCP_TILED_POOL_WAVES 8
@@ -55,17 +50,14 @@ constexpr uint32_t kChunkWindow = 10000;    // 100 us
 // 6 = variant 3 compiled for 6 waves per SIMD instead of 5 (80 VGPRs, a few spills): faster
 // once the frame is large enough that latency hiding beats the spills (automatic from
 // kWideMinSamples pixel-samples per frame).
-// 9 = variant 3 with the workgroup ray pool: a workgroup's rays are scanned in full 64-ray
-// passes shared out over its waves (no empty ray slots in the scan).
-// 10 = variant 4 with the workgroup ray pool (full passes against each LDS tile).
-// (7 and 8 are the stats codes of the BVH and mode-2 kernels, not schedules.)
+// 10 = variant 4 with the workgroup ray pool: the rays of a workgroup of kTiledPoolWaves waves
+// are scanned against each LDS tile in 64-ray passes shared out over its waves (the automatic
+// choice wherever 4 was).  (7 and 8 are the stats codes of the BVH and mode-2 kernels, 9 is
+// unused: a non-tiled pool measured slower)
 constexpr int kDefaultVariant = 3;
 constexpr int kMaxVariant = 10;
-constexpr int kPoolVariant = 9;
-constexpr int variant_block(int v)
-{
-    return v == kPoolVariant ? kPoolWaves * kWave : v == 10 ? kTiledPoolWaves * kWave : kBlock;
-}
+constexpr int kTiledPoolVariant = 10;
+constexpr int variant_block(int v) { return v == kTiledPoolVariant ? kTiledPoolWaves * kWave : kBlock; }
 constexpr uint64_t kWideMinSamples = 8ull << 20;   // auto: variant 6 from 8 Msamples per frame
 constexpr int kOccupancyBvh = 100;          // rvcp_games101_occupancy code of the BVH kernel
 #ifndef RVCP_TILE

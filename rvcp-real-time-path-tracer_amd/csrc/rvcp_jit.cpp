@@ -426,8 +426,7 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         return nullptr;
     }
     if (hipModuleGetFunction(&k->path5, k->module, "rvcp_spec_path_kernel5") != hipSuccess ||
-        hipModuleGetFunction(&k->path6, k->module, "rvcp_spec_path_kernel6") != hipSuccess ||
-        hipModuleGetFunction(&k->pool, k->module, "rvcp_spec_pool_kernel") != hipSuccess) {
+        hipModuleGetFunction(&k->path6, k->module, "rvcp_spec_path_kernel6") != hipSuccess) {
         err = "specialised kernels missing from the module";
         return nullptr;
     }
@@ -442,8 +441,6 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         k->blocks_per_cu5 = bpc;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->path6, kBlock, 0) == hipSuccess)
         k->blocks_per_cu6 = bpc;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->pool, kPoolWaves * kWave, 0) == hipSuccess)
-        k->blocks_per_cu_pool = bpc;
     g_cache.push_front(CacheEntry{device, h, scan, k});
     if (g_cache.size() > kCacheEntries) g_cache.pop_back();
     return k;

@@ -1202,8 +1202,8 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 // event, read when the shadow ray resolves) and the pixel's running sum `acc` live in this
 // lane's column of an LDS block (SoA, stride = the block size) instead of 10 VGPRs across the
 // scan.
-// POOL_W > 0 (schedule 9): the workgroup of POOL_W waves pools its rays in LDS every iteration
-// and scans them in full 64-ray passes shared out over its waves (see the POOL_W branch).
+// POOL_W > 0 (schedule 10, with TILED): the workgroup of POOL_W waves pools its rays in LDS
+// every iteration and scans them in 64-ray passes shared out over its waves.
 template <bool TILED, bool BVH, bool SINGLE = false, bool LDS_STATE = false, int POOL_W = 0>
 __device__ __forceinline__ void path_body(
     const FrameArgs &A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
@@ -1215,6 +1215,7 @@ __device__ __forceinline__ void path_body(
     int32_t *bvh_stack = nullptr, float4 *compact_lds = nullptr, float *state_lds = nullptr,
     float4 *pool = nullptr, uint32_t *pool_count = nullptr)
 {
+    static_assert(POOL_W == 0 || TILED, "the workgroup ray pool is built for the tiled scan");
     constexpr int BLK = POOL_W ? POOL_W * kWave : kBlock;     // threads per workgroup
     float *const st = LDS_STATE ? state_lds + threadIdx.x : nullptr;   // st[f * BLK]
     auto st_put3 = [&](int f, f3 v) { st[f * BLK] = v.x; st[(f + 1) * BLK] = v.y; st[(f + 2) * BLK] = v.z; };
@@ -1258,7 +1259,6 @@ __device__ __forceinline__ void path_body(
     float nee_dist = 0.0f;
     bool hasB = false;
     f3 b_o = mk(0, 0, 0), b_d = mk(0, 0, 1);
-    uint32_t pool_iter = 0;              // POOL_W: the workgroup's iteration (wave-uniform)
 
     for (;;) {
         // ---- settle: end samples, take pixels, emit surface events ----
@@ -1361,10 +1361,9 @@ __device__ __forceinline__ void path_body(
         const f3 s_ad = (SINGLE && !hasA) ? b_d : a_d;
         const uint64_t mA = __ballot(sA), mB = __ballot(sB);
         const bool wave_active = (mA | mB) != 0ull;
-        // POOL_W: this wave's first A and B slots in the workgroup's ray pool, the pool's size
-        // R, its A rays RA, and the pool slots scanned this iteration (pool_cut; the B rays
-        // beyond it wait for the next iteration)
-        uint32_t pool_baseA = 0, pool_baseB = 0, pool_R = 0, pool_RA = 0, pool_cut = 0;
+        // POOL_W: this wave's first A and B slots in the workgroup's ray pool and the pool's
+        // size R (its A rays first, wave by wave, then its B rays)
+        uint32_t pool_baseA = 0, pool_baseB = 0, pool_R = 0;
         if (POOL_W) {
             // every wave of the workgroup takes part in every iteration until the whole group
             // has no ray left (the pool is filled and scanned between workgroup barriers)
@@ -1373,34 +1372,19 @@ __device__ __forceinline__ void path_body(
                 pool_count[2 * wv + 1] = (uint32_t)__builtin_popcountll(mB);
             }
             __syncthreads();
-            // A rays wave by wave, then B rays wave by wave starting at wave pool_iter mod W
-            // (the rotation spreads the deferred B rays over the waves)
-            const uint32_t rot = pool_iter % (uint32_t)POOL_W;
-            const uint32_t my_pos = (wv + (uint32_t)POOL_W - rot) % (uint32_t)POOL_W;
-            uint32_t RB = 0;
+            uint32_t RA = 0, RB = 0;
 #pragma unroll
             for (int v = 0; v < POOL_W; ++v) {
                 const uint32_t ca = pool_count[2 * v], cb = pool_count[2 * v + 1];
-                const uint32_t pos = ((uint32_t)v + (uint32_t)POOL_W - rot) % (uint32_t)POOL_W;
                 pool_baseA += (uint32_t)v < wv ? ca : 0u;
-                pool_baseB += pos < my_pos ? cb : 0u;
-                pool_RA += ca;
+                pool_baseB += (uint32_t)v < wv ? cb : 0u;
+                RA += ca;
                 RB += cb;
             }
-            pool_R = __builtin_amdgcn_readfirstlane(pool_RA + RB);
-            pool_RA = __builtin_amdgcn_readfirstlane(pool_RA);
+            pool_R = __builtin_amdgcn_readfirstlane(RA + RB);
             pool_baseA = __builtin_amdgcn_readfirstlane(pool_baseA);
-            pool_baseB = __builtin_amdgcn_readfirstlane(pool_baseB + pool_RA);
+            pool_baseB = __builtin_amdgcn_readfirstlane(pool_baseB + RA);
             if (pool_R == 0u) break;
-            pool_iter += 1u;
-            // full passes only: floor(R / 64) passes (but every A ray), the rest waits; a
-            // small pool (the tail partition below) is scanned whole
-            const bool part_mode = pool_R * 2u <= (uint32_t)(POOL_W * kWave);
-            const uint32_t pf = pool_R / (uint32_t)kWave, pa = (pool_RA + (uint32_t)kWave - 1u) / (uint32_t)kWave;
-            pool_cut = part_mode ? pool_R : (pf > pa ? pf : pa) * (uint32_t)kWave;
-            // the tiled scan streams every triangle tile once per iteration, so an iteration
-            // added by waiting rays costs a whole tile stream: scan every ray (ceil passes)
-            if (pool_cut > pool_R || TILED) pool_cut = pool_R;
         } else if (TILED) {
             // every wave of the workgroup keeps loading tiles until the whole group is done
             if (!__syncthreads_or(wave_active ? 1 : 0)) break;
@@ -1408,139 +1392,28 @@ __device__ __forceinline__ void path_body(
             break;
         }
         if (wave_active) iters += 1;
-        if (POOL_W)   // a deferred B ray is counted when it is scanned
-            trav_wave += (uint32_t)__builtin_popcountll(mA) +
-                         (uint32_t)__builtin_popcountll(__ballot(sB && pool_baseB + rank_in(mB) < pool_cut));
-        else
-            trav_wave += (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
+        trav_wave += (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
         if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
 
         int bestA = -1, bestB = -1;
         float btA = A.t_max, btB = A.t_max;
-        bool pool_deferB = false;
         const uint32_t na = (uint32_t)__builtin_popcountll(mA);
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
         const bool tail = wave_active && (q.exhausted || A.early_tail) && nr <= kWave / 2 && !BVH &&
                           !POOL_W;
-        if (POOL_W && !TILED) {
-            // ---- workgroup ray pool (schedule 9) ----
-            // Ray j of the pool: the waves' A (shadow) rays, wave by wave in lane order, then
-            // their B (path) rays.  Each slot is two float4s: (o, t) and (d, face).  The first
-            // pool_cut rays -- floor(R / 64) full passes of 64, at least every A ray -- are
-            // scanned, pass p by wave p mod POOL_W (a wave with two passes scans them as the two
-            // rays of the dual scan); the B rays beyond the cut wait for the next iteration
-            // (their lanes resolve the shadow ray and start no new event meanwhile).  So the
-            // workgroup scans full passes instead of two slots per lane whether or not they
-            // hold a ray.  When R is at most half the workgroup's lanes, every ray gets K >= 2
-            // lanes that scan every K-th triangle (the tail partition, combined with the scan's
-            // order rule).  Each ray meets the same triangles with the same test wherever and
-            // whenever it is scanned, so every nearest hit is unchanged.
-            const uint32_t jA = pool_baseA + rank_in(mA), jB = pool_baseB + rank_in(mB);
-            pool_deferB = jB >= pool_cut;
-            if (sA) {
-                pool[2 * jA] = make_float4(s_ao.x, s_ao.y, s_ao.z, 0.0f);
-                pool[2 * jA + 1] = make_float4(s_ad.x, s_ad.y, s_ad.z, 0.0f);
-            }
-            if (sB) {
-                pool[2 * jB] = make_float4(b_o.x, b_o.y, b_o.z, 0.0f);
-                pool[2 * jB + 1] = make_float4(b_d.x, b_d.y, b_d.z, 0.0f);
-            }
-            __syncthreads();
-            float *const poolf = reinterpret_cast<float *>(pool);
-            if (pool_cut == pool_R && pool_R * 2u <= (uint32_t)(POOL_W * kWave)) {
-                // tail partition over the whole workgroup: K lanes per ray (power of two <= 64)
-                uint32_t lgK = 1;
-                while (lgK < 6u && (pool_R << (lgK + 1)) <= (uint32_t)(POOL_W * kWave)) lgK += 1;
-                const uint32_t K = 1u << lgK;
-                const uint32_t g = wv * kWave + lane;
-                const uint32_t j = g >> lgK, part = g & (K - 1u);
-                const bool worker = j < pool_R;
-                float bt = A.t_max;
-                int best = -1;
-                if (worker) {
-                    const float4 ro = pool[2 * j], rd = pool[2 * j + 1];
-                    const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
-                    for (uint32_t i = part; i < A.n_faces; i += K) {
-                        float t;
-                        if (tri_accept(tri[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
-                    }
-                }
-                for (uint32_t off = K >> 1; off >= 1; off >>= 1) {
-                    const float ot = __shfl_xor(bt, (int)off);
-                    const int ob = __shfl_xor(best, (int)off);
-                    if (ot < bt || (ot == bt && ob > best)) { bt = ot; best = ob; }
-                }
-                if (worker && part == 0u) {
-                    poolf[8 * j + 3] = bt;
-                    poolf[8 * j + 7] = __int_as_float(best);
-                }
-            } else {
-                const uint32_t P = pool_cut / (uint32_t)kWave + (pool_cut % (uint32_t)kWave != 0u);
-                const uint32_t p0 = wv, p1 = wv + POOL_W;          // this wave's passes
-                if (p0 < P) {
-                    const bool two = p1 < P;
-                    const uint32_t j0 = p0 * kWave + lane, j1 = p1 * kWave + lane;
-                    const bool v0 = j0 < pool_cut, v1 = two && j1 < pool_cut;
-                    // (slots beyond the cut hold stale or waiting rays: scanned, never read back)
-                    const float4 o0r = pool[2 * j0], d0r = pool[2 * j0 + 1];
-                    const float4 o1r = two ? pool[2 * j1] : o0r, d1r = two ? pool[2 * j1 + 1] : d0r;
-                    const f3 o0 = mk(o0r.x, o0r.y, o0r.z), d0 = mk(d0r.x, d0r.y, d0r.z);
-                    const f3 o1 = mk(o1r.x, o1r.y, o1r.z), d1 = mk(d1r.x, d1r.y, d1r.z);
-                    float bt0 = A.t_max, bt1 = A.t_max;
-                    int best0 = -1, best1 = -1;
-#ifdef RVCP_SPEC_SCAN
-                    if (!__any((v0 && !ray_in_range(o0, d0)) || (v1 && !ray_in_range(o1, d1)))) {
-                        if (two) spec_scan2(o0, d0, o1, d1, A.t_min, bt0, best0, bt1, best1);
-                        else spec_scan1(o0, d0, A.t_min, bt0, best0);
-                    } else
-#endif
-                    if (two) {
-#pragma unroll RVCP_SCAN_UNROLL
-                        for (uint32_t i = 0; i < A.n_faces; ++i) {
-                            const TriRecord T = tri[i];
-                            float t0, t1;
-                            if (tri_accept(T, o0, d0, A.t_min, bt0, t0)) { bt0 = t0; best0 = (int)i; }
-                            if (tri_accept(T, o1, d1, A.t_min, bt1, t1)) { bt1 = t1; best1 = (int)i; }
-                        }
-                    } else {
-#pragma unroll RVCP_SCAN_UNROLL
-                        for (uint32_t i = 0; i < A.n_faces; ++i) {
-                            float t0;
-                            if (tri_accept(tri[i], o0, d0, A.t_min, bt0, t0)) { bt0 = t0; best0 = (int)i; }
-                        }
-                    }
-                    if (v0) {
-                        poolf[8 * j0 + 3] = bt0;
-                        poolf[8 * j0 + 7] = __int_as_float(best0);
-                    }
-                    if (v1) {
-                        poolf[8 * j1 + 3] = bt1;
-                        poolf[8 * j1 + 7] = __int_as_float(best1);
-                    }
-                }
-            }
-            __syncthreads();
-            // read back this lane's rays with their results: the rays come from LDS rather
-            // than being held in registers across the scan, so they are loaded by every lane
-            // (a lane without the ray reads an in-bounds slot it never uses) -- a conditional
-            // load would keep the old registers live through the scan
-            {
-                const uint32_t cap = (uint32_t)(POOL_W * 2 * kWave) - 1u;
-                const uint32_t ia = jA < cap ? jA : cap, ib = jB < cap ? jB : cap;
-                const float4 ra = pool[2 * ia], rda = pool[2 * ia + 1];
-                const float4 rb = pool[2 * ib], rdb = pool[2 * ib + 1];
-                a_o = mk(ra.x, ra.y, ra.z);
-                a_d = mk(rda.x, rda.y, rda.z);
-                b_o = mk(rb.x, rb.y, rb.z);
-                b_d = mk(rdb.x, rdb.y, rdb.z);
-                if (sA) { btA = ra.w; bestA = __float_as_int(rda.w); }
-                if (sB) { btB = rb.w; bestB = __float_as_int(rdb.w); }
-            }
-        } else if (TILED) {
+        if (TILED) {
             // ---- LDS-tiled scan (optionally with the tail partition below) ----
             // The scan's operands: slot 0 (so0, sd0; lanes m0) and slot 1 (so1, sd1; lanes m1)
             // are the lane's A and B rays, or with POOL_W the wave's passes of the workgroup
             // ray pool; `ttail`: R lanes per ray (o, d), each scanning every R-th triangle.
+            // Workgroup ray pool (schedule 10): ray j of the pool is two float4s, (o, t) and
+            // (d, face); the R rays are scanned in ceil(R / 64) passes of 64, pass p by wave p
+            // mod POOL_W, as that wave's slots, so the workgroup's waves scan what it holds
+            // instead of two slots per lane whether or not they hold a ray (the tiles are
+            // streamed once per iteration either way).  When R is at most half the
+            // workgroup's lanes, every ray gets R >= 2 lanes that scan every R-th triangle of
+            // each tile (the tail partition).  Each ray meets the same triangles with the same
+            // test wherever it is scanned, so every nearest hit is unchanged.
             f3 so0 = s_ao, sd0 = s_ad, so1 = b_o, sd1 = b_d;
             uint64_t m0 = mA, m1 = mB;
             bool ttail = tail;
@@ -1553,7 +1426,6 @@ __device__ __forceinline__ void path_body(
                 // this wave's slots, or every ray gets R lanes when the pool is small
                 jA = pool_baseA + rank_in(mA);
                 jB = pool_baseB + rank_in(mB);
-                pool_deferB = jB >= pool_cut;
                 if (sA) {
                     pool[2 * jA] = make_float4(s_ao.x, s_ao.y, s_ao.z, 0.0f);
                     pool[2 * jA + 1] = make_float4(s_ad.x, s_ad.y, s_ad.z, 0.0f);
@@ -1563,7 +1435,7 @@ __device__ __forceinline__ void path_body(
                     pool[2 * jB + 1] = make_float4(b_d.x, b_d.y, b_d.z, 0.0f);
                 }
                 __syncthreads();
-                if (pool_cut == pool_R && pool_R * 2u <= (uint32_t)(POOL_W * kWave)) {
+                if (pool_R * 2u <= (uint32_t)(POOL_W * kWave)) {
                     uint32_t lgK = 1;
                     while (lgK < 6u && (pool_R << (lgK + 1)) <= (uint32_t)(POOL_W * kWave)) lgK += 1;
                     R = 1u << lgK;
@@ -1579,11 +1451,10 @@ __device__ __forceinline__ void path_body(
                     m0 = m1 = 0ull;
                 } else {
                     ttail = false;
-                    const uint32_t P = pool_cut / (uint32_t)kWave + (pool_cut % (uint32_t)kWave != 0u);
                     pj0 = wv * kWave + lane;
                     pj1 = (wv + POOL_W) * kWave + lane;
-                    const bool v0 = wv < P && pj0 < pool_cut;
-                    const bool v1 = wv + POOL_W < P && pj1 < pool_cut;
+                    const bool v0 = pj0 < pool_R;
+                    const bool v1 = pj1 < pool_R;
                     const uint32_t i0 = v0 ? pj0 : 0u, i1 = v1 ? pj1 : 0u;
                     const float4 o0r = pool[2 * i0], d0r = pool[2 * i0 + 1];
                     const float4 o1r = pool[2 * i1], d1r = pool[2 * i1 + 1];
@@ -1918,9 +1789,7 @@ __device__ __forceinline__ void path_body(
             }
         }
         // ---- resolve B: next bounce (:421-429) ----
-        // B was not traced this iteration: SINGLE traces A first; POOL_W defers the B rays
-        // beyond the pool's cut
-        const bool defer_B = (SINGLE && hasA && hasB) || (POOL_W && hasB && pool_deferB);
+        const bool defer_B = SINGLE && hasA && hasB;    // B was not traced this iteration
         if (hasB && !defer_B) {
             if (bestB < 0) {
                 col = add(col, mk(0.1f, 0.1f, 0.1f));
@@ -1974,24 +1843,6 @@ __global__ __launch_bounds__(kBlock, MIN_WAVES) void games101_path_kernel(
     path_body<false, false, false, RVCP_STATE_LDS != 0>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
-}
-
-// Schedule 9: schedule 3 with the workgroup ray pool (path_body POOL_W): workgroups of
-// kPoolWaves waves, 5 waves per SIMD.
-__global__ __launch_bounds__(kPoolWaves * kWave, RVCP_PATH_MIN_WAVES) void games101_pool_kernel(
-    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
-    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
-    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
-    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
-    const FaceShade *__restrict__ shade)
-{
-    __shared__ uint8_t tail_tab[kPoolWaves][kWave];
-    __shared__ float state_lds[kStateCols * kPoolWaves * kWave];
-    __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
-    __shared__ uint32_t pool_count[2 * kPoolWaves];   // A and B rays per wave
-    path_body<false, false, false, true, kPoolWaves>(
-        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
-        nullptr, nullptr, nullptr, nullptr, nullptr, state_lds, pool, pool_count);
 }
 
 // Opt-in BVH (RVCP_ACCEL_BVH): the variant-3 machine with per-lane BVH traversal in place of
@@ -2440,21 +2291,6 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void rvcp_s
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
 }
-extern "C" __global__ __launch_bounds__(kPoolWaves * kWave, RVCP_PATH_MIN_WAVES) void rvcp_spec_pool_kernel(
-    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
-    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
-    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
-    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
-    const FaceShade *__restrict__ shade)
-{
-    __shared__ uint8_t tail_tab[kPoolWaves][kWave];
-    __shared__ float state_lds[kStateCols * kPoolWaves * kWave];
-    __shared__ float4 pool[2 * kPoolWaves * 2 * kWave];
-    __shared__ uint32_t pool_count[2 * kPoolWaves];   // A and B rays per wave
-    path_body<false, false, false, true, kPoolWaves>(
-        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
-        nullptr, nullptr, nullptr, nullptr, nullptr, state_lds, pool, pool_count);
-}
 extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
@@ -2513,8 +2349,7 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
         rvcp::FrameArgs a = *args;
         void *params[] = {&a, &tri, &mats, &lights, &gamma_t, &out_rgba, &out_lin, &counters,
                           &surf, &shade};
-        const unsigned bs = args->variant == 9 ? rvcp::kPoolWaves * rvcp::kWave : rvcp::kBlock;
-        if (hipModuleLaunchKernel((hipFunction_t)spec_path_fn, grid_blocks, 1, 1, bs,
+        if (hipModuleLaunchKernel((hipFunction_t)spec_path_fn, grid_blocks, 1, 1, rvcp::kBlock,
                                   1, 1, 0, (hipStream_t)stream, params, nullptr) != hipSuccess)
             return -2;
     } else if (args->accel)
@@ -2523,10 +2358,6 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                            out_lin, counters, surf, shade, bvh_nodes, bvh_tris);
     else if (args->variant == 10)
         hipLaunchKernelGGL(rvcp::games101_tiled_pool_kernel, dim3(grid_blocks), dim3(rvcp::kTiledPoolWaves * rvcp::kWave), 0,
-                           (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
-                           out_lin, counters, surf, shade);
-    else if (args->variant == 9)
-        hipLaunchKernelGGL(rvcp::games101_pool_kernel, dim3(grid_blocks), dim3(rvcp::kPoolWaves * rvcp::kWave), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade);
     else if (args->variant == 5)
@@ -2580,8 +2411,6 @@ extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_single_kernel, rvcp::kBlock, 0)
         : variant == 4
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_kernel, rvcp::kBlock, 0)
-        : variant == 9
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_pool_kernel, rvcp::kPoolWaves * rvcp::kWave, 0)
         : variant == 10
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_tiled_pool_kernel, rvcp::kTiledPoolWaves * rvcp::kWave, 0)
         : variant == 6

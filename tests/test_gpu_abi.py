@@ -189,13 +189,13 @@ def test_stats_report_schedule(cornell):
         rt.render(32, 32, TIME)
         assert int(rt.last_stats["kernel_variant"]) == 5         # large mesh, small frame
         rt.render(1024, 512, TIME)
-        assert int(rt.last_stats["kernel_variant"]) == 4         # large mesh, >= 512 Ki samples
+        assert int(rt.last_stats["kernel_variant"]) == 10        # large mesh, >= 512 Ki samples
     with rvcp_amd.RayTracer(spp=1) as rt:
         rt.upload_scene(rvcp_amd.scene.with_random_triangles(cornell, 40))     # 72 faces
         rt.render(64, 64, TIME)
         assert int(rt.last_stats["kernel_variant"]) == 3
         rt.render(1024, 512, TIME)
-        assert int(rt.last_stats["kernel_variant"]) == 4
+        assert int(rt.last_stats["kernel_variant"]) == 10
     with rvcp_amd.RayTracer(spp=2, integrator=1) as rt:                         # mode 2
         rt.upload_scene(rvcp_amd.scene.sphere_scene())
         rt.render(64, 64, TIME)

@@ -39,7 +39,7 @@ def _assert_same(gpu, orc):
     assert int(stats["traversals"]) == o_trav
 
 
-VARIANTS = [1, 2, 3, 4, 5, 6, 9, 10]  # kernel schedules (rvcp_config_t::kernel_variant); 0 = default
+VARIANTS = [1, 2, 3, 4, 5, 6, 10]  # kernel schedules (rvcp_config_t::kernel_variant); 0 = default
 
 
 @pytest.mark.parametrize("variant", VARIANTS)

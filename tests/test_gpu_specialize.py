@@ -62,18 +62,6 @@ def test_specialised_vs_oracle(cornell, case):
     assert np.array_equal(s[0], o_rgba) and int(s[2]["traversals"]) == o_trav
 
 
-@pytest.mark.parametrize("W,H,spp", [(1024, 1024, 30), (384, 384, 10), (129, 67, 7), (16, 8, 3)])
-def test_pool_schedule_equals_schedule3(cornell, W, H, spp):
-    """Schedule 9 (the workgroup ray pool), specialised and generic, renders the schedule-3
-    frame bit for bit (the C3 and C2 frames among them)."""
-    ref = _render(cornell, W, H, spp=spp, kernel_variant=3, specialize=rvcp_amd.abi.SPECIALIZE_OFF)
-    for spec in (rvcp_amd.abi.SPECIALIZE_AUTO, rvcp_amd.abi.SPECIALIZE_OFF):
-        s = _render(cornell, W, H, spp=spp, kernel_variant=9, specialize=spec)
-        assert int(s[2]["kernel_variant"]) & ~SPEC == 9
-        assert bool(int(s[2]["kernel_variant"]) & SPEC) == (spec == rvcp_amd.abi.SPECIALIZE_AUTO)
-        _same(s, ref)
-
-
 def test_nonpositive_t_min_uses_generic(cornell):
     """The exactness argument needs t_min > 0: with ray_t_min = 0 the generic kernel runs."""
     s = _render(cornell, 64, 64, spp=2, ray_t_min=0.0)
