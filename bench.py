@@ -279,8 +279,9 @@ def main():
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
     ap.add_argument("--launch-pass", type=int, default=10,
-                    help="frames of the post-timing one-frame-in-flight pass that measures the "
-                         "path kernel's isolated launch time (roofline.per_launch; 0 = skip)")
+                    help="frames (at most --steps) of the post-timing one-frame-in-flight pass "
+                         "that measures the path kernel's isolated launch time "
+                         "(roofline.per_launch; 0 = skip)")
     args = ap.parse_args()
 
     # Hardware queues per process: HIP's default is 4; with 4 frames in flight on small frames
@@ -484,7 +485,7 @@ def main():
     # so its HIP-event time is its own (roofline.per_launch).
     iso_ms = []
     if args.launch_pass > 0:
-        for _ in range(args.launch_pass):
+        for _ in range(max(1, min(args.launch_pass, args.steps))):
             rt.render_shard_async(push, W, H, rank, world,
                                   (frames[0] if world == 1 else shard_bufs[0]).data_ptr())
             iso_ms.append(float(rt.sync_stats()["main_kernel_ms"]))

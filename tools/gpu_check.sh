@@ -55,6 +55,12 @@ for s in $STEPS; do
         pmcw) run pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
         sqpmc) run sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
         sqpmc2) run sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
+        c5pmcf) run c5pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5pmcf_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
+        c5pmcw) run c5pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5pmcw_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
+        c5sqpmc) run c5sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c5sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
+        c5sqpmc2) run c5sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d "$OUT/c5sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
+        m2sqpmc) run m2sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/m2sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
+        m2sqpmc2) run m2sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/m2sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
         # the chip's VALU issue ceiling and its in-kernel clock; the C3 kernel's in-kernel clock
         valu) run valu_rate 180 tools/build/valu_rate ;;
         valupmc) run valupmc 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/valupmc_$TAG" -o run --output-format csv -- tools/build/valu_rate ;;
