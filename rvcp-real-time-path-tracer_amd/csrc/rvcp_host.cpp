@@ -550,14 +550,14 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         int32_t root4 = 0;
         if (bvh4_collapse(nodes, root, nodes4, root4) > kBvhStack)
             return fail(ctx, RVCP_E_UNSUPPORTED, "BVH traversal stack bound exceeded");
-        // the Bvh4QNode copy rides behind the nodes in the same buffer (FrameArgs::bvh_n4)
+        // only the byte-quantised copy (Bvh4QNode, 64 B) is traversed: it is uploaded alone,
+        // at the start of the node buffer (FrameArgs::bvh_n4 = 0)
         std::vector<Bvh4QNode> q4;
         bvh4_quantize(nodes4, q4);
-        const size_t n4 = nodes4.size();
-        nodes4.resize(n4 + (q4.size() + 1) / 2);
-        if (!q4.empty()) std::memcpy(static_cast<void *>(nodes4.data() + n4), q4.data(), q4.size() * sizeof(Bvh4QNode));
-        ctx->bvh_n4 = (uint32_t)n4;
-        if ((rc = dev_upload<Bvh4Node>(ctx, &ctx->d_bvh_nodes, nodes4.data(), nodes4.size())) ||
+        std::vector<Bvh4Node> qbuf((q4.size() * sizeof(Bvh4QNode) + sizeof(Bvh4Node) - 1) / sizeof(Bvh4Node));
+        if (!q4.empty()) std::memcpy(static_cast<void *>(qbuf.data()), q4.data(), q4.size() * sizeof(Bvh4QNode));
+        ctx->bvh_n4 = 0;
+        if ((rc = dev_upload<Bvh4Node>(ctx, &ctx->d_bvh_nodes, qbuf.data(), qbuf.size())) ||
             (rc = dev_upload<TriRecord>(ctx, &ctx->d_bvh_tris, btri.data(), btri.size())))
             return rc;
         ctx->bvh_root = root4;

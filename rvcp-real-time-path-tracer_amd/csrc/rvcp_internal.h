@@ -206,7 +206,7 @@ struct FrameArgs {
     uint32_t chunk_window;   // grab = pixels this wave consumes in chunk_window ticks (10 ns)
     int32_t accel;           // RVCP_ACCEL_*
     int32_t bvh_root;        // root reference (see BvhNode) when accel == RVCP_ACCEL_BVH
-    uint32_t bvh_n4;         // Bvh4Node count; the Bvh4QNode copy follows them in the buffer
+    uint32_t bvh_n4;         // Bvh4Node offset of the quantised nodes in the node buffer (0)
     uint32_t bvh_slots;      // TriRecord offset of the packed 10-float leaf records (0: buffer start)
     // small frames (path kernels of schedules 3/6): when the surface list fits the resident
     // lanes, spread it over every resident wave, at least spread_min pixels each (0 = off),

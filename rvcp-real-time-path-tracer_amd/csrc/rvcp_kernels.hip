@@ -324,27 +324,21 @@ __device__ __forceinline__ f3 slab_inv(f3 d) {
 
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 
-// 4-wide traversal (Bvh4Node, rvcp_bvh.cpp).  A step loads one node (seven 16-B loads in
-// flight together), tests its four boxes, sorts the children by entry distance (5-comparator
-// network, misses keyed +inf), pushes the hit ones but the nearest -- farthest first -- and
-// continues with the nearest.  Leaves are tested by bvh_leaf.  The slab test may cull only
-// boxes entered beyond the current nearest hit (tn > bt): the hit rule keeps a later face at
-// equal t, so a box entered exactly at bt must still be visited.
+// 4-wide traversal (rvcp_bvh.cpp), over the byte-quantised nodes (Bvh4QNode, 64 B: four 16-B
+// loads in flight together per step).  A step tests the node's four boxes, sorts the children
+// by entry distance (5-comparator network, misses keyed +inf), pushes the hit ones but the
+// nearest -- farthest first -- and continues with the nearest.  Leaves are tested by bvh_leaf.
+// The slab test may cull only boxes entered beyond the current nearest hit (tn > bt): the hit
+// rule keeps a later face at equal t, so a box entered exactly at bt must still be visited.
+// Each child bound is decoded straight into slab time, t = q * (scale * inv) + (origin - o) *
+// inv, with the near and far bytes chosen by the sign of the ray's inverse direction (the
+// ordered slab test: an inverted unused child is never entered); the roundings of that form
+// are relative errors of a few ulp of t, far below the build's box enlargement, and a NaN from
+// it only widens a slab, so nothing a float box keeps is culled.  (The 128-B float nodes the
+// quantised ones come from measured 180 vs 151 ms per C5 frame)
 // LDS = true: the stack is the caller's LDS column (stk[i * kBlock]; the lanes of a wave hit
 // distinct banks whatever their depths); LDS = false: a private array (the pre-pass kernel,
 // whose 1024-thread blocks would need 128 KiB of LDS).
-__device__ __forceinline__ void bvh4_box(float lx, float ly, float lz, float hx, float hy, float hz,
-                                         f3 o, f3 inv, float tmin, float bt, float &key) {
-    const float x0 = (lx - o.x) * inv.x, x1 = (hx - o.x) * inv.x;
-    const float y0 = (ly - o.y) * inv.y, y1 = (hy - o.y) * inv.y;
-    const float z0 = (lz - o.z) * inv.z, z1 = (hz - o.z) * inv.z;
-    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
-                                     __builtin_fmaxf(__builtin_fminf(z0, z1), tmin));
-    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
-                                     __builtin_fminf(__builtin_fmaxf(z0, z1), bt));
-    key = tn <= tf ? tn : __builtin_inff();
-}
-
 __device__ __forceinline__ void bvh4_cas(float &ka, int32_t &ca, float &kb, int32_t &cb) {
     const bool sw = kb < ka;
     const float k = sw ? kb : ka;
@@ -355,16 +349,6 @@ __device__ __forceinline__ void bvh4_cas(float &ka, int32_t &ca, float &kb, int3
     ca = c;
 }
 
-// RVCP_BVH_QUANT: traverse the byte-quantised copy of the nodes (Bvh4QNode, four 16-B loads
-// per step instead of seven).  Each child bound is decoded straight into slab time,
-// t = q * (scale * inv) + (origin - o) * inv, with the near and far bytes chosen by the sign of
-// the ray's inverse direction (the ordered slab test: an inverted unused child is never
-// entered); the roundings of that form are relative errors of a few ulp of t, far below the
-// build's box enlargement, and a NaN from it only widens a slab, so nothing a float box keeps
-// is culled.
-#ifndef RVCP_BVH_QUANT
-#define RVCP_BVH_QUANT 1
-#endif
 __device__ __forceinline__ float ubyte_f(uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xFFu); }
 
 template <bool LDS>
@@ -376,13 +360,10 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
     int32_t priv[LDS ? 1 : kBvhStack];
     int sp = 0;
     int32_t ref = root;
-#if RVCP_BVH_QUANT
     const Bvh4QNode *__restrict__ qn = reinterpret_cast<const Bvh4QNode *>(nodes + n4);
     const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
-#endif
     for (;;) {
         if (ref >= 0) {
-#if RVCP_BVH_QUANT
             const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
             const float4 w0 = q[0], w1 = q[1], w2 = q[2];
             const int4 r = reinterpret_cast<const int4 *>(qn + ref)[3];
@@ -405,16 +386,6 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
                 kk[c] = tn <= tf ? tn : __builtin_inff();
             }
             float k0 = kk[0], k1 = kk[1], k2 = kk[2], k3 = kk[3];
-#else
-            const float4 *q = reinterpret_cast<const float4 *>(nodes + ref);
-            const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
-            const int4 r = reinterpret_cast<const int4 *>(nodes + ref)[6];
-            float k0, k1, k2, k3;
-            bvh4_box(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, o, inv, tmin, bt, k0);
-            bvh4_box(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, o, inv, tmin, bt, k1);
-            bvh4_box(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, o, inv, tmin, bt, k2);
-            bvh4_box(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, o, inv, tmin, bt, k3);
-#endif
             int32_t c0 = r.x, c1 = r.y, c2 = r.z, c3 = r.w;
             bvh4_cas(k0, c0, k1, c1);
             bvh4_cas(k2, c2, k3, c3);

@@ -41,11 +41,13 @@ def test_committed_pmc_summaries_load():
     """The bench line's traffic / VALU fields come from these summaries: they exist for the
     headline C3 kernel and the C5 tiled kernel, and carry per-launch numbers."""
     for wl, kname in [("cornell_1024sq_spp30", "rvcp_spec_path_kernel5"),
-                      ("cornell_plus_100k_tris_1024sq_spp30", "games101_tiled_kernel")]:
+                      ("cornell_plus_100k_tris_1024sq_spp30", "games101_tiled_pool_kernel")]:
         traffic, src = bench.load_traffic(wl, kname)
         assert traffic and traffic > 0 and src.startswith("profiles/")
         busy, frac = bench.load_valu_busy(wl, kname)
         assert 0 < busy <= 1 and 0 < frac <= 1
+    busy, frac = bench.load_valu_busy("cornell_mode2_1024sq_spp30", "rvcp_spec_legacy_kernel")
+    assert 0 < busy <= 1 and 0 < frac <= 1
 
 
 def _negotiate_worker(rank, world, port, outdir):
