@@ -158,13 +158,15 @@ typedef struct rvcp_config {
      * (ray_tracer_games101_branch.comp:109-111 vs vulkan.rs:473-478): element i is
      * ids[4*i] when 4*i < n_ids, else 0.  0 = the intended packed semantics. */
     int32_t lum_id_std140_quirk;
-    /* Kernel schedule, for A/B measurement only: 0 = automatic (3, 6 for large frames, or 5
-     * for meshes of 256+ faces), 1 = one ray per lane per iteration, 2 = shadow + continuation ray per lane per
-     * iteration, 3 = primary pre-pass + 2 over surface pixels (scalar-cache scan), 4 = 3 with
-     * the scan staged through LDS tiles shared by the workgroup, 5 = 4 with one ray per lane
-     * per iteration (shadow ray, then path ray: no empty ray slots), 6 = 3 compiled for 6
-     * waves per SIMD (automatic for frames of 8 Msamples or more).  Every schedule produces
-     * bit-identical frames. */
+    /* Kernel schedule, for A/B measurement only: 0 = automatic (3; 6 for large frames with the
+     * generic scan; 10 for meshes of 256+ faces on frames of 512 Ki samples or more, 5 on
+     * smaller ones), 1 = one ray per lane per iteration, 2 = shadow + continuation ray per
+     * lane per iteration, 3 = primary pre-pass + 2 over surface pixels (scalar-cache scan),
+     * 4 = 3 with the scan staged through LDS tiles shared by the workgroup, 5 = 4 with one ray
+     * per lane per iteration (shadow ray, then path ray: no empty ray slots), 6 = 3 compiled
+     * for 6 waves per SIMD, 10 = 4 with the workgroup's rays pooled in LDS and scanned in
+     * 64-ray passes (7, 8 and 9 are not schedules).  Every schedule produces bit-identical
+     * frames. */
     int32_t kernel_variant;
     /* Acceleration structure: RVCP_ACCEL_NONE (default) scans every triangle like the
      * shader (bit-exact, the parity path).  RVCP_ACCEL_BVH (opt-in, games101 only) builds a
