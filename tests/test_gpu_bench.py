@@ -1,0 +1,54 @@
+"""bench.py end to end on the GPU (the driver's command, a short run): the JSON line carries
+the contract's fields, its roofline is the wall-clock one (frac <= 1, derived from
+ms_per_step), the per-launch pass ran with one frame in flight, and the frame it rendered is
+bit-identical to the oracle's on sampled rows (--save-frame)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle as O
+import rvcp_amd
+from conftest import scene_arrays
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_line_c2(tmp_path):
+    frame_path = tmp_path / "frame.npy"
+    env = dict(os.environ)
+    env.pop("RVCP_LIB", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c2",
+                        "--steps", "6", "--warmup", "2", "--no-cpu-baseline",
+                        "--save-frame", str(frame_path)],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 6 and d["warmup"] == 2
+    W, H, spp = 384, 384, 10
+    assert d["value"] == pytest.approx(W * H * spp / (d["ms_per_step"] / 1000.0) / 1e6, rel=2e-3)
+    rl = d["roofline"]
+    assert rl["bound"] == "valu" and rl["peak"] == 157.3
+    flop = rl["tests_per_launch"] * 52
+    assert rl["achieved"] == pytest.approx(flop / (d["ms_per_step"] / 1000.0) / 1e12, rel=2e-2)
+    assert 0 < rl["frac"] <= 1 and 0 < rl["frac_executed"] <= rl["frac"]
+    pl = rl["per_launch"]
+    assert pl["frames"] >= 1 and 0 < pl["frac"] <= 1
+    assert pl["kernel_ms_min"] <= pl["kernel_ms"]
+    # the saved frame is the oracle's
+    frame = np.load(frame_path)
+    sc = rvcp_amd.Scene.default()
+    cfg = rvcp_amd.abi.make_config(spp=spp)
+    for y in (0, 131, 200, 383):
+        _, o_rgba, _ = O.render(scene_arrays(sc), sc.push_constant(123.0), cfg, W, H,
+                                rect=(0, y, W, 1), want_linear=False)
+        assert np.array_equal(frame[y:y + 1], o_rgba), y
