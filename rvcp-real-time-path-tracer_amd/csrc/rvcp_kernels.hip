@@ -284,33 +284,40 @@ __device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, f
 // leaf costs one memory round trip instead of one per triangle.  The leaf-ordered triangles
 // are packed as 10 floats per slot (v0, e1, e2, face id bits; leaves start at even slots, so
 // 16-B aligned, rvcp_host.cpp): ceil(2.5 cnt) 16-B loads.
+#ifndef RVCP_BVH_LEAF_CHUNK
+#define RVCP_BVH_LEAF_CHUNK 4      // triangles loaded together (one memory round trip; 2: 2 % slower)
+#endif
 __device__ __forceinline__ void bvh_leaf(const TriRecord *__restrict__ btri, int32_t ref, f3 o, f3 d,
                                          float tmin, float &bt, int &best, uint32_t slots = 0) {
     const uint32_t code = ~(uint32_t)ref;
     const uint32_t first = code >> 5, cnt = (code & 31u) + 1u;
-    const float4 *base = reinterpret_cast<const float4 *>(
-        reinterpret_cast<const float *>(btri + slots) + 10u * first);
-    const uint32_t nld = (10u * cnt + 3u) >> 2;
-    float4 W[(10 * kBvhLeafMax + 3) / 4];
+    constexpr uint32_t kCh = RVCP_BVH_LEAF_CHUNK;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += kCh) {
+        const float4 *base = reinterpret_cast<const float4 *>(
+            reinterpret_cast<const float *>(btri + slots) + 10u * (first + c0));
+        const uint32_t nc = cnt - c0 < kCh ? cnt - c0 : kCh;
+        const uint32_t nld = (10u * nc + 3u) >> 2;
+        float4 W[(10 * kCh + 3) / 4];
 #pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)((10 * kBvhLeafMax + 3) / 4); ++k)
-        if (k < nld) W[k] = base[k];
-    const float *F = reinterpret_cast<const float *>(W);
+        for (uint32_t k = 0; k < (uint32_t)((10 * kCh + 3) / 4); ++k)
+            if (k < nld) W[k] = base[k];
+        const float *F = reinterpret_cast<const float *>(W);
 #pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)kBvhLeafMax; ++k) {
-        if (k < cnt) {
-            TriRecord T;
+        for (uint32_t k = 0; k < kCh; ++k) {
+            if (k < nc) {
+                TriRecord T;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                T.v0[c] = F[10 * k + c];
-                T.e1[c] = F[10 * k + 3 + c];
-                T.e2[c] = F[10 * k + 6 + c];
-            }
-            float t;
-            const int id = __float_as_int(F[10 * k + 9]);
-            if (tri_accept(T, o, d, tmin, bt, t) && (t < bt || id > best)) {
-                bt = t;
-                best = id;
+                for (int c = 0; c < 3; ++c) {
+                    T.v0[c] = F[10 * k + c];
+                    T.e1[c] = F[10 * k + 3 + c];
+                    T.e2[c] = F[10 * k + 6 + c];
+                }
+                float t;
+                const int id = __float_as_int(F[10 * k + 9]);
+                if (tri_accept(T, o, d, tmin, bt, t) && (t < bt || id > best)) {
+                    bt = t;
+                    best = id;
+                }
             }
         }
     }
@@ -1818,6 +1825,8 @@ __global__ __launch_bounds__(kBlock, MIN_WAVES) void games101_path_kernel(
 
 // Opt-in BVH (RVCP_ACCEL_BVH): the variant-3 machine with per-lane BVH traversal in place of
 // the brute-force scan.
+// (Measured and not kept: private scratch stacks, the path state in LDS columns, 5 waves per SIMD
+// (96 VGPRs with two-triangle leaf chunks): all slower)
 __global__ __launch_bounds__(kBlock, 4) void games101_bvh_path_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
