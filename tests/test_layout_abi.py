@@ -116,6 +116,18 @@ def test_library_links_no_oracle():
     assert "oracle" not in ldd and "amdhip64" in ldd
 
 
+def test_product_library_reads_no_debug_knobs():
+    """Experiment knobs (RVCP_DEBUG_*, RVCP_NO_SPECIALIZE, RVCP_SPEC_GROUP*) live only in the
+    -DRVCP_DEBUG_KNOBS build (csrc/build/librvcp_debug.so); the product library must not
+    change behaviour with the environment."""
+    blob = open(abi.LIB_PATH, "rb").read()
+    for knob in (b"RVCP_DEBUG_", b"RVCP_NO_SPECIALIZE", b"RVCP_SPEC_GROUP", b"RVCP_JIT_FLAGS"):
+        assert knob not in blob, knob
+    dbg = os.path.join(os.path.dirname(abi.LIB_PATH), "librvcp_debug.so")
+    if os.path.exists(dbg):
+        assert b"RVCP_DEBUG_TIMELINE" in open(dbg, "rb").read()
+
+
 def test_library_has_gfx950_code_object():
     blob = open(abi.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob          # the offload bundle targets gfx950
