@@ -125,6 +125,39 @@ __device__ __forceinline__ float rcp_ieee(float den) {
     return f;
 }
 
+// v / s for the three components of v, bit-identical to the IEEE quotients, for the shader's
+// vector-by-scalar divisions.  y = RN(1/s) (rcp_ieee) is shared; each quotient
+// is q = RN(v y) refined by Markstein's step q' = RN(q + r y) with r = v - s q exact by fma,
+// which is the correctly rounded v / s whenever y = RN(1/s) and no quantity leaves the normal
+// range -- guaranteed when s and every nonzero |v_i| lie in [2^-50, 2^50].  The step is
+// written -RN(-(r y) - q) so that a -0 numerator keeps its -0 quotient (RN(q + r y) would give
+// +0).  A lane outside that box (zero, tiny, huge, inf or NaN operands) takes the IEEE
+// divisions.  tests/test_markstein_cpu.py checks the same arithmetic against IEEE division.
+__device__ __forceinline__ float quot_refine(float v, float s, float y) {
+    const float q = v * y;
+    const float r = __builtin_fmaf(-s, q, v);
+    return -__builtin_fmaf(-r, y, -q);
+}
+__device__ __forceinline__ bool quot_box(f3 v) {
+    // |v_i| as bits << 1 (sign dropped); zero maps to 0xFFFFFFFF under the -1 of the lower test
+    const uint32_t bx = __float_as_uint(v.x) << 1, by = __float_as_uint(v.y) << 1,
+                   bz = __float_as_uint(v.z) << 1;
+    const uint32_t hi = max(max(bx, by), bz);
+    const uint32_t lo = min(min(bx - 1u, by - 1u), bz - 1u);
+    return (hi <= (0x58800000u << 1)) & (lo >= (0x26800000u << 1) - 1u);   // 2^50, 2^-50
+}
+#ifndef RVCP_DIV_SHARED
+#define RVCP_DIV_SHARED 1
+#endif
+__device__ __forceinline__ f3 divs_y(f3 v, float s, float y) {
+    if (!RVCP_DIV_SHARED) return divs(v, s);
+    f3 o = mk(quot_refine(v.x, s, y), quot_refine(v.y, s, y), quot_refine(v.z, s, y));
+    const bool ok = (s >= 0x1p-50f) & (s <= 0x1p50f) & quot_box(v);
+    if (__builtin_expect(!ok, 0)) o = divs(v, s);
+    return o;
+}
+__device__ __forceinline__ f3 divs_pos(f3 v, float s) { return divs_y(v, s, rcp_ieee(s)); }
+
 // The scan's 1 / den: rcp_ieee, except that a zero or NaN denominator keeps the fast result
 // (NaN) instead of taking the IEEE division (+-inf / NaN).  Exact for the scan's decision: with
 // den = +-0 the shader's t = f * dot(s2, e2) is +-inf or NaN and fails t >= t_min & t <= t_max
@@ -513,13 +546,13 @@ __device__ __forceinline__ bool nee_sample(const FrameArgs &A, const LightRecord
                       muls(ld3(L.v2), x * y));                                     // :324
     const f3 dv = sub(Xp, S_pos);
     dist = len(dv);                                                                // :438
-    ws = divs(dv, dist);                                                           // :439
+    ws = divs_pos(dv, dist);                                                       // :439
     const float cosp = dot(S_nrm, ws);
     const f3 f = cosp > 0.0f ? alb_pi : mk(0, 0, 0);                               // :344-349
     C = mulv(mulv(att, ld3(L.le)), f);                                             // :450-458
     C = muls(C, cosp);
     C = muls(C, dot(ld3(L.n), neg(ws)));
-    C = divs(C, dist * dist * A.light_pdf);
+    C = divs_pos(C, dist * dist * A.light_pdf);
     return true;
 }
 
@@ -541,7 +574,7 @@ __device__ __forceinline__ bool brdf_continue(const FrameArgs &A, const MatRecor
     const f3 f = cosw > 0.0f ? ld3(m.alb_pi) : mk(0, 0, 0);
     const float pdf = dot(wi, S_nrm) > 0.0f ? 0.5f / 3.1415926f : 0.0f;            // :358-365
     const float denom = __builtin_fmaxf(0.1f, pdf) * A.rr;
-    att = mulv(att, divs(muls(f, cosw), denom));                                   // :465-471
+    att = mulv(att, divs_pos(muls(f, cosw), denom));                                   // :465-471
     return true;
 }
 
@@ -555,7 +588,7 @@ __device__ __forceinline__ void brdf_finish(const FrameArgs &A, f3 alb_pi, f3 S_
     const f3 f = cosw > 0.0f ? alb_pi : mk(0, 0, 0);
     const float pdf = dot(wi, S_nrm) > 0.0f ? 0.5f / 3.1415926f : 0.0f;
     const float denom = __builtin_fmaxf(0.1f, pdf) * A.rr;
-    att = mulv(att, divs(muls(f, cosw), denom));
+    att = mulv(att, divs_pos(muls(f, cosw), denom));
 }
 
 // random_in_unit_sphere (:195-201) for every lane with `need`, cooperatively: each round the
@@ -745,6 +778,7 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
     const uint32_t lane = lane_id();
     Queue q = queue_init(A);
     const float sppf = (float)A.spp;
+    const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
 
     int action = A_NEED, kind = K_PRIMARY;
     uint32_t pix = 0, k = 0, depth = 0, trav = 0, iters = 0;
@@ -777,7 +811,7 @@ __global__ __launch_bounds__(kBlock) void games101_kernel(
                 }
             }
             if (action == A_END) {                                  // color += L / SPP (:495)
-                acc = add(acc, divs(col, sppf));
+                acc = add(acc, divs_y(col, sppf, inv_spp));
                 k += 1;
                 if (k >= A.spp) {
                     store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
@@ -901,6 +935,7 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
     const uint32_t lane = lane_id();
     Queue q = queue_init(A);
     const float sppf = (float)A.spp;
+    const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
 
     bool need_pixel = true, done = false;
     uint32_t pix = 0, k = 0, depth = 0, trav = 0, iters = 0;
@@ -1004,7 +1039,7 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
         for (;;) {
             if (ended) {
                 ended = false;
-                acc = add(acc, divs(col, sppf));
+                acc = add(acc, divs_y(col, sppf, inv_spp));
                 k += 1;
                 if (k >= A.spp) {
                     store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
@@ -1223,6 +1258,7 @@ __device__ __forceinline__ void path_body(
     }
     Queue q = queue_init(Q);
     const float sppf = (float)A.spp;
+    const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
 
     bool need_pixel = true, done = false, ended = false, surf_ev = false;
     // the pixel's surface record (cached primary hit, pixel index) is re-read from the list at
@@ -1244,7 +1280,7 @@ __device__ __forceinline__ void path_body(
             if (ended) {                                            // color += L / SPP (:495)
                 ended = false;
                 if (LDS_STATE) acc = st_get3(7);
-                acc = add(acc, divs(col, sppf));
+                acc = add(acc, divs_y(col, sppf, inv_spp));
                 if (LDS_STATE) st_put3(7, acc);
                 k += 1;
                 if (k >= A.spp) {
@@ -1985,6 +2021,13 @@ __device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d
 
 constexpr int L_IDLE = 0, L_TRACE = 1, L_SCATTER = 2, L_END = 3;
 
+// RVCP_LEGACY_DEFER: the most lanes left ending a sample that sit out one trace (below).  16
+// measured best: sphere room 0.367 -> 0.345 ms, mode 2 on the C3 frame 2.237 -> 2.156 ms per
+// frame (profiles/r03v_m2_defer_sweep.log; 8, 24, 32, 40 and 64 less good).
+#ifndef RVCP_LEGACY_DEFER
+#define RVCP_LEGACY_DEFER 16
+#endif
+
 }  // namespace
 
 __device__ __forceinline__ void legacy_body(
@@ -1998,6 +2041,8 @@ __device__ __forceinline__ void legacy_body(
     const uint32_t lane = lane_id();
     Queue q = queue_init(A);
     const float sppf = (float)A.spp;
+    const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
+    const float inv_rr = rcp_ieee(A.rr);
 
     int st = L_IDLE;
     bool need_pixel = true, done = false, primary = false;
@@ -2020,7 +2065,7 @@ __device__ __forceinline__ void legacy_body(
                 acc = add(acc, col);
                 k += 1;
                 if (k >= A.spp) {
-                    store_pixel(pix, divs(acc, sppf), A, unorm_t, out_rgba, out_lin);   // :819-821
+                    store_pixel(pix, divs_y(acc, sppf, inv_spp), A, unorm_t, out_rgba, out_lin);   // :819-821
                     need_pixel = true;
                     st = L_IDLE;
                 } else {                                            // next sample, cached hit
@@ -2104,7 +2149,7 @@ __device__ __forceinline__ void legacy_body(
                     } else if (rnd(seed, ridx) >= A.rr) {                   // :679-681
                         st = L_END;
                     } else {
-                        att = divs(att, A.rr);                              // :683
+                        att = divs_y(att, A.rr, inv_rr);                     // :683
                         if (left == 0u) {
                             st = L_END;                                     // :633
                         } else {
@@ -2115,6 +2160,13 @@ __device__ __forceinline__ void legacy_body(
                 }
             }
             if (!__any(st == L_END)) break;
+#if RVCP_LEGACY_DEFER
+            // Lanes whose sample ended in this scatter (bounce limit) sit out one trace when
+            // few of them did and other lanes have rays: their next sample's scatter then runs
+            // inside the next settle with the whole wave's instead of in a nearly empty pass
+            // now.  Timing only: each lane's own sequence of operations is unchanged.
+            if (__any(st == L_TRACE) && __popcll(__ballot(st == L_END)) <= RVCP_LEGACY_DEFER) break;
+#endif
         }
         if (!__any(st == L_TRACE)) break;
         iters += 1;
@@ -2211,7 +2263,7 @@ __device__ __forceinline__ void legacy_body(
                     // miss / light: every sample returns this same color without touching the
                     // RNG; sum it SPP times in order (:816-818)
                     for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, col);
-                    store_pixel(pix, divs(acc, sppf), A, unorm_t, out_rgba, out_lin);
+                    store_pixel(pix, divs_y(acc, sppf, inv_spp), A, unorm_t, out_rgba, out_lin);
                     need_pixel = true;
                     st = L_IDLE;
                 } else {
