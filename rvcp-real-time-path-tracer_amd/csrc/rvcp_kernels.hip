@@ -126,7 +126,7 @@ __device__ __forceinline__ float rcp_ieee(float den) {
 }
 
 // v / s for the three components of v, bit-identical to the IEEE quotients, for the shader's
-// vector-by-scalar divisions (DESIGN.md §3.7).  y = RN(1/s) (rcp_ieee) is shared; each quotient
+// vector-by-scalar divisions (DESIGN.md §3.8).  y = RN(1/s) (rcp_ieee) is shared; each quotient
 // is q = RN(v y) refined by Markstein's step q' = RN(q + r y) with r = v - s q exact by fma,
 // which is the correctly rounded v / s whenever y = RN(1/s) and no quantity leaves the normal
 // range -- guaranteed when s and every nonzero |v_i| lie in [2^-50, 2^50].  The step is
