@@ -40,6 +40,7 @@
 #include <list>
 #include <memory>
 #include <mutex>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -95,22 +96,15 @@ const RtcApi &rtc()
 // ------------------------------------------------------------------ source generator ----
 // A value of the generated expression graph: an exact zero, a named float, or a non-zero
 // literal (the triangle's own float, written as its bit pattern).
+// `key` spells the value's whole expression (operands by their own keys), so that two
+// triangles' equal expressions -- e.g. the shared denominator of an axis-aligned quad's two
+// triangles -- are recognised and computed once.
 struct Val {
     enum Kind { kZero, kVar, kLit } kind = kZero;
     std::string name;
     float lit = 0.0f;
+    std::string key = "0";
 };
-
-Val zero() { return Val{}; }
-Val var(const std::string &n) { Val v; v.kind = Val::kVar; v.name = n; return v; }
-Val lit_or_zero(float x)
-{
-    if (x == 0.0f) return zero();          // +0 and -0: dropped terms (see the header)
-    Val v;
-    v.kind = Val::kLit;
-    v.lit = x;
-    return v;
-}
 
 std::string lit_text(float x)
 {
@@ -121,39 +115,66 @@ std::string lit_text(float x)
     return buf;
 }
 
+Val zero() { return Val{}; }
+Val var(const std::string &n) { Val v; v.kind = Val::kVar; v.name = n; v.key = n; return v; }
+Val lit_or_zero(float x)
+{
+    if (x == 0.0f) return zero();          // +0 and -0: dropped terms (see the header)
+    Val v;
+    v.kind = Val::kLit;
+    v.lit = x;
+    v.key = lit_text(x);
+    return v;
+}
+
 struct Gen {
     std::string out;
     int n = 0;
+    // expressions already computed by an earlier test of the same scan: key -> variable (the
+    // scan's temporaries are declared at function scope, so a later test can use them)
+    std::map<std::string, std::string> *seen = nullptr;
 
     std::string prefix;
     std::string text(const Val &v) const { return v.kind == Val::kLit ? lit_text(v.lit) : v.name; }
-    Val tmp(const std::string &expr)
+    Val tmp(const std::string &expr, const std::string &key)
     {
+        if (seen) {
+            const auto it = seen->find(key);
+            if (it != seen->end()) {
+                Val v = var(it->second);
+                v.key = key;
+                return v;
+            }
+        }
         const std::string name = prefix + "r" + std::to_string(n++);
-        out += "        const float " + name + " = " + expr + ";\n";
-        return var(name);
+        out += "    const float " + name + " = " + expr + ";\n";
+        if (seen) (*seen)[key] = name;
+        Val v = var(name);
+        v.key = key;
+        return v;
     }
     Val mul(const Val &a, const Val &b)
     {
         if (a.kind == Val::kZero || b.kind == Val::kZero) return zero();
-        return tmp(text(a) + " * " + text(b));
+        return tmp(text(a) + " * " + text(b), "m(" + a.key + "," + b.key + ")");
     }
     Val neg(const Val &a)
     {
         if (a.kind == Val::kZero) return a;
         if (a.kind == Val::kLit) return lit_or_zero(-a.lit);
-        return tmp("-" + a.name);
+        return tmp("-" + a.name, "n(" + a.key + ")");
     }
     Val fma(const Val &a, const Val &b, const Val &c)
     {
         if (a.kind == Val::kZero || b.kind == Val::kZero) return c;
         if (c.kind == Val::kZero) return mul(a, b);
-        return tmp("__builtin_fmaf(" + text(a) + ", " + text(b) + ", " + text(c) + ")");
+        return tmp("__builtin_fmaf(" + text(a) + ", " + text(b) + ", " + text(c) + ")",
+                   "f(" + a.key + "," + b.key + "," + c.key + ")");
     }
     Val sub(const Val &a, const Val &b)       // a - b; x - (+-0) == x exactly, so b = 0 drops
     {
         if (b.kind == Val::kZero) return a;
-        return tmp(text(a) + " - " + text(b));
+        return tmp(text(a) + " - " + text(b), "s(" + a.key + "," + b.key + ")");
     }
     // dot = fma(z, z', fma(y, y', x*x')), cross_i = fma(a_j, b_k, -(a_k*b_j)): DESIGN.md §3.1
     Val dot(const Val *a, const Val *b) { return fma(a[2], b[2], fma(a[1], b[1], mul(a[0], b[0]))); }
@@ -170,9 +191,10 @@ struct Gen {
 // its acceptance (`accept`: the compares with `t <= bt` and the update); false when it can
 // never accept.
 bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, uint32_t index,
-                   const char *r)
+                   const char *r, std::map<std::string, std::string> &seen)
 {
     Gen g;
+    g.seen = &seen;
     g.prefix = "t" + std::to_string(index) + r + "_";
     const std::string R(r);
     Val o[3] = {var("o" + R + ".x"), var("o" + R + ".y"), var("o" + R + ".z")};
@@ -187,20 +209,23 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     Val s1[3], s2[3];
     g.cross(d, e2, s1);                                                        // :250
     const Val den = g.dot(s1, e1);                                             // :254
-    if (den.kind == Val::kZero) return false;
+    if (den.kind == Val::kZero) {
+        decl += g.out;          // its temporaries may be named by a later test (`seen`)
+        return false;
+    }
     g.cross(s, e1, s2);                                                        // :251
     const Val n1 = g.dot(s1, s);
     const Val n2 = g.dot(s2, d);
     const Val tt = g.dot(s2, e2);
-    const Val f = g.tmp("RVCP_SPEC_RCP(" + g.text(den) + ")");               // :254
+    const Val f = g.tmp("RVCP_SPEC_RCP(" + g.text(den) + ")", "r(" + den.key + ")");   // :254
     // t = f * dot(s2, e2) (:255); a vanished dot leaves t = +-0 or NaN, rejected by
     // t >= t_min > 0 in both forms
-    const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.tmp(f.name + " * " + g.text(tt)).name;
+    const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.mul(f, tt).name;
     std::string cond;
     auto add = [&](const std::string &c) { cond += (cond.empty() ? "" : " & ") + c; };
     std::string b1, b2;
-    if (n1.kind != Val::kZero) b1 = g.tmp(f.name + " * " + g.text(n1)).name;   // :256
-    if (n2.kind != Val::kZero) b2 = g.tmp(f.name + " * " + g.text(n2)).name;   // :257
+    if (n1.kind != Val::kZero) b1 = g.mul(f, n1).name;                        // :256
+    if (n2.kind != Val::kZero) b2 = g.mul(f, n2).name;                        // :257
     if (!b1.empty()) add("(" + b1 + " >= 0.0f)");
     if (!b2.empty()) add("(" + b2 + " >= 0.0f)");
     if (!b1.empty() && !b2.empty()) add("(" + b1 + " + " + b2 + " <= 1.0f)");
@@ -229,16 +254,21 @@ void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *c
                int n_rays, uint32_t group)
 {
     const uint32_t units = n * (uint32_t)n_rays;
+    std::map<std::string, std::string> seen;
     for (uint32_t u0 = 0; u0 < units; u0 += group) {
         std::string decl, accept;
         bool used[2] = {false, false};
         for (uint32_t u = u0; u < units && u < u0 + group; u++) {
             const int r = (int)(u % (uint32_t)n_rays);
-            if (emit_triangle(decl, accept, tri[u / (uint32_t)n_rays], u / (uint32_t)n_rays, rays[r]))
+            if (emit_triangle(decl, accept, tri[u / (uint32_t)n_rays], u / (uint32_t)n_rays, rays[r],
+                              seen))
                 used[r] = true;
         }
-        if (accept.empty()) continue;
-        out += "    {\n" + decl + accept + "    }\n";
+        if (accept.empty()) {
+            out += decl;
+            continue;
+        }
+        out += decl + "    {\n" + accept + "    }\n";
         for (int r = 0; r < n_rays; r++)
             if (used[r]) out += "    RVCP_SPEC_COMMIT(bt" + std::string(rays[r]) + ", best" + std::string(rays[r]) + ");\n";
     }
