@@ -79,6 +79,8 @@ struct rvcp_ctx {
     // primary pre-pass output (variant 3): compact list of surface pixels
     SurfRecord *d_surf = nullptr;
     size_t cap_surf = 0;
+    float *d_acc = nullptr;         // linear colours for tonemap_kernel when the caller wants none
+    size_t cap_acc = 0;
 
     // staging for the synchronous host API
     uint32_t *d_rgba = nullptr;
@@ -442,6 +444,7 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     (void)hipFree(ctx->d_rgba);
     (void)hipFree(ctx->d_lin);
     (void)hipFree(ctx->d_surf);
+    (void)hipFree(ctx->d_acc);
     (void)hipFree(ctx->d_timeline);
     (void)hipFree(ctx->d_pack_rgba);
     (void)hipFree(ctx->d_pack_lin);
@@ -748,9 +751,22 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                     HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)A.n_pixels * sizeof(SurfRecord)));
                     ctx->cap_surf = A.n_pixels;
                 }
+                // these kernels leave linear colours and tonemap_kernel stores the bytes: into
+                // the caller's linear buffer, else the context's scratch
+                float *lin = (float *)d_linear_rgb;
+                if (!lin) {
+                    if (ctx->cap_acc < A.n_pixels) {
+                        (void)hipFree(ctx->d_acc);
+                        ctx->d_acc = nullptr;
+                        ctx->cap_acc = 0;
+                        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_acc, (size_t)A.n_pixels * 12));
+                        ctx->cap_acc = A.n_pixels;
+                    }
+                    lin = ctx->d_acc;
+                }
                 rc = rvcp_launch_games101_v3(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
                                              ctx->d_mats, ctx->d_lights, ctx->d_gamma,
-                                             (uint32_t *)d_rgba8, (float *)d_linear_rgb,
+                                             (uint32_t *)d_rgba8, lin,
                                              ctx->d_counters, ctx->d_surf, ctx->d_shade,
                                              ctx->d_bvh_nodes, ctx->d_bvh_tris,
                                              blocks, s, ctx->evm,

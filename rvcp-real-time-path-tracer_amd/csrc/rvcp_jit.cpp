@@ -95,15 +95,19 @@ const RtcApi &rtc()
 
 // ------------------------------------------------------------------ source generator ----
 // A value of the generated expression graph: an exact zero, a named float, or a non-zero
-// literal (the triangle's own float, written as its bit pattern).
-// `key` spells the value's whole expression (operands by their own keys), so that two
-// triangles' equal expressions -- e.g. the shared denominator of an axis-aligned quad's two
-// triangles -- are recognised and computed once.
+// literal (the triangle's own float, written as its bit pattern), each with a sign: the value
+// is -|x| when `neg` is set.  Signs are carried, not computed -- RN(-x) = -RN(x), so a
+// product or fma with negated operands is the negation of the one with positive operands
+// (exactly, up to the sign of a zero result, which the header's argument already allows) --
+// and `key` spells the magnitude's whole expression with commutative operands in a fixed
+// order, so that equal expressions anywhere in the scan are computed once: the shared
+// denominator of an axis-aligned quad's two triangles, the products d.y * c they repeat, ...
 struct Val {
     enum Kind { kZero, kVar, kLit } kind = kZero;
-    std::string name;
-    float lit = 0.0f;
-    std::string key = "0";
+    std::string name;       // kVar: the variable holding the magnitude
+    float lit = 0.0f;       // kLit: the magnitude (> 0)
+    bool neg = false;
+    std::string key = "0";  // the magnitude's expression
 };
 
 std::string lit_text(float x)
@@ -122,10 +126,22 @@ Val lit_or_zero(float x)
     if (x == 0.0f) return zero();          // +0 and -0: dropped terms (see the header)
     Val v;
     v.kind = Val::kLit;
-    v.lit = x;
-    v.key = lit_text(x);
+    v.lit = std::fabs(x);
+    v.neg = std::signbit(x);
+    v.key = lit_text(v.lit);
     return v;
 }
+Val negate(Val v)
+{
+    if (v.kind != Val::kZero) v.neg = !v.neg;
+    return v;
+}
+Val magnitude(Val v)
+{
+    v.neg = false;
+    return v;
+}
+std::string signed_key(const Val &v) { return (v.neg ? "-" : "+") + v.key; }
 
 struct Gen {
     std::string out;
@@ -135,7 +151,11 @@ struct Gen {
     std::map<std::string, std::string> *seen = nullptr;
 
     std::string prefix;
-    std::string text(const Val &v) const { return v.kind == Val::kLit ? lit_text(v.lit) : v.name; }
+    std::string text(const Val &v) const
+    {
+        if (v.kind == Val::kLit) return lit_text(v.neg ? -v.lit : v.lit);
+        return v.neg ? "(-" + v.name + ")" : v.name;
+    }
     Val tmp(const std::string &expr, const std::string &key)
     {
         if (seen) {
@@ -153,28 +173,36 @@ struct Gen {
         v.key = key;
         return v;
     }
+    // |a| * |b| (commutative: operands in key order), carrying the sign
     Val mul(const Val &a, const Val &b)
     {
         if (a.kind == Val::kZero || b.kind == Val::kZero) return zero();
-        return tmp(text(a) + " * " + text(b), "m(" + a.key + "," + b.key + ")");
+        const bool swap = b.key < a.key;
+        const Val &x = swap ? b : a, &y = swap ? a : b;
+        Val r = tmp(text(magnitude(x)) + " * " + text(magnitude(y)), "m(" + x.key + "," + y.key + ")");
+        r.neg = a.neg != b.neg;
+        return r;
     }
-    Val neg(const Val &a)
-    {
-        if (a.kind == Val::kZero) return a;
-        if (a.kind == Val::kLit) return lit_or_zero(-a.lit);
-        return tmp("-" + a.name, "n(" + a.key + ")");
-    }
+    Val neg(const Val &a) { return negate(a); }
+    // fma(a, b, c) = s * fma(|a|, |b|, s * c) with s the product's sign
     Val fma(const Val &a, const Val &b, const Val &c)
     {
         if (a.kind == Val::kZero || b.kind == Val::kZero) return c;
         if (c.kind == Val::kZero) return mul(a, b);
-        return tmp("__builtin_fmaf(" + text(a) + ", " + text(b) + ", " + text(c) + ")",
-                   "f(" + a.key + "," + b.key + "," + c.key + ")");
+        const bool sp = a.neg != b.neg;
+        const Val cc = sp ? negate(c) : c;
+        const bool swap = b.key < a.key;
+        const Val &x = swap ? b : a, &y = swap ? a : b;
+        Val r = tmp("__builtin_fmaf(" + text(magnitude(x)) + ", " + text(magnitude(y)) + ", " +
+                        text(cc) + ")",
+                    "f(" + x.key + "," + y.key + "," + signed_key(cc) + ")");
+        r.neg = sp;
+        return r;
     }
     Val sub(const Val &a, const Val &b)       // a - b; x - (+-0) == x exactly, so b = 0 drops
     {
         if (b.kind == Val::kZero) return a;
-        return tmp(text(a) + " - " + text(b), "s(" + a.key + "," + b.key + ")");
+        return tmp(text(a) + " - " + text(b), "s(" + signed_key(a) + "," + signed_key(b) + ")");
     }
     // dot = fma(z, z', fma(y, y', x*x')), cross_i = fma(a_j, b_k, -(a_k*b_j)): DESIGN.md §3.1
     Val dot(const Val *a, const Val *b) { return fma(a[2], b[2], fma(a[1], b[1], mul(a[0], b[0]))); }
@@ -217,15 +245,17 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     const Val n1 = g.dot(s1, s);
     const Val n2 = g.dot(s2, d);
     const Val tt = g.dot(s2, e2);
-    const Val f = g.tmp("RVCP_SPEC_RCP(" + g.text(den) + ")", "r(" + den.key + ")");   // :254
+    // the reciprocal of the signed denominator (its sign stays inside: v_rcp's symmetry is
+    // not relied on)
+    const Val f = g.tmp("RVCP_SPEC_RCP(" + g.text(den) + ")", "r(" + signed_key(den) + ")");   // :254
     // t = f * dot(s2, e2) (:255); a vanished dot leaves t = +-0 or NaN, rejected by
     // t >= t_min > 0 in both forms
-    const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.mul(f, tt).name;
+    const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.text(g.mul(f, tt));
     std::string cond;
     auto add = [&](const std::string &c) { cond += (cond.empty() ? "" : " & ") + c; };
     std::string b1, b2;
-    if (n1.kind != Val::kZero) b1 = g.mul(f, n1).name;                        // :256
-    if (n2.kind != Val::kZero) b2 = g.mul(f, n2).name;                        // :257
+    if (n1.kind != Val::kZero) b1 = g.text(g.mul(f, n1));                     // :256
+    if (n2.kind != Val::kZero) b2 = g.text(g.mul(f, n2));                     // :257
     if (!b1.empty()) add("(" + b1 + " >= 0.0f)");
     if (!b2.empty()) add("(" + b2 + " >= 0.0f)");
     if (!b1.empty() && !b2.empty()) add("(" + b1 + " + " + b2 + " <= 1.0f)");

@@ -203,6 +203,17 @@ __device__ __forceinline__ void store_pixel(uint32_t pix, f3 acc, const FrameArg
     }
 }
 
+// The pre-pass and the path kernels (variants 3-6, 10, BVH) leave each finished pixel's linear
+// colour in `lin` (the caller's linear output, or a scratch buffer of the context) and
+// tonemap_kernel converts the frame afterwards, one pixel per lane: the eight dependent table
+// probes per channel of gamma_u8 otherwise ran once per finished pixel inside the path kernel,
+// nearly always for a single lane of its wave.
+__device__ __forceinline__ void store_acc(uint32_t pix, f3 acc, float *__restrict__ lin) {
+    lin[3 * (size_t)pix + 0] = acc.x;
+    lin[3 * (size_t)pix + 1] = acc.y;
+    lin[3 * (size_t)pix + 2] = acc.z;
+}
+
 // One exact ray-triangle test (is_intersect_with_face, :238-260) with the nearest-hit rule
 // of get_intersection_with_scene (:291), in two stages.  Stage 1: the products that do not
 // need 1/den -- s = o - v0, s1 = d x e2, s2 = s x e1, den = s1.e1, n1 = s1.s, n2 = s2.d.
@@ -1142,7 +1153,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
             const f3 Ls = divs(L, (float)A.spp);
             f3 acc = mk(0, 0, 0);
             for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, Ls);
-            store_pixel(pix, acc, A, gamma_t, out_rgba, out_lin);
+            store_acc(pix, acc, out_lin);
         } else {
             is_surf = true;
         }
@@ -1284,7 +1295,7 @@ __device__ __forceinline__ void path_body(
                 if (LDS_STATE) st_put3(7, acc);
                 k += 1;
                 if (k >= A.spp) {
-                    store_pixel(surf[pslot].pix, acc, A, gamma_t, out_rgba, out_lin);
+                    store_acc(surf[pslot].pix, acc, out_lin);
                     need_pixel = true;
                 } else {
                     depth = 0;
@@ -1938,6 +1949,21 @@ __global__ void assemble_kernel(const uint32_t *__restrict__ gathered, uint32_t 
         dst[x] = src[x];
 }
 
+// The frame's tone map + UNORM8 store after the v3-family kernels (store_acc above): the
+// threshold table in LDS, one pixel per lane.
+constexpr uint32_t kToneBlock = 256;
+__global__ __launch_bounds__(kToneBlock) void tonemap_kernel(const float *__restrict__ lin, uint32_t n,
+                                                             const float *__restrict__ gamma_t,
+                                                             uint32_t *__restrict__ out_rgba)
+{
+    __shared__ float T[257];
+    T[threadIdx.x] = gamma_t[threadIdx.x];
+    if (threadIdx.x == 0) T[256] = gamma_t[256];
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * kToneBlock + threadIdx.x; i < n; i += gridDim.x * kToneBlock)
+        out_rgba[i] = pack_rgba(mk(lin[3 * (size_t)i], lin[3 * (size_t)i + 1], lin[3 * (size_t)i + 2]), T);
+}
+
 __global__ void fill_kernel(uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
                             uint32_t n, uint32_t rgba)
 {
@@ -2406,6 +2432,12 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                            dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade);
+    if (hipGetLastError() != hipSuccess) return -2;
+    // the frame's UNORM8 store from the linear colours (out_lin is never null here)
+    uint32_t tb = (args->n_pixels + rvcp::kToneBlock - 1) / rvcp::kToneBlock;
+    if (tb > 8192u) tb = 8192u;
+    hipLaunchKernelGGL(rvcp::tonemap_kernel, dim3(tb), dim3(rvcp::kToneBlock), 0, (hipStream_t)stream,
+                       out_lin, args->n_pixels, gamma_t, out_rgba);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
