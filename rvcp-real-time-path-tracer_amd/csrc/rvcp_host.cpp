@@ -736,11 +736,24 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                 A.timeline = ctx->d_timeline;
                 ctx->last_timeline_waves = waves;
             }
+            // the mode-2 and v3-family kernels leave linear colours and tonemap_kernel stores
+            // the bytes: into the caller's linear buffer, else the context's scratch
+            float *lin = (float *)d_linear_rgb;
+            if (!lin && (legacy || A.variant >= 3)) {
+                if (ctx->cap_acc < A.n_pixels) {
+                    (void)hipFree(ctx->d_acc);
+                    ctx->d_acc = nullptr;
+                    ctx->cap_acc = 0;
+                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_acc, (size_t)A.n_pixels * 12));
+                    ctx->cap_acc = A.n_pixels;
+                }
+                lin = ctx->d_acc;
+            }
             if (legacy) {
                 HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_legacy(&A, ctx->d_tri, ctx->d_shade, ctx->d_spheres,
                                         ctx->d_rawmats, ctx->d_unorm, (uint32_t *)d_rgba8,
-                                        (float *)d_linear_rgb, ctx->d_counters, blocks, s,
+                                        lin, ctx->d_counters, blocks, s,
                                         spec_legacy ? (void *)jk->legacy : nullptr);
                 if (spec_legacy) ctx->last_spec = true;
             } else if (A.variant >= 3) {
@@ -750,19 +763,6 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                     ctx->cap_surf = 0;
                     HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)A.n_pixels * sizeof(SurfRecord)));
                     ctx->cap_surf = A.n_pixels;
-                }
-                // these kernels leave linear colours and tonemap_kernel stores the bytes: into
-                // the caller's linear buffer, else the context's scratch
-                float *lin = (float *)d_linear_rgb;
-                if (!lin) {
-                    if (ctx->cap_acc < A.n_pixels) {
-                        (void)hipFree(ctx->d_acc);
-                        ctx->d_acc = nullptr;
-                        ctx->cap_acc = 0;
-                        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_acc, (size_t)A.n_pixels * 12));
-                        ctx->cap_acc = A.n_pixels;
-                    }
-                    lin = ctx->d_acc;
                 }
                 rc = rvcp_launch_games101_v3(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
                                              ctx->d_mats, ctx->d_lights, ctx->d_gamma,

@@ -2091,7 +2091,7 @@ __device__ __forceinline__ void legacy_body(
                 acc = add(acc, col);
                 k += 1;
                 if (k >= A.spp) {
-                    store_pixel(pix, divs_y(acc, sppf, inv_spp), A, unorm_t, out_rgba, out_lin);   // :819-821
+                    store_acc(pix, divs_y(acc, sppf, inv_spp), out_lin);   // :819-821
                     need_pixel = true;
                     st = L_IDLE;
                 } else {                                            // next sample, cached hit
@@ -2289,7 +2289,7 @@ __device__ __forceinline__ void legacy_body(
                     // miss / light: every sample returns this same color without touching the
                     // RNG; sum it SPP times in order (:816-818)
                     for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, col);
-                    store_pixel(pix, divs_y(acc, sppf, inv_spp), A, unorm_t, out_rgba, out_lin);
+                    store_acc(pix, divs_y(acc, sppf, inv_spp), out_lin);
                     need_pixel = true;
                     st = L_IDLE;
                 } else {
@@ -2500,13 +2500,20 @@ extern "C" int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRe
         rvcp::FrameArgs a = *args;
         void *params[] = {&a, &tri, &shade, &spheres, &materials, &unorm_t, &out_rgba, &out_lin,
                           &counters};
-        return hipModuleLaunchKernel((hipFunction_t)spec_legacy_fn, grid_blocks, 1, 1,
-                                     rvcp::kBlock, 1, 1, 0, (hipStream_t)stream, params,
-                                     nullptr) == hipSuccess ? 0 : -2;
+        if (hipModuleLaunchKernel((hipFunction_t)spec_legacy_fn, grid_blocks, 1, 1, rvcp::kBlock,
+                                  1, 1, 0, (hipStream_t)stream, params, nullptr) != hipSuccess)
+            return -2;
+    } else {
+        hipLaunchKernelGGL(rvcp::legacy_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
+                           (hipStream_t)stream, *args, tri, shade, (const rvcp_sphere_t *)spheres,
+                           (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters);
+        if (hipGetLastError() != hipSuccess) return -2;
     }
-    hipLaunchKernelGGL(rvcp::legacy_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
-                       (hipStream_t)stream, *args, tri, shade, (const rvcp_sphere_t *)spheres,
-                       (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters);
+    // the frame's UNORM8 store (no gamma in mode 2) from the linear colours
+    uint32_t tb = (args->n_pixels + rvcp::kToneBlock - 1) / rvcp::kToneBlock;
+    if (tb > 8192u) tb = 8192u;
+    hipLaunchKernelGGL(rvcp::tonemap_kernel, dim3(tb), dim3(rvcp::kToneBlock), 0, (hipStream_t)stream,
+                       out_lin, args->n_pixels, unorm_t, out_rgba);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
