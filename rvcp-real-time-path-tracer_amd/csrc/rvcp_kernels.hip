@@ -328,6 +328,12 @@ __device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, f
 // leaf costs one memory round trip instead of one per triangle.  The leaf-ordered triangles
 // are packed as 10 floats per slot (v0, e1, e2, face id bits; leaves start at even slots, so
 // 16-B aligned, rvcp_host.cpp): ceil(2.5 cnt) 16-B loads.
+#ifndef RVCP_BVH_SPEC
+#define RVCP_BVH_SPEC 1            // speculative while-while traversal (bvh_nearest)
+#endif
+#ifndef RVCP_BVH_SPEC_MIN
+#define RVCP_BVH_SPEC_MIN 64       // ... whose node phase ends once this many lanes hold a leaf
+#endif
 #ifndef RVCP_BVH_LEAF_CHUNK
 #define RVCP_BVH_LEAF_CHUNK 4      // triangles loaded together (one memory round trip; 2: 2 % slower)
 #endif
@@ -413,6 +419,79 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
     int32_t ref = root;
     const Bvh4QNode *__restrict__ qn = reinterpret_cast<const Bvh4QNode *>(nodes + n4);
     const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+#if RVCP_BVH_SPEC
+    // Speculative while-while: a lane that reaches a leaf parks it and keeps stepping through
+    // nodes until every lane holds a parked leaf (or cannot step), then the wave tests the
+    // parked leaves together -- node steps and leaf tests each run with most lanes active
+    // instead of the wave paying for both whenever its lanes are mixed.  Culling uses the bt
+    // of the tests done so far, which is never below the final one, so nothing is lost; the
+    // order rule makes the nearest hit independent of the order leaves are tested in.
+    bool alive = true, parked = false;
+    int32_t lref = 0;
+    for (;;) {
+        for (;;) {
+            if (alive && ref < 0 && !parked) {
+                parked = true;
+                lref = ref;
+                if (sp == 0) alive = false;
+                else { sp -= 1; ref = LDS ? stk[sp * kBlock] : priv[sp]; }
+            }
+            const bool step = alive && ref >= 0;
+#if RVCP_BVH_SPEC_MIN >= 64
+            if (!__any(step) || __all(parked || !alive)) break;
+#else
+            // (a leaf phase must have a parked leaf to test, or finished lanes alone could
+            // satisfy the count and the loop would never step again)
+            if (!__any(step) ||
+                (__any(parked) && __builtin_popcountll(__ballot(parked || !alive)) >= RVCP_BVH_SPEC_MIN))
+                break;
+#endif
+            if (step) {
+                const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
+                const float4 w0 = q[0], w1 = q[1], w2 = q[2];
+                const int4 r = reinterpret_cast<const int4 *>(qn + ref)[3];
+                const float ax = w0.w * inv.x, ay = w1.x * inv.y, az = w1.y * inv.z;
+                const float bx = (w0.x - o.x) * inv.x, by = (w0.y - o.y) * inv.y, bz = (w0.z - o.z) * inv.z;
+                const uint32_t lx = __float_as_uint(w1.z), ly = __float_as_uint(w1.w), lz = __float_as_uint(w2.x);
+                const uint32_t hx = __float_as_uint(w2.y), hy = __float_as_uint(w2.z), hz = __float_as_uint(w2.w);
+                const uint32_t nx = px ? lx : hx, fx = px ? hx : lx;
+                const uint32_t ny = py ? ly : hy, fy = py ? hy : ly;
+                const uint32_t nz = pz ? lz : hz, fz = pz ? hz : lz;
+                float kk[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float tn = __builtin_fmaxf(
+                        __builtin_fmaxf(__builtin_fmaf(ubyte_f(nx, c), ax, bx), __builtin_fmaf(ubyte_f(ny, c), ay, by)),
+                        __builtin_fmaxf(__builtin_fmaf(ubyte_f(nz, c), az, bz), tmin));
+                    const float tf = __builtin_fminf(
+                        __builtin_fminf(__builtin_fmaf(ubyte_f(fx, c), ax, bx), __builtin_fmaf(ubyte_f(fy, c), ay, by)),
+                        __builtin_fminf(__builtin_fmaf(ubyte_f(fz, c), az, bz), bt));
+                    kk[c] = tn <= tf ? tn : __builtin_inff();
+                }
+                float k0 = kk[0], k1 = kk[1], k2 = kk[2], k3 = kk[3];
+                int32_t c0 = r.x, c1 = r.y, c2 = r.z, c3 = r.w;
+                bvh4_cas(k0, c0, k1, c1);
+                bvh4_cas(k2, c2, k3, c3);
+                bvh4_cas(k0, c0, k2, c2);
+                bvh4_cas(k1, c1, k3, c3);
+                bvh4_cas(k1, c1, k2, c2);
+                const float inf = __builtin_inff();
+                if (k3 < inf) { if (LDS) stk[sp * kBlock] = c3; else priv[sp] = c3; sp += 1; }
+                if (k2 < inf) { if (LDS) stk[sp * kBlock] = c2; else priv[sp] = c2; sp += 1; }
+                if (k1 < inf) { if (LDS) stk[sp * kBlock] = c1; else priv[sp] = c1; sp += 1; }
+                if (k0 < inf) ref = c0;
+                else if (sp == 0) alive = false;
+                else { sp -= 1; ref = LDS ? stk[sp * kBlock] : priv[sp]; }
+            }
+        }
+        if (parked) {
+            bvh_leaf(btri, lref, o, d, tmin, bt, best, slots);
+            parked = false;
+        }
+        if (!__any(alive)) break;
+    }
+    return;
+#endif
     for (;;) {
         if (ref >= 0) {
             const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
