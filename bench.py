@@ -278,6 +278,10 @@ def main():
                          "N>1 rehearsals always use 1)")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
+    ap.add_argument("--schedule", type=int, default=0,
+                    help="rvcp_config_t.kernel_variant (0 = the library's automatic choice; with "
+                         "--accel bvh, 3 = the persistent BVH path kernel instead of the "
+                         "wavefront form)")
     ap.add_argument("--launch-pass", type=int, default=10,
                     help="frames (at most --steps) of the post-timing one-frame-in-flight pass "
                          "that measures the path kernel's isolated launch time "
@@ -327,6 +331,8 @@ def main():
         cfg_kw["integrator"] = 1
     if args.accel == "bvh":
         cfg_kw["accel"] = 1
+    if args.schedule:
+        cfg_kw["kernel_variant"] = args.schedule
     # Frames in flight: `fif` contexts render consecutive frames on their own
     # streams, so frame f+1's pre-pass and path kernel fill the CUs that frame f's tail leaves
     # idle -- the per-image fences of the reference's swapchain loop (vulkan.rs:367-369).  A

@@ -165,7 +165,9 @@ typedef struct rvcp_config {
      * 4 = 3 with the scan staged through LDS tiles shared by the workgroup, 5 = 4 with one ray
      * per lane per iteration (shadow ray, then path ray: no empty ray slots), 6 = 3 compiled
      * for 6 waves per SIMD, 10 = 4 with the workgroup's rays pooled in LDS and scanned in
-     * 64-ray passes (7, 8 and 9 are not schedules).  Every schedule produces bit-identical
+     * 64-ray passes (7 and 8 are not schedules; 9 only with RVCP_ACCEL_BVH: the BVH path in
+     * wavefront form, shade / trace kernel generations -- measured slower than the default
+     * persistent BVH path kernel, kept for A/B).  Every schedule produces bit-identical
      * frames. */
     int32_t kernel_variant;
     /* Acceleration structure: RVCP_ACCEL_NONE (default) scans every triangle like the
@@ -211,6 +213,7 @@ typedef struct rvcp_stats {
     uint32_t faces;                   /* F, triangles tested per traversal */
     int32_t kernel_variant;           /* the kernel schedule that ran (rvcp_config_t::
                                          kernel_variant resolved; 7 = BVH path kernel,
+                                         9 = BVH wavefront form,
                                          8 = RVCP_INTEGRATOR_LEGACY kernel, 0 = none), plus
                                          RVCP_VARIANT_SPECIALIZED when the scene-specialised
                                          path kernel ran */

@@ -81,6 +81,11 @@ struct rvcp_ctx {
     size_t cap_surf = 0;
     float *d_acc = nullptr;         // linear colours for tonemap_kernel when the caller wants none
     size_t cap_acc = 0;
+    // wavefront BVH path (rvcp_launch_bvh_wavefront): slot state, ray list, results, counters,
+    // trace stacks, the pinned read-back words and their events; allocated on the first BVH frame
+    WfBuffers wf{};
+    size_t cap_wf = 0;
+    int wf_trace_per_cu = 0;
 
     // staging for the synchronous host API
     uint32_t *d_rgba = nullptr;
@@ -303,7 +308,7 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         return fail(nullptr, RVCP_E_UNSUPPORTED, "unsupported integrator");
     if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
     if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant || cfg->kernel_variant == 7 ||
-        cfg->kernel_variant == 8 || cfg->kernel_variant == 9)
+        cfg->kernel_variant == 8 || (cfg->kernel_variant == 9 && cfg->accel != RVCP_ACCEL_BVH))
         return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
     if (cfg->n_gpus < 0 || cfg->n_gpus > 64)
         return fail(nullptr, RVCP_E_INVALID, "n_gpus must be in [0, 64]");
@@ -383,6 +388,9 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         if (rvcp_games101_occupancy(kOccupancyBvh, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
         if (cap > 0 && cap < per_cu) per_cu = cap;
         ctx->bvh_capacity = per_cu * cus;
+        per_cu = 0;
+        if (rvcp_wf_trace_occupancy(&per_cu) != 0 || per_cu <= 0) per_cu = 1;
+        ctx->wf_trace_per_cu = per_cu * cus;
     }
     if (cfg->n_gpus > 1) {   // one sub-context per further GPU (shards 1..N-1)
         for (int i = 1; i < cfg->n_gpus; i++) {
@@ -445,6 +453,14 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     (void)hipFree(ctx->d_lin);
     (void)hipFree(ctx->d_surf);
     (void)hipFree(ctx->d_acc);
+    (void)hipFree(ctx->wf.st);
+    (void)hipFree(ctx->wf.rays);
+    (void)hipFree(ctx->wf.res);
+    (void)hipFree(ctx->wf.counters);
+    (void)hipFree(ctx->wf.gstk);
+    if (ctx->wf.pinned) (void)hipHostFree(ctx->wf.pinned);
+    for (void *e : ctx->wf.ev)
+        if (e) (void)hipEventDestroy((hipEvent_t)e);
     (void)hipFree(ctx->d_timeline);
     (void)hipFree(ctx->d_pack_rgba);
     (void)hipFree(ctx->d_pack_lin);
@@ -612,6 +628,36 @@ uint32_t rvcp_shard_rows(uint32_t height, uint32_t shard_index, uint32_t shard_c
     return rows;
 }
 
+// Buffers of the wavefront BVH path for a frame of n pixels: min(n, kWfMaxSlots) path slots.
+static constexpr uint32_t kWfMaxSlots = 1u << 19;
+static int wf_reserve(rvcp_ctx_t *ctx, uint32_t n_pixels)
+{
+    const uint32_t N = n_pixels < kWfMaxSlots ? n_pixels : kWfMaxSlots;
+    WfBuffers &w = ctx->wf;
+    if (!w.counters) {
+        HIP_TRY(ctx, hipMalloc(&w.counters, kWfCountersBytes));
+        HIP_TRY(ctx, hipHostMalloc((void **)&w.pinned, 2 * sizeof(uint32_t), hipHostMallocDefault));
+        for (void *&e : w.ev) HIP_TRY(ctx, hipEventCreateWithFlags((hipEvent_t *)&e, hipEventDisableTiming));
+        w.trace_blocks = (uint32_t)ctx->wf_trace_per_cu;
+        HIP_TRY(ctx, hipMalloc((void **)&w.gstk, (size_t)w.trace_blocks * kWfTraceThreads *
+                                                     kWfStackGlobal * sizeof(int32_t)));
+    }
+    if (ctx->cap_wf < N) {
+        (void)hipFree(w.st);
+        (void)hipFree(w.rays);
+        (void)hipFree(w.res);
+        w.st = nullptr;
+        w.rays = w.res = nullptr;
+        ctx->cap_wf = 0;
+        HIP_TRY(ctx, hipMalloc((void **)&w.st, (size_t)N * kWfStateFields * sizeof(float)));
+        HIP_TRY(ctx, hipMalloc(&w.rays, (size_t)N * 64));      // two lists (generation parity)
+        HIP_TRY(ctx, hipMalloc(&w.res, (size_t)N * 8));
+        ctx->cap_wf = N;
+    }
+    w.n_slots = N;
+    return RVCP_OK;
+}
+
 static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
                             uint32_t height, uint32_t shard_index, uint32_t shard_count,
                             void *d_rgba8, void *d_linear_rgb, void *stream)
@@ -764,14 +810,26 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                     HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)A.n_pixels * sizeof(SurfRecord)));
                     ctx->cap_surf = A.n_pixels;
                 }
-                rc = rvcp_launch_games101_v3(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
-                                             ctx->d_mats, ctx->d_lights, ctx->d_gamma,
-                                             (uint32_t *)d_rgba8, lin,
-                                             ctx->d_counters, ctx->d_surf, ctx->d_shade,
-                                             ctx->d_bvh_nodes, ctx->d_bvh_tris,
-                                             blocks, s, ctx->evm,
-                                             spec ? (void *)(A.variant == 6 ? jk->path6 : jk->path5)
-                                                  : nullptr);
+                if (A.accel && ctx->cfg.kernel_variant == 9) {
+                    // the BVH path in wavefront form (shade / trace generations; measured
+                    // slower than the persistent BVH path kernel)
+                    if ((rc = wf_reserve(ctx, A.n_pixels)) != RVCP_OK) return rc;
+                    rc = rvcp_launch_bvh_wavefront(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
+                                                   ctx->d_mats, ctx->d_lights, ctx->d_gamma,
+                                                   (uint32_t *)d_rgba8, lin, ctx->d_counters,
+                                                   ctx->d_surf, ctx->d_shade, ctx->d_bvh_nodes,
+                                                   ctx->d_bvh_tris, s, ctx->evm, &ctx->wf);
+                    if (rc == -3) return fail(ctx, RVCP_E_HIP, "wavefront BVH frame did not finish");
+                } else {
+                    rc = rvcp_launch_games101_v3(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
+                                                 ctx->d_mats, ctx->d_lights, ctx->d_gamma,
+                                                 (uint32_t *)d_rgba8, lin,
+                                                 ctx->d_counters, ctx->d_surf, ctx->d_shade,
+                                                 ctx->d_bvh_nodes, ctx->d_bvh_tris,
+                                                 blocks, s, ctx->evm,
+                                                 spec ? (void *)(A.variant == 6 ? jk->path6 : jk->path5)
+                                                      : nullptr);
+                }
                 if (spec) ctx->last_spec = true;
             } else {
                 HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
@@ -788,7 +846,8 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
     ctx->pending = true;
     ctx->last_trivial = trivial;
-    ctx->last_variant = (trivial || A.n_pixels == 0) ? 0 : legacy ? 8 : A.accel ? 7 : A.variant;
+    ctx->last_variant = (trivial || A.n_pixels == 0) ? 0 : legacy ? 8
+                      : A.accel ? (ctx->cfg.kernel_variant == 9 ? 9 : 7) : A.variant;
     if (ctx->last_spec && ctx->last_variant != 0) ctx->last_variant |= RVCP_VARIANT_SPECIALIZED;
     ctx->last_pixels = A.n_pixels;
     ctx->last_spp = A.spp;

@@ -337,11 +337,11 @@ __device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, f
 #ifndef RVCP_BVH_LEAF_CHUNK
 #define RVCP_BVH_LEAF_CHUNK 4      // triangles loaded together (one memory round trip; 2: 2 % slower)
 #endif
+template <uint32_t kCh = RVCP_BVH_LEAF_CHUNK>
 __device__ __forceinline__ void bvh_leaf(const TriRecord *__restrict__ btri, int32_t ref, f3 o, f3 d,
                                          float tmin, float &bt, int &best, uint32_t slots = 0) {
     const uint32_t code = ~(uint32_t)ref;
     const uint32_t first = code >> 5, cnt = (code & 31u) + 1u;
-    constexpr uint32_t kCh = RVCP_BVH_LEAF_CHUNK;
     for (uint32_t c0 = 0; c0 < cnt; c0 += kCh) {
         const float4 *base = reinterpret_cast<const float4 *>(
             reinterpret_cast<const float *>(btri + slots) + 10u * (first + c0));
@@ -2043,6 +2043,400 @@ __global__ __launch_bounds__(kToneBlock) void tonemap_kernel(const float *__rest
         out_rgba[i] = pack_rgba(mk(lin[3 * (size_t)i], lin[3 * (size_t)i + 1], lin[3 * (size_t)i + 2]), T);
 }
 
+// ======================================================================================
+// Opt-in BVH, wavefront form.  The BVH path kernel above traverses one ray
+// per lane with the lane's whole path state live around the traversal: 4 waves per SIMD, and a
+// wave waits for the longest of its 64 traversals (PMC: 0.21 of the lanes active per VALU
+// instruction).  Here the same SINGLE ray machine is cut at the traversal:
+//   wf_shade_kernel -- one lane per path slot: resolve the ray the slot traced in the previous
+//       generation, run the settle step (end samples, take pixels from the pre-pass's surface
+//       list, surface events), append the slot's next ray to the generation's ray list and
+//       store the state (structure of arrays in HBM, WF_* fields);
+//   wf_trace_kernel -- persistent, few registers: every lane traverses a ray of the list and
+//       takes the next one as soon as it finishes (per-wave grabs of kWfGrab rays), so lanes do
+//       not idle behind the wave's longest traversal; a short LDS stack (kWfShort entries, the
+//       rest of the kBvhStack bound in global memory) leaves room for 8 waves per SIMD.
+// Each slot performs exactly the operations of path_body<false, true, true> on its pixels, in
+// the same order, and the traversal is bvh_nearest's (same nearest-hit rule), so frames are
+// the BVH path kernel's.  The host runs generations in batches and stops when no slot has work
+// left (wf_counters.alive), reading that count one batch behind so the GPU stays fed.
+// ======================================================================================
+struct WfCounters {
+    uint32_t n_rays[2];     // rays appended by the shade kernel of generation g (index g & 1)
+    uint32_t fetch[2];      // the trace kernel's next ray of generation g
+    uint32_t alive[2];      // slots with work left after the shade kernel of generation g
+    uint32_t pix_next;      // next entry of the surface list
+    uint32_t pad;
+};
+enum : uint32_t { WF_HASA = 1u, WF_HASB = 2u, WF_DONE = 4u, WF_PIX = 8u, WF_TRACED = 16u };
+enum : int {
+    WF_PSLOT = 0, WF_K, WF_DEPTH, WF_SEED, WF_RIDX, WF_ACC = 5, WF_ATT = 8, WF_COL = 11,
+    WF_FLAGS = 14, WF_RAYJ = 15, WF_AP = 16, WF_NEEC = 19, WF_NEED = 22, WF_BO = 23, WF_BD = 26,
+    WF_FIELDS = 29
+};
+constexpr uint32_t kWfShort = 16;           // LDS stack entries per trace lane
+constexpr uint32_t kWfTraceBlock = 256;
+constexpr uint32_t kWfGrab = 64;            // rays per wave grab
+#ifndef RVCP_WF_LEAF_CHUNK
+#define RVCP_WF_LEAF_CHUNK 2                // leaf triangles loaded together in the trace kernel
+#endif
+
+static_assert(sizeof(WfCounters) == kWfCountersBytes, "WfCounters layout (rvcp_internal.h)");
+static_assert(WF_FIELDS == (int)kWfStateFields, "slot state fields (rvcp_internal.h)");
+static_assert(kWfTraceBlock == kWfTraceThreads, "trace block (rvcp_internal.h)");
+static_assert(kBvhStack - (int)kWfShort == (int)kWfStackGlobal, "trace stack split (rvcp_internal.h)");
+
+__device__ __forceinline__ uint32_t wave_append(uint64_t M, uint32_t lane, uint32_t *ctr) {
+    // one atomic per wave: returns the base index of the wave's popc(M) appended entries
+    const int first = __builtin_ctzll(M);
+    uint32_t base = 0;
+    if ((int)lane == first) base = atomicAdd(ctr, (uint32_t)__builtin_popcountll(M));
+    return (uint32_t)__shfl((int)base, first);
+}
+
+__global__ __launch_bounds__(kBlock) void wf_shade_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, float *__restrict__ lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade, float *__restrict__ st, uint32_t N, uint32_t gen,
+    WfCounters *__restrict__ wc, float4 *__restrict__ rays, const float2 *__restrict__ res)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    const uint32_t par = gen & 1u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) wc->fetch[par] = 0u;
+    if (gen > 0 && *(volatile uint32_t *)&wc->alive[par ^ 1u] == 0u) return;   // frame finished
+    const uint32_t lane = lane_id();
+    const uint32_t wv = threadIdx.x / kWave;
+    const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
+    const bool live = slot < N;
+    const uint32_t n_surf = (uint32_t)(*(volatile unsigned long long *)&counters[3]);
+    const float sppf = (float)A.spp;
+    const float inv_spp = rcp_ieee(sppf);
+    float *const S = st + slot;                       // field f at S[f * N]
+    auto ldu = [&](int f) { return __float_as_uint(S[(size_t)f * N]); };
+    auto ld3f = [&](int f) { return mk(S[(size_t)f * N], S[(size_t)(f + 1) * N], S[(size_t)(f + 2) * N]); };
+    auto st3f = [&](int f, f3 v) { S[(size_t)f * N] = v.x; S[(size_t)(f + 1) * N] = v.y; S[(size_t)(f + 2) * N] = v.z; };
+
+    uint32_t flags = live ? ldu(WF_FLAGS) : WF_DONE;
+    bool done = (flags & WF_DONE) != 0u, have_pix = (flags & WF_PIX) != 0u;
+    bool hasA = (flags & WF_HASA) != 0u, hasB = (flags & WF_HASB) != 0u;
+    uint32_t pslot = 0, k = 0, depth = 0;
+    float seed = 0.0f, ridx = 0.0f, nee_dist = 0.0f;
+    f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
+    f3 a_o = mk(0, 0, 0), a_d = mk(0, 0, 1), a_p = mk(0, 0, 0), nee_C = mk(0, 0, 0);
+    f3 b_o = mk(0, 0, 0), b_d = mk(0, 0, 1);
+    if (have_pix) {
+        pslot = ldu(WF_PSLOT);
+        k = ldu(WF_K);
+        depth = ldu(WF_DEPTH);
+        seed = S[(size_t)WF_SEED * N];
+        ridx = S[(size_t)WF_RIDX * N];
+        acc = ld3f(WF_ACC);
+        att = ld3f(WF_ATT);
+        col = ld3f(WF_COL);
+        if (hasA) {
+            a_p = ld3f(WF_AP);
+            nee_C = ld3f(WF_NEEC);
+            nee_dist = S[(size_t)WF_NEED * N];
+        }
+        if (hasB) {
+            b_o = ld3f(WF_BO);
+            b_d = ld3f(WF_BD);
+        }
+    }
+    bool ended = false, surf_ev = false;
+    f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0), S_alb = mk(0, 0, 0);
+
+    // ---- the ray traced in the previous generation: resolve A (light sample) or B (bounce) ----
+    // the ray lists alternate by generation parity (this kernel appends to list `par` while
+    // it reads its slots' previous rays from list `par ^ 1`)
+    const float4 *__restrict__ prev_rays = rays + 2 * (size_t)N * (par ^ 1u);
+    float4 *__restrict__ next_rays = rays + 2 * (size_t)N * par;
+    if (flags & WF_TRACED) {
+        const uint32_t j = ldu(WF_RAYJ);
+        const float2 r = res[j];
+        const float bt = r.x;
+        const int best = __float_as_int(r.y);
+        if (hasA) {                                         // :447-459
+            const float4 ro = prev_rays[2 * j], rd = prev_rays[2 * j + 1];
+            a_o = mk(ro.x, ro.y, ro.z);
+            a_d = mk(rd.x, rd.y, rd.z);
+            const f3 hp = best >= 0 ? add(a_o, muls(a_d, bt))
+                                    : mk(__builtin_inff(), __builtin_inff(), __builtin_inff());
+            const float dist_blocked = len(sub(hp, a_p));
+            if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) col = add(col, nee_C);
+        }
+        const bool defer_B = hasA && hasB;                  // B was not traced
+        if (hasB && !defer_B) {                             // :421-429
+            if (best < 0) {
+                col = add(col, mk(0.1f, 0.1f, 0.1f));
+                ended = true;
+            } else {
+                f3 hpos, hn;
+                FaceShade fs;
+                hit_shade(tri, shade, best, b_o, b_d, bt, hpos, hn, fs);
+                if (fs.ty == kLight) {
+                    ended = true;
+                } else {
+                    S_pos = hpos; S_nrm = hn; S_alb = ld3(fs.alb_pi);
+                    surf_ev = true;
+                }
+            }
+        } else if (hasA && !hasB) {
+            ended = true;
+        }
+        hasA = false;
+        if (!defer_B) hasB = false;
+    }
+
+    // ---- settle: end samples, take pixels, emit surface events (path_body's) ----
+    for (;;) {
+        if (ended) {                                        // color += L / SPP (:495)
+            ended = false;
+            acc = add(acc, divs_y(col, sppf, inv_spp));
+            k += 1;
+            if (k >= A.spp) {
+                store_acc(surf[pslot].pix, acc, lin);
+                have_pix = false;
+            } else {
+                depth = 0;
+                att = mk(1, 1, 1);
+                col = mk(0, 0, 0);
+                const SurfRecord r = surf[pslot];
+                S_pos = ld3(r.pos); S_nrm = ld3(r.nrm); S_alb = ld3(r.alb_pi);
+                surf_ev = true;
+            }
+        }
+        {   // new pixels from the surface list
+            const bool need = live && !have_pix && !done;
+            const uint64_t M = __ballot(need);
+            if (M) {
+                const uint32_t base = wave_append(M, lane, &wc->pix_next);
+                if (need) {
+                    const uint32_t idx = base + rank_in(M);
+                    if (idx < n_surf) {
+                        const SurfRecord r = surf[idx];
+                        pslot = idx;
+                        seed = r.seed;
+                        ridx = 0.0f;
+                        k = 0;
+                        acc = mk(0, 0, 0);
+                        depth = 0;
+                        att = mk(1, 1, 1);
+                        col = mk(0, 0, 0);
+                        S_pos = ld3(r.pos); S_nrm = ld3(r.nrm); S_alb = ld3(r.alb_pi);
+                        have_pix = true;
+                        surf_ev = true;
+                    } else {
+                        done = true;
+                    }
+                }
+            }
+        }
+        bool need_dir = false;
+        if (surf_ev) {                                      // :431-462
+            surf_ev = false;
+            f3 ws;
+            if (nee_sample(A, lights, S_alb, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist, ws)) {
+                a_o = add(S_pos, muls(ws, A.eps));
+                a_d = ws;
+                a_p = S_pos;
+                hasA = true;
+            }
+            need_dir = !(rnd(seed, ridx) > A.rr);           // Russian roulette :462
+            if (!need_dir && !hasA) ended = true;
+        }
+        f3 p = mk(0, 0, 0);
+        coop_unit_sphere(need_dir, seed, ridx, p, lane, tail_tab[wv]);
+        if (need_dir) {                                     // :464-478
+            f3 wi;
+            brdf_finish(A, S_alb, S_nrm, p, att, wi);
+            depth += 1;
+            if (!(depth >= A.max_bounces || att_stop(A, att))) {
+                b_o = add(S_pos, muls(wi, A.eps));
+                b_d = wi;
+                hasB = true;
+            }
+            if (!hasA && !hasB) ended = true;
+        }
+        if (!__any(ended)) break;
+    }
+
+    // ---- this generation's ray: the light sample while pending, else the bounce ----
+    const bool sA = hasA || hasB;
+    const uint64_t M = __ballot(sA);
+    uint32_t j = 0;
+    if (M) {
+        const uint32_t base = wave_append(M, lane, &wc->n_rays[par]);
+        if (sA) {
+            j = base + rank_in(M);
+            const f3 o = hasA ? a_o : b_o, d = hasA ? a_d : b_d;
+            next_rays[2 * j] = make_float4(o.x, o.y, o.z, 0.0f);
+            next_rays[2 * j + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+        }
+        if (lane == 0) {
+            atomicAdd(&counters[0], (unsigned long long)__builtin_popcountll(M));
+            atomicAdd(&counters[2], 1ull);
+        }
+    }
+    const uint64_t L = __ballot(live && !done);
+    if (L) (void)wave_append(L, lane, &wc->alive[par]);
+    if (!live) return;
+    S[(size_t)WF_FLAGS * N] = __uint_as_float((hasA ? WF_HASA : 0u) | (hasB ? WF_HASB : 0u) |
+                                              (done ? WF_DONE : 0u) | (have_pix ? WF_PIX : 0u) |
+                                              (sA ? WF_TRACED : 0u));
+    if (!have_pix) return;
+    S[(size_t)WF_PSLOT * N] = __uint_as_float(pslot);
+    S[(size_t)WF_K * N] = __uint_as_float(k);
+    S[(size_t)WF_DEPTH * N] = __uint_as_float(depth);
+    S[(size_t)WF_SEED * N] = seed;
+    S[(size_t)WF_RIDX * N] = ridx;
+    S[(size_t)WF_RAYJ * N] = __uint_as_float(j);
+    st3f(WF_ACC, acc);
+    st3f(WF_ATT, att);
+    st3f(WF_COL, col);
+    if (hasA) {
+        st3f(WF_AP, a_p);
+        st3f(WF_NEEC, nee_C);
+        S[(size_t)WF_NEED * N] = nee_dist;
+    }
+    if (hasB) {
+        st3f(WF_BO, b_o);
+        st3f(WF_BD, b_d);
+    }
+}
+
+__global__ __launch_bounds__(kWfTraceBlock) void wf_trace_kernel(
+    const Bvh4Node *__restrict__ nodes, const TriRecord *__restrict__ btri, int32_t root,
+    uint32_t n4, uint32_t slots, const float4 *__restrict__ rays, float2 *__restrict__ res,
+    uint32_t gen, WfCounters *__restrict__ wc, float tmin, float tmax, int32_t *__restrict__ gstk)
+{
+    __shared__ int32_t stk[kWfShort * kWfTraceBlock];
+    const uint32_t par = gen & 1u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {     // the next generation's lists start empty
+        wc->n_rays[par ^ 1u] = 0u;
+        wc->alive[par ^ 1u] = 0u;
+    }
+    const uint32_t n = *(volatile uint32_t *)&wc->n_rays[par];
+    if (n == 0u) return;
+    const uint32_t lane = lane_id();
+    lds_i32 *const ls = (lds_i32 *)stk + threadIdx.x;            // ls[i * kWfTraceBlock]
+    int32_t *const gs = gstk + ((size_t)blockIdx.x * kWfTraceBlock + threadIdx.x) *
+                                   (uint32_t)(kBvhStack - (int)kWfShort);
+    const Bvh4QNode *__restrict__ qn = reinterpret_cast<const Bvh4QNode *>(nodes + n4);
+    uint32_t wnext = 0, wend = 0;      // this wave's grabbed range of the ray list (uniform)
+    bool wex = false;                  // the list is used up
+    bool has = false;
+    uint32_t j = 0;
+    f3 o = mk(0, 0, 0), d = mk(0, 0, 1), inv = mk(1, 1, 1);
+    bool px = true, py = true, pz = true;
+    int32_t ref = 0;
+    int sp = 0;
+    float bt = tmax;
+    int best = -1;
+    for (;;) {
+        const uint64_t M = __ballot(!has);
+        if (M && !wex) {
+            if (wnext >= wend) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(&wc->fetch[par], kWfGrab);
+                b = (uint32_t)__shfl((int)b, 0);
+                if (b >= n) {
+                    wex = true;
+                } else {
+                    wnext = b;
+                    wend = b + kWfGrab < n ? b + kWfGrab : n;
+                }
+            }
+            const uint32_t avail = wex ? 0u : wend - wnext;
+            if (!has) {
+                const uint32_t r = rank_in(M);
+                if (r < avail) {
+                    j = wnext + r;
+                    const float4 a = rays[2 * j], b = rays[2 * j + 1];
+                    o = mk(a.x, a.y, a.z);
+                    d = mk(b.x, b.y, b.z);
+                    inv = slab_inv(d);
+                    px = inv.x >= 0.0f; py = inv.y >= 0.0f; pz = inv.z >= 0.0f;
+                    ref = root;
+                    sp = 0;
+                    bt = tmax;
+                    best = -1;
+                    has = true;
+                }
+            }
+            const uint32_t took = (uint32_t)__builtin_popcountll(M);
+            wnext += took < avail ? took : avail;
+        }
+        if (!__any(has)) {
+            if (wex) break;
+            continue;
+        }
+        if (has) {
+            bool fin = false;
+            if (ref >= 0) {
+                const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
+                const float4 w0 = q[0], w1 = q[1], w2 = q[2];
+                const int4 r = reinterpret_cast<const int4 *>(qn + ref)[3];
+                const float ax = w0.w * inv.x, ay = w1.x * inv.y, az = w1.y * inv.z;
+                const float bx = (w0.x - o.x) * inv.x, by = (w0.y - o.y) * inv.y, bz = (w0.z - o.z) * inv.z;
+                const uint32_t lx = __float_as_uint(w1.z), ly = __float_as_uint(w1.w), lz = __float_as_uint(w2.x);
+                const uint32_t hx = __float_as_uint(w2.y), hy = __float_as_uint(w2.z), hz = __float_as_uint(w2.w);
+                const uint32_t nx = px ? lx : hx, fx = px ? hx : lx;
+                const uint32_t ny = py ? ly : hy, fy = py ? hy : ly;
+                const uint32_t nz = pz ? lz : hz, fz = pz ? hz : lz;
+                float kk[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float tn = __builtin_fmaxf(
+                        __builtin_fmaxf(__builtin_fmaf(ubyte_f(nx, c), ax, bx), __builtin_fmaf(ubyte_f(ny, c), ay, by)),
+                        __builtin_fmaxf(__builtin_fmaf(ubyte_f(nz, c), az, bz), tmin));
+                    const float tf = __builtin_fminf(
+                        __builtin_fminf(__builtin_fmaf(ubyte_f(fx, c), ax, bx), __builtin_fmaf(ubyte_f(fy, c), ay, by)),
+                        __builtin_fminf(__builtin_fmaf(ubyte_f(fz, c), az, bz), bt));
+                    kk[c] = tn <= tf ? tn : __builtin_inff();
+                }
+                float k0 = kk[0], k1 = kk[1], k2 = kk[2], k3 = kk[3];
+                int32_t c0 = r.x, c1 = r.y, c2 = r.z, c3 = r.w;
+                bvh4_cas(k0, c0, k1, c1);
+                bvh4_cas(k2, c2, k3, c3);
+                bvh4_cas(k0, c0, k2, c2);
+                bvh4_cas(k1, c1, k3, c3);
+                bvh4_cas(k1, c1, k2, c2);
+                const float inf = __builtin_inff();
+                auto push = [&](int32_t c) {
+                    if (sp < (int)kWfShort) ls[sp * kWfTraceBlock] = c;
+                    else gs[sp - (int)kWfShort] = c;
+                    sp += 1;
+                };
+                if (k3 < inf) push(c3);
+                if (k2 < inf) push(c2);
+                if (k1 < inf) push(c1);
+                if (k0 < inf) {
+                    ref = c0;
+                } else if (sp == 0) {
+                    fin = true;
+                } else {
+                    sp -= 1;
+                    ref = sp < (int)kWfShort ? ls[sp * kWfTraceBlock] : gs[sp - (int)kWfShort];
+                }
+            } else {
+                bvh_leaf<RVCP_WF_LEAF_CHUNK>(btri, ref, o, d, tmin, bt, best, slots);
+                if (sp == 0) {
+                    fin = true;
+                } else {
+                    sp -= 1;
+                    ref = sp < (int)kWfShort ? ls[sp * kWfTraceBlock] : gs[sp - (int)kWfShort];
+                }
+            }
+            if (fin) {
+                res[j] = make_float2(bt, __int_as_float(best));
+                has = false;
+            }
+        }
+    }
+}
+
 __global__ void fill_kernel(uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
                             uint32_t n, uint32_t rgba)
 {
@@ -2518,6 +2912,75 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
     hipLaunchKernelGGL(rvcp::tonemap_kernel, dim3(tb), dim3(rvcp::kToneBlock), 0, (hipStream_t)stream,
                        out_lin, args->n_pixels, gamma_t, out_rgba);
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// Opt-in BVH, wavefront form: pre-pass, then shade / trace generations until no slot has work
+// left, then the tone map.  Blocks the calling thread until the frame's last generation is
+// queued (the loop reads the live-slot count of a batch while the next batch runs).
+extern "C" int rvcp_launch_bvh_wavefront(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
+                                         const void *faces, const void *verts,
+                                         const rvcp::MatRecord *mats,
+                                         const rvcp::LightRecord *lights, const float *gamma_t,
+                                         uint32_t *out_rgba, float *out_lin,
+                                         unsigned long long *counters, rvcp::SurfRecord *surf,
+                                         const rvcp::FaceShade *shade,
+                                         const rvcp::Bvh4Node *bvh_nodes,
+                                         const rvcp::TriRecord *bvh_tris, void *stream,
+                                         void *main_event, const rvcp::WfBuffers *wb)
+{
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
+    hipLaunchKernelGGL(rvcp::games101_primary_kernel<true>, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
+                       s, *args, tri, (const rvcp_face_t *)faces, (const rvcp_vertex_t *)verts, mats,
+                       gamma_t, out_rgba, out_lin, counters, surf, shade, bvh_nodes, bvh_tris);
+    if (main_event && hipEventRecord((hipEvent_t)main_event, s) != hipSuccess) return -2;
+    const uint32_t N = wb->n_slots;
+    rvcp::WfCounters *wc = (rvcp::WfCounters *)wb->counters;
+    if (hipMemsetAsync(wc, 0, sizeof(rvcp::WfCounters), s) != hipSuccess) return -2;
+    if (hipMemsetAsync(wb->st + (size_t)rvcp::WF_FLAGS * N, 0, (size_t)N * 4, s) != hipSuccess) return -2;
+    const uint32_t shade_blocks = (N + rvcp::kBlock - 1) / rvcp::kBlock;
+    float4 *rays = (float4 *)wb->rays;
+    float2 *res = (float2 *)wb->res;
+    // generations: a slot spends at most 2 per bounce plus a few per sample, and takes pixels
+    // until the list is empty; the cap only stops a runaway loop
+    const uint64_t per_pixel = (uint64_t)args->spp * (2ull * args->max_bounces + 4ull) + 8ull;
+    const uint64_t cap = per_pixel * ((args->n_pixels + N - 1) / N + 1) + 64ull;
+    constexpr uint32_t kBatch = 8;
+    for (uint32_t g0 = 0, it = 0;; g0 += kBatch, ++it) {
+        for (uint32_t g = g0; g < g0 + kBatch; ++g) {
+            hipLaunchKernelGGL(rvcp::wf_shade_kernel, dim3(shade_blocks), dim3(rvcp::kBlock), 0, s,
+                               *args, tri, mats, lights, out_lin, counters, surf, shade, wb->st, N, g,
+                               wc, rays, (const float2 *)res);
+            hipLaunchKernelGGL(rvcp::wf_trace_kernel, dim3(wb->trace_blocks), dim3(rvcp::kWfTraceBlock), 0, s,
+                               bvh_nodes, bvh_tris, args->bvh_root, args->bvh_n4, args->bvh_slots,
+                               (const float4 *)(rays + 2 * (size_t)N * (g & 1u)), res, g, wc,
+                               args->t_min, args->t_max, wb->gstk);
+        }
+        if (hipGetLastError() != hipSuccess) return -2;
+        const uint32_t last = (g0 + kBatch - 1) & 1u;
+        if (hipMemcpyAsync(&wb->pinned[it & 1u], &wc->alive[last], 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipEventRecord((hipEvent_t)wb->ev[it & 1u], s) != hipSuccess)
+            return -2;
+        if (it > 0) {
+            if (hipEventSynchronize((hipEvent_t)wb->ev[(it - 1) & 1u]) != hipSuccess) return -2;
+            if (wb->pinned[(it - 1) & 1u] == 0u) break;
+        }
+        if (g0 > cap) return -3;
+    }
+    uint32_t tb = (args->n_pixels + rvcp::kToneBlock - 1) / rvcp::kToneBlock;
+    if (tb > 8192u) tb = 8192u;
+    hipLaunchKernelGGL(rvcp::tonemap_kernel, dim3(tb), dim3(rvcp::kToneBlock), 0, s,
+                       out_lin, args->n_pixels, gamma_t, out_rgba);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int rvcp_wf_trace_occupancy(int *blocks_per_cu)
+{
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::wf_trace_kernel, rvcp::kWfTraceBlock, 0) != hipSuccess)
+        return -2;
+    *blocks_per_cu = b;
+    return 0;
 }
 
 extern "C" void rvcp_static_split(uint32_t n, uint32_t grid_waves, uint32_t n_simds,

@@ -172,6 +172,10 @@ def test_create_rejects_bad_config_without_device():
     assert L.rvcp_create(abi.ptr(bad), ctypes.byref(h)) == abi.RVCP_E_UNSUPPORTED
     assert L.rvcp_create(None, ctypes.byref(h)) == abi.RVCP_E_INVALID
     assert L.rvcp_destroy(None) == 0
+    # 7 and 8 are not schedules; 9 (the BVH wavefront form) only with the BVH
+    for v, accel in ((7, 0), (8, 1), (9, 0), (11, 0), (-1, 0)):
+        bad = abi.make_config(kernel_variant=v, accel=accel)
+        assert L.rvcp_create(abi.ptr(bad), ctypes.byref(h)) == abi.RVCP_E_INVALID, (v, accel)
 
 
 def test_shard_rows_library_matches_python():

@@ -60,6 +60,8 @@ for s in $STEPS; do
         c5pmcw) run c5pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5pmcw_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
         c5sqpmc) run c5sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c5sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
         c5sqpmc2) run c5sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d "$OUT/c5sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
+        bvhsqpmc) run bvhsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/bvhsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
+        bvhsqpmc2) run bvhsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/bvhsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
         m2sqpmc) run m2sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/m2sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
         m2sqpmc2) run m2sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/m2sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
         spsqpmc) run spsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/spsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --frames-in-flight 1 ;;
