@@ -331,6 +331,15 @@ __device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, f
 #ifndef RVCP_BVH_SPEC
 #define RVCP_BVH_SPEC 1            // speculative while-while traversal (bvh_nearest)
 #endif
+// RVCP_BVH_POOL: the wave's A and B rays pooled over its lanes (bvh_pool): C5 BVH 138 -> 103
+// ms per frame; with two-triangle leaf loads and the traversal inlined (112 VGPRs, no
+// spills) 97.5 ms (profiles/r03zj_bvh_pool_ab.log, r03zk_bvh_pool_ab.log).
+#ifndef RVCP_BVH_POOL
+#define RVCP_BVH_POOL 1
+#endif
+#ifndef RVCP_BVH_POOL_INLINE
+#define RVCP_BVH_POOL_INLINE 1
+#endif
 #ifndef RVCP_BVH_SPEC_MIN
 #define RVCP_BVH_SPEC_MIN 64       // ... whose node phase ends once this many lanes hold a leaf
 #endif
@@ -533,6 +542,154 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
         if (sp == 0) break;
         sp -= 1;
         ref = LDS ? stk[sp * kBlock] : priv[sp];
+    }
+}
+
+// One 4-wide node step of a lane (the body of bvh_nearest's node branch): pushes the hit
+// children but the nearest, continues with the nearest or pops; `alive` drops when the stack
+// is empty.
+__device__ __forceinline__ void bvh4_step(const Bvh4QNode *__restrict__ qn, lds_i32 *stk, f3 o,
+                                          f3 inv, bool px, bool py, bool pz, float tmin, float bt,
+                                          int32_t &ref, int &sp, bool &alive) {
+    const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
+    const float4 w0 = q[0], w1 = q[1], w2 = q[2];
+    const int4 r = reinterpret_cast<const int4 *>(qn + ref)[3];
+    const float ax = w0.w * inv.x, ay = w1.x * inv.y, az = w1.y * inv.z;
+    const float bx = (w0.x - o.x) * inv.x, by = (w0.y - o.y) * inv.y, bz = (w0.z - o.z) * inv.z;
+    const uint32_t lx = __float_as_uint(w1.z), ly = __float_as_uint(w1.w), lz = __float_as_uint(w2.x);
+    const uint32_t hx = __float_as_uint(w2.y), hy = __float_as_uint(w2.z), hz = __float_as_uint(w2.w);
+    const uint32_t nx = px ? lx : hx, fx = px ? hx : lx;
+    const uint32_t ny = py ? ly : hy, fy = py ? hy : ly;
+    const uint32_t nz = pz ? lz : hz, fz = pz ? hz : lz;
+    float kk[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float tn = __builtin_fmaxf(
+            __builtin_fmaxf(__builtin_fmaf(ubyte_f(nx, c), ax, bx), __builtin_fmaf(ubyte_f(ny, c), ay, by)),
+            __builtin_fmaxf(__builtin_fmaf(ubyte_f(nz, c), az, bz), tmin));
+        const float tf = __builtin_fminf(
+            __builtin_fminf(__builtin_fmaf(ubyte_f(fx, c), ax, bx), __builtin_fmaf(ubyte_f(fy, c), ay, by)),
+            __builtin_fminf(__builtin_fmaf(ubyte_f(fz, c), az, bz), bt));
+        kk[c] = tn <= tf ? tn : __builtin_inff();
+    }
+    float k0 = kk[0], k1 = kk[1], k2 = kk[2], k3 = kk[3];
+    int32_t c0 = r.x, c1 = r.y, c2 = r.z, c3 = r.w;
+    bvh4_cas(k0, c0, k1, c1);
+    bvh4_cas(k2, c2, k3, c3);
+    bvh4_cas(k0, c0, k2, c2);
+    bvh4_cas(k1, c1, k3, c3);
+    bvh4_cas(k1, c1, k2, c2);
+    const float inf = __builtin_inff();
+    if (k3 < inf) { stk[sp * kBlock] = c3; sp += 1; }
+    if (k2 < inf) { stk[sp * kBlock] = c2; sp += 1; }
+    if (k1 < inf) { stk[sp * kBlock] = c1; sp += 1; }
+    if (k0 < inf) ref = c0;
+    else if (sp == 0) alive = false;
+    else { sp -= 1; ref = stk[sp * kBlock]; }
+}
+
+// Wave-pooled traversal (RVCP_BVH_POOL): the wave's shadow rays (lanes sA, in lane order) and
+// path rays (sB) form one list of up to 128 rays; every lane takes the next untaken ray as soon
+// as its current one is finished, with the speculative while-while steps of bvh_nearest, so a
+// wave's 64 lanes share its rays instead of each waiting for its own longest traversal.  A
+// ray's (o, d) is read from its owner lane's registers (ds_bpermute via the wave's LDS table of
+// owners, tab[128]), its (t, face) is left in res[128] and read back by the owner.  Same
+// traversal per ray, so the same nearest hits.
+#ifndef RVCP_BVH_POOL_CHUNK
+#define RVCP_BVH_POOL_CHUNK 2      // leaf triangles loaded together in bvh_pool
+#endif
+#if RVCP_BVH_POOL_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+void bvh_pool(const Bvh4Node *__restrict__ nodes,
+                                      const TriRecord *__restrict__ btri, int32_t root,
+                                      lds_i32 *stk, uint8_t *tab, float2 *res, uint32_t lane,
+                                      bool sA, bool sB, f3 a_o, f3 a_d, f3 b_o, f3 b_d,
+                                      float tmin, float tmax, float &btA, int &bestA, float &btB,
+                                      int &bestB, uint32_t n4, uint32_t slots) {
+    const uint64_t mA = __ballot(sA), mB = __ballot(sB);
+    const uint32_t nA = (uint32_t)__builtin_popcountll(mA);
+    const uint32_t nr = nA + (uint32_t)__builtin_popcountll(mB);
+    if (sA) tab[rank_in(mA)] = (uint8_t)lane;
+    if (sB) tab[nA + rank_in(mB)] = (uint8_t)lane;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const Bvh4QNode *__restrict__ qn = reinterpret_cast<const Bvh4QNode *>(nodes + n4);
+    uint32_t next = 0;                  // the list's next untaken ray (wave-uniform)
+    bool has = false, alive = false, parked = false;
+    uint32_t r = 0;
+    f3 o = mk(0, 0, 0), inv = mk(1, 1, 1), d = mk(0, 0, 1);
+    bool px = true, py = true, pz = true;
+    int32_t ref = 0, lref = 0;
+    int sp = 0;
+    float bt = tmax;
+    int best = -1;
+    for (;;) {
+        const uint64_t M = __ballot(!has);
+        if (M && next < nr) {
+            const uint32_t k = rank_in(M);
+            const bool take = !has && next + k < nr;
+            const uint32_t rr = next + k;
+            const int src = take ? (int)tab[rr] : (int)lane;
+            const f3 oa = mk(__shfl(a_o.x, src), __shfl(a_o.y, src), __shfl(a_o.z, src));
+            const f3 da = mk(__shfl(a_d.x, src), __shfl(a_d.y, src), __shfl(a_d.z, src));
+            const f3 ob = mk(__shfl(b_o.x, src), __shfl(b_o.y, src), __shfl(b_o.z, src));
+            const f3 db = mk(__shfl(b_d.x, src), __shfl(b_d.y, src), __shfl(b_d.z, src));
+            if (take) {
+                r = rr;
+                const bool isA = rr < nA;
+                o = isA ? oa : ob;
+                d = isA ? da : db;
+                inv = slab_inv(d);
+                px = inv.x >= 0.0f; py = inv.y >= 0.0f; pz = inv.z >= 0.0f;
+                ref = root;
+                sp = 0;
+                bt = tmax;
+                best = -1;
+                has = true;
+                alive = true;
+                parked = false;
+            }
+            const uint32_t pm = (uint32_t)__builtin_popcountll(M);
+            next += pm < nr - next ? pm : nr - next;
+        }
+        if (!__any(has)) break;
+        // node phase: step until every lane with a ray holds a parked leaf or is finished
+        for (;;) {
+            if (has && alive && ref < 0 && !parked) {
+                parked = true;
+                lref = ref;
+                if (sp == 0) alive = false;
+                else { sp -= 1; ref = stk[sp * kBlock]; }
+            }
+            const bool step = has && alive && ref >= 0;
+            if (!__any(step) || __all(!has || parked || !alive)) break;
+            if (step) bvh4_step(qn, stk, o, inv, px, py, pz, tmin, bt, ref, sp, alive);
+        }
+        if (parked) {
+            bvh_leaf<RVCP_BVH_POOL_CHUNK>(btri, lref, o, d, tmin, bt, best, slots);
+            parked = false;
+        }
+        if (has && !alive) {            // this ray is done: leave its result for the owner
+            res[r] = make_float2(bt, __int_as_float(best));
+            has = false;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (sA) {
+        const float2 v = res[rank_in(mA)];
+        btA = v.x;
+        bestA = __float_as_int(v.y);
+    }
+    if (sB) {
+        const float2 v = res[nA + rank_in(mB)];
+        btB = v.x;
+        bestB = __float_as_int(v.y);
     }
 }
 
@@ -1743,10 +1900,21 @@ __device__ __forceinline__ void path_body(
                 if (sB) { btB = tB_; bestB = iB_; }
             }
         } else if (BVH) {
-            // ---- opt-in BVH: each lane traverses for its own rays ----
+            // ---- opt-in BVH: each lane traverses for its own rays, or the wave's rays are
+            // pooled over its lanes (RVCP_BVH_POOL) ----
             lds_i32 *stk = (lds_i32 *)bvh_stack;
+#if RVCP_BVH_POOL
+            if (!SINGLE) {
+                float4 *pl = pool + wv * 72;            // res: 64 float4 (128 float2), tab: 8 float4
+                bvh_pool(bvh_nodes, bvh_tris, A.bvh_root, stk, reinterpret_cast<uint8_t *>(pl + 64),
+                         reinterpret_cast<float2 *>(pl), lane, sA, sB, s_ao, s_ad, b_o, b_d, A.t_min,
+                         A.t_max, btA, bestA, btB, bestB, A.bvh_n4, A.bvh_slots);
+            } else
+#endif
+            {
             if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA, A.bvh_n4, A.bvh_slots);
             if (sB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB, A.bvh_n4, A.bvh_slots);
+            }
         } else if (tail) {
             // ---- tail: R lanes per ray, each scanning every R-th triangle ----
             // The frame queue is empty, so what is left are the serial sample chains of the
@@ -1963,9 +2131,16 @@ __global__ __launch_bounds__(kBlock, 4) void games101_bvh_path_kernel(
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ int32_t bvh_stack[kBvhStack * kBlock];     // traversal stacks, column per thread
+#if RVCP_BVH_POOL
+    __shared__ float4 bvh_pool_lds[(kBlock / kWave) * 72];  // per wave: 128 results + 128-B owner table
+    path_body<false, true, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
+                           shade, tail_tab, nullptr, bvh_nodes, bvh_tris,
+                           bvh_stack + threadIdx.x, nullptr, nullptr, bvh_pool_lds);
+#else
     path_body<false, true, RVCP_BVH_SINGLE>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
                            shade, tail_tab, nullptr, bvh_nodes, bvh_tris,
                            bvh_stack + threadIdx.x);
+#endif
 }
 
 __global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_kernel(
