@@ -868,7 +868,9 @@ __device__ __forceinline__ void coop_unit_sphere(bool need, float seed, float &r
             }
             continue;
         }
-        const uint32_t lgK = 31u - (uint32_t)__builtin_clz((uint32_t)kWave / n);   // floor(log2(64/n))
+        // floor(log2(64 / n)) = 6 - ceil(log2 n) (64 / n >= 2^k <=> n <= 2^(6-k)), from the
+        // wave-uniform n without an integer division
+        const uint32_t lgK = 6u - (n > 1u ? 32u - (uint32_t)__builtin_clz(n - 1u) : 0u);
         const uint32_t K = 1u << lgK;
         const uint32_t r = rank_in(M);
         if (need) tab[r] = (uint8_t)lane;
