@@ -259,6 +259,40 @@ def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe=None):
     return "rccl", None
 
 
+def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues):
+    """Frames in flight and the path kernel's grid per frame (rvcp_config_t.grid_waves_per_simd,
+    0 = every resident slot) for a rank-frame of `pixels` pixels.
+
+    `fif` contexts render consecutive frames on their own streams, so frame f+1's pre-pass and
+    path kernel fill the CUs that frame f's tail leaves idle -- the per-image fences of the
+    reference's swapchain loop (vulkan.rs:367-369).  A context holds one frame at a time
+    (rvcp.h), so frame f waits, at its enqueue, for the frame its context rendered fif steps
+    earlier.  A pixel is a serial chain of SPP samples: a frame of P surface pixels on L
+    resident lanes ends in a tail once P/L is small (C3: ~2.6 pixels per lane, the N=8 share of
+    C4: ~1.3), and a smaller grid per frame with a third frame beside it lets the next frame's
+    waves start in that tail.  Measured (profiles/r03zp_grid_bench_ab.log, r03zp_grid_share.log):
+      - up to 1.5 Mpixel, brute-force scan of a small scene: 3 in flight on 3 waves per SIMD --
+        C3 3.35 -> 3.25 ms, mode 2 on the C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269
+        ms, the N=8 share of C4 3.80 -> 3.63 ms, the N=4 share 7.05 -> 6.92 ms;
+      - larger frames keep the full grid: C4 on one GPU 26.35 ms, 26.91 with 3 / 3;
+      - below 4 Msamples (C2): 4 in flight (C2 0.59/0.32/0.27/0.33 ms for 1/2/3/4 in flight,
+        profiles/r02_fif_sweep.log), the full grid (3 waves measured equal);
+      - otherwise 2 in flight, 3 in mode 2 (one kernel per frame, no pre-pass: C3 frame
+        2.84/2.40/2.29/2.46 ms for 1/2/3/4 in flight, profiles/r02_m2_fif_sweep.log).
+    Contexts beyond the hardware queues minus one contend for queues."""
+    if pixels * spp < (4 << 20):
+        fif, grid = 4, 0
+    elif small_scene and pixels <= 1536 * 1024:
+        fif, grid = 3, 3
+    else:
+        fif, grid = (3 if legacy else 2), 0
+    try:
+        fif = max(1, min(fif, int(hw_queues) - 1))
+    except ValueError:
+        pass
+    return fif, grid
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -273,15 +307,17 @@ def main():
     ap.add_argument("--save-frame", default="")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="contexts rendering consecutive frames concurrently (1 = one frame "
-                         "at a time; 0 = auto: 4 below 4 Msamples per rank-frame, 3 in "
-                         "integrator mode 2, else 2; "
-                         "N>1 rehearsals always use 1)")
+                         "at a time; 0 = auto, see auto_pipeline; N>1 rehearsals always use 1)")
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
     ap.add_argument("--schedule", type=int, default=0,
                     help="rvcp_config_t.kernel_variant (0 = the library's automatic choice; with "
                          "--accel bvh, 3 = the persistent BVH path kernel instead of the "
                          "wavefront form)")
+    ap.add_argument("--grid-waves", type=int, default=-1,
+                    help="rvcp_config_t.grid_waves_per_simd: the path kernel's persistent grid "
+                         "per frame in waves per SIMD (0 = every resident slot; -1 = auto, "
+                         "chosen with the frames in flight)")
     ap.add_argument("--launch-pass", type=int, default=10,
                     help="frames (at most --steps) of the post-timing one-frame-in-flight pass "
                          "that measures the path kernel's isolated launch time "
@@ -344,14 +380,12 @@ def main():
     # C3 frame 2.84/2.40/2.29/2.46 ms for 1/2/3/4 in flight, profiles/r02_m2_fif_sweep.log)
     # (small frames, 8 hardware queues: C2 4 in flight 0.269 ms vs 3 in flight 0.284 ms,
     # profiles/r02_hwq_fif_sweep.log; C3 2 and 3 equal)
-    rank_samples = W * spp * rvcp_amd.shard_rows(H, rank, world)
-    auto_fif = 4 if rank_samples < (4 << 20) else (3 if legacy else 2)
-    # contexts beyond the hardware queues minus one contend for queues
-    try:
-        auto_fif = max(1, min(auto_fif, int(hw_queues) - 1))
-    except ValueError:
-        pass
-    fif = 1 if rehearsal else (args.frames_in_flight or auto_fif)
+    small_scene = args.accel == "none" and not wl["extra_tris"]
+    fif_auto, grid_auto = auto_pipeline(W * rvcp_amd.shard_rows(H, rank, world), spp, legacy,
+                                        small_scene, hw_queues)
+    fif = 1 if rehearsal else (args.frames_in_flight or fif_auto)
+    grid_waves = args.grid_waves if args.grid_waves >= 0 else grid_auto
+    cfg_kw["grid_waves_per_simd"] = grid_waves
     rts = [rvcp_amd.RayTracer(**cfg_kw) for _ in range(fif)]
     t_up = time.perf_counter()
     rts[0].upload_scene(sc)              # includes the scene-specialised compile (§4.7)
@@ -523,29 +557,43 @@ def main():
     frame_check, one_gpu_ms = None, None
     if world > 1 and rank == 0:
         # the assembled N-rank frame must be bit-identical to a 1-rank render of the same frame
-        # (outside timing); the same frame rendered by this GPU alone, with the same frames in
-        # flight as the N-rank run, is the single-GPU reference for the speedup
-        singles = [torch.zeros((H, W), dtype=torch.int32, device=dev) for _ in range(fif)]
-        n1 = 3 * fif
-        for i in range(fif):                               # warm-up, one per context
-            rts[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
-        for i in range(fif):
-            rts[i].sync_stats()
+        # (outside timing); the same frame rendered by this GPU alone, pipelined the way a
+        # one-GPU run of that frame is (auto_pipeline for the whole frame, unless the command
+        # line fixed fif / grid for both), is the single-GPU reference for the speedup
+        fif1, grid1 = auto_pipeline(W * H, spp, legacy, small_scene, hw_queues)
+        fif1 = args.frames_in_flight or fif1
+        grid1 = args.grid_waves if args.grid_waves >= 0 else grid1
+        if (fif1, grid1) == (fif, grid_waves):
+            rts1, own1 = rts, False
+        else:
+            rts1 = [rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=grid1)) for _ in range(fif1)]
+            for r in rts1:
+                r.upload_scene(sc)
+            own1 = True
+        singles = [torch.zeros((H, W), dtype=torch.int32, device=dev) for _ in range(fif1)]
+        n1 = 3 * fif1
+        for i in range(fif1):                              # warm-up, one per context
+            rts1[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
+        for i in range(fif1):
+            rts1[i].sync_stats()
         torch.cuda.synchronize()
-        busy = [False] * fif
+        busy = [False] * fif1
         ts = time.perf_counter()
         for f in range(n1):
-            i = f % fif
+            i = f % fif1
             if busy[i]:
-                rts[i].sync_stats()
-            rts[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
+                rts1[i].sync_stats()
+            rts1[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
             busy[i] = True
-        for i in range(fif):
+        for i in range(fif1):
             if busy[i]:
-                rts[i].sync_stats()
+                rts1[i].sync_stats()
         torch.cuda.synchronize()
         one_gpu_ms = (time.perf_counter() - ts) * 1000.0 / n1
         frame_check = bool(torch.equal(singles[0], frame))
+        if own1:
+            for r in rts1:
+                r.close()
 
     per_rank = None
     if world > 1:
@@ -589,7 +637,7 @@ def main():
                        "scan": ("scene-specialised (hipRTC at upload, DESIGN.md §4.7)"
                                 if variant & rvcp_amd.abi.VARIANT_SPECIALIZED else "generic"),
                        "upload_s": round(upload_s, 3),
-                       "frames_in_flight": fif,
+                       "frames_in_flight": fif, "grid_waves_per_simd": grid_waves,
                        "gpu_max_hw_queues": hw_queues,
                        "gather": ("none" if world == 1 else
                                   "gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
@@ -643,7 +691,8 @@ def main():
         if frame_check is not None:
             out["config"]["assembled_frame_bitexact_vs_1gpu"] = frame_check
             out["config"]["one_gpu_ms"] = round(one_gpu_ms, 4)
-            out["config"]["one_gpu_frames_in_flight"] = fif
+            out["config"]["one_gpu_frames_in_flight"] = fif1
+            out["config"]["one_gpu_grid_waves_per_simd"] = grid1
             out["config"]["speedup_vs_one_gpu_same_frame"] = round(one_gpu_ms / ms_per_step, 3)
             if rehearsal:
                 out["config"]["physical_gpus"] = 1

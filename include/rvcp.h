@@ -199,7 +199,13 @@ typedef struct rvcp_config {
      * bit-identical to the generic kernels; without hipRTC the generic kernels run.
      * RVCP_SPECIALIZE_OFF (1): always the generic kernels. */
     int32_t specialize;
-    uint32_t _reserved[1];
+    /* Persistent grid of one frame's path kernel, in waves per SIMD: 0 (default) = every
+     * resident slot the kernel's occupancy allows; N > 0 caps it at N waves per SIMD (never
+     * above the occupancy).  A pixel is a serial chain of SPP samples, so a frame ends with a
+     * tail in which lanes whose pixels are done wait for the last chains; a caller that keeps
+     * F > 1 frames in flight on F contexts can leave room for the next frame's waves so that
+     * they start in that tail.  No effect on the frame's bits. */
+    uint32_t grid_waves_per_simd;
 } rvcp_config_t;
 
 /* Per-render statistics (all optional). */

@@ -20,7 +20,7 @@ CONFIG_DTYPE = np.dtype([("device", "<i4"), ("integrator", "<i4"), ("spp", "<u4"
                          ("ray_t_min", "<f4"), ("ray_t_max", "<f4"), ("rr_probability", "<f4"),
                          ("eps", "<f4"), ("lum_id_std140_quirk", "<i4"), ("kernel_variant", "<i4"),
                          ("accel", "<i4"), ("n_gpus", "<i4"), ("unorm_rule", "<i4"),
-                         ("specialize", "<i4"), ("_reserved", "<u4", 1)])
+                         ("specialize", "<i4"), ("grid_waves_per_simd", "<u4")])
 STATS_DTYPE = np.dtype([("kernel_ms", "<f8"), ("traversals", "<u8"),
                         ("traversals_executed", "<u8"), ("samples", "<u8"), ("faces", "<u4"),
                         ("kernel_variant", "<i4"), ("wave_iterations", "<u8"),
@@ -38,7 +38,8 @@ VARIANT_SPECIALIZED = 16
 # Defaults == the shader's #defines (ray_tracer_games101_branch.comp:5-13).
 DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop_eps=0.05,
                 ray_t_min=0.01, ray_t_max=10000.0, rr_probability=0.8, eps=0.001,
-                lum_id_std140_quirk=1, kernel_variant=0, accel=0, n_gpus=1, unorm_rule=0, specialize=0)
+                lum_id_std140_quirk=1, kernel_variant=0, accel=0, n_gpus=1, unorm_rule=0, specialize=0,
+                grid_waves_per_simd=0)
 
 # Error codes
 RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E_NOMEM, \
@@ -56,7 +57,8 @@ EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "r
 # Integrator mode 2 (ray_tracer.comp ray_trace): its own #defines (ray_tracer.comp:5-13).
 LEGACY_DEFAULTS = dict(device=0, integrator=1, spp=5, max_bounces=3, attenuation_stop_eps=0.01,
                        ray_t_min=0.01, ray_t_max=1000.0, rr_probability=1.0, eps=0.001,
-                       lum_id_std140_quirk=1, kernel_variant=0, accel=0, n_gpus=1, unorm_rule=0, specialize=0)
+                       lum_id_std140_quirk=1, kernel_variant=0, accel=0, n_gpus=1, unorm_rule=0, specialize=0,
+                       grid_waves_per_simd=0)
 INTEGRATOR_GAMES101, INTEGRATOR_LEGACY = 0, 1
 ACCEL_NONE, ACCEL_BVH = 0, 1
 UNORM_DRIVER, UNORM_NEAREST = 0, 1

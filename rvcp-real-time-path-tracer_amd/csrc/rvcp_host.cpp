@@ -746,6 +746,10 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             A.n_simds = ctx->n_simds;
             uint32_t waves = 0, chunk = 0;
             const uint32_t wpb = (uint32_t)((legacy || A.accel ? kBlock : variant_block(A.variant)) / kWave);
+            if (ctx->cfg.grid_waves_per_simd > 0) {     // the caller's grid per frame (rvcp.h)
+                const uint64_t lim = (uint64_t)ctx->cfg.grid_waves_per_simd * ctx->n_simds / wpb;
+                if (lim < cap) cap = lim > 0 ? (uint32_t)lim : 1u;
+            }
             rvcp_static_split(A.n_pixels, cap * wpb, A.n_simds, &waves, &chunk);
             uint32_t blocks = (waves + wpb - 1) / wpb;
             if (blocks > cap) blocks = cap;

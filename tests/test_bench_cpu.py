@@ -31,6 +31,25 @@ def test_workloads_match_baseline_configs():
         bench.workload("nope", 1)
 
 
+def test_auto_pipeline():
+    """Frames in flight and the grid per frame: small frames 4 in flight on
+    the full grid, up to 1.5 Mpixel of a small scene 3 in flight on 3 waves per SIMD (C3, the
+    N=4 / N=8 shares of C4, the sphere room), larger frames the full grid; never more contexts
+    than the hardware queues minus one."""
+    ap = bench.auto_pipeline
+    assert ap(384 * 384, 10, False, True, "8") == (4, 0)                 # C2
+    assert ap(384 * 384, 10, False, True, "4") == (3, 0)                 # the box's 4 queues
+    assert ap(1024 * 1024, 30, False, True, "4") == (3, 3)               # C3
+    assert ap(1024 * 1024, 30, True, True, "4") == (3, 3)                # mode 2 on the C3 frame
+    assert ap(1024 * 1024, 5, True, True, "4") == (3, 3)                 # sphere room
+    assert ap(2048 * 256, 64, False, True, "4") == (3, 3)                # C4, N=8 share
+    assert ap(2048 * 1024, 64, False, True, "4") == (2, 0)               # C4, N=2 share
+    assert ap(2048 * 2048, 64, False, True, "4") == (2, 0)               # C4, one GPU
+    assert ap(1024 * 1024, 30, False, False, "4") == (2, 0)              # C5 (mesh / BVH)
+    assert ap(1024 * 1024, 30, False, True, "2") == (1, 3)
+    assert ap(1024 * 1024, 30, False, True, "x") == (3, 3)
+
+
 def test_roofline_constants():
     assert bench.FLOP_PER_TEST == 52 and bench.FP32_PEAK_TFLOPS == 157.3
     assert bench.REFERENCE_MSAMPLES["c3"] == pytest.approx(1024 * 1024 * 30 * 3 / 1e6, rel=0.01)

@@ -201,3 +201,20 @@ def test_stats_report_schedule(cornell):
         rt.render(64, 64, TIME)
         v = int(rt.last_stats["kernel_variant"])
         assert v == 8 | spec and rvcp_amd.abi.KERNEL_NAMES[v] == "rvcp_spec_legacy_kernel"
+
+
+@pytest.mark.parametrize("integrator,spp", [(0, 6), (1, 3)])
+def test_grid_waves_per_simd_keeps_the_frame(cornell, integrator, spp):
+    """rvcp_config_t.grid_waves_per_simd only sizes the persistent grid of a frame's path
+    kernel (1 wave per SIMD, the 3 bench.py uses for C3-sized frames, more than the occupancy):
+    every frame and the traversal count equal the full-grid render, in both integrators."""
+    W, H = 320, 200
+    outs = []
+    for g in (0, 1, 3, 64):
+        with rvcp_amd.RayTracer(spp=spp, integrator=integrator, grid_waves_per_simd=g) as rt:
+            rt.upload_scene(cornell)
+            img = rt.render(W, H, TIME)
+            outs.append((img, int(rt.last_stats["traversals"])))
+    for img, trav in outs[1:]:
+        assert np.array_equal(img, outs[0][0])
+        assert trav == outs[0][1]

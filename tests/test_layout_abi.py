@@ -31,7 +31,7 @@ int main(void) {
   S(rvcp_config_t); F(rvcp_config_t, spp); F(rvcp_config_t, max_bounces);
   F(rvcp_config_t, attenuation_stop_eps); F(rvcp_config_t, ray_t_min); F(rvcp_config_t, ray_t_max);
   F(rvcp_config_t, rr_probability); F(rvcp_config_t, eps); F(rvcp_config_t, lum_id_std140_quirk);
-  F(rvcp_config_t, kernel_variant); F(rvcp_config_t, accel); F(rvcp_config_t, n_gpus); F(rvcp_config_t, unorm_rule); F(rvcp_config_t, specialize);
+  F(rvcp_config_t, kernel_variant); F(rvcp_config_t, accel); F(rvcp_config_t, n_gpus); F(rvcp_config_t, unorm_rule); F(rvcp_config_t, specialize); F(rvcp_config_t, grid_waves_per_simd);
   S(rvcp_stats_t); F(rvcp_stats_t, kernel_ms); F(rvcp_stats_t, traversals);
   F(rvcp_stats_t, traversals_executed); F(rvcp_stats_t, samples); F(rvcp_stats_t, faces);
   F(rvcp_stats_t, wave_iterations); F(rvcp_stats_t, main_kernel_ms);
