@@ -384,7 +384,8 @@ def main():
     fif_auto, grid_auto = auto_pipeline(W * rvcp_amd.shard_rows(H, rank, world), spp, legacy,
                                         small_scene, hw_queues)
     fif = 1 if rehearsal else (args.frames_in_flight or fif_auto)
-    grid_waves = args.grid_waves if args.grid_waves >= 0 else grid_auto
+    # (the smaller grid leaves room for frames beside it: with fewer in flight, the full grid)
+    grid_waves = args.grid_waves if args.grid_waves >= 0 else (grid_auto if fif >= 3 else 0)
     cfg_kw["grid_waves_per_simd"] = grid_waves
     rts = [rvcp_amd.RayTracer(**cfg_kw) for _ in range(fif)]
     t_up = time.perf_counter()
@@ -522,13 +523,20 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
 
     # Isolated launch time (after the timed region): the path kernel with ONE frame in flight,
-    # so its HIP-event time is its own (roofline.per_launch).
+    # so its HIP-event time is its own (roofline.per_launch), on the full resident grid -- the
+    # launch a one-frame-at-a-time caller makes (a grid left partly free for the next frame,
+    # grid_waves_per_simd, only pays off with frames beside it)
     iso_ms = []
     if args.launch_pass > 0:
+        rt_iso = rt if grid_waves == 0 else rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0))
+        if rt_iso is not rt:
+            rt_iso.upload_scene(sc)
         for _ in range(max(1, min(args.launch_pass, args.steps))):
-            rt.render_shard_async(push, W, H, rank, world,
-                                  (frames[0] if world == 1 else shard_bufs[0]).data_ptr())
-            iso_ms.append(float(rt.sync_stats()["main_kernel_ms"]))
+            rt_iso.render_shard_async(push, W, H, rank, world,
+                                      (frames[0] if world == 1 else shard_bufs[0]).data_ptr())
+            iso_ms.append(float(rt_iso.sync_stats()["main_kernel_ms"]))
+        if rt_iso is not rt:
+            rt_iso.close()
 
     # roofline of the dominant kernel (this rank's launches).  The pre-pass (schedules 3-6,
     # games101 only) traces each pixel's primary ray once; every other reference-algorithm
@@ -562,7 +570,7 @@ def main():
         # line fixed fif / grid for both), is the single-GPU reference for the speedup
         fif1, grid1 = auto_pipeline(W * H, spp, legacy, small_scene, hw_queues)
         fif1 = args.frames_in_flight or fif1
-        grid1 = args.grid_waves if args.grid_waves >= 0 else grid1
+        grid1 = args.grid_waves if args.grid_waves >= 0 else (grid1 if fif1 >= 3 else 0)
         if (fif1, grid1) == (fif, grid_waves):
             rts1, own1 = rts, False
         else:
@@ -662,8 +670,10 @@ def main():
                              "achieved": round(flop_per_launch / iso_s / 1e12, 2),
                              "frac": round(flop_per_launch / iso_s / 1e12 / FP32_PEAK_TFLOPS, 4),
                              "frames": len(iso_ms),
+                             "grid_waves_per_simd": 0,
                              "definition": "useful FLOP / the path kernel's HIP-event time with "
-                                           "one frame in flight (post-timing pass)"},
+                                           "one frame in flight on the full resident grid "
+                                           "(post-timing pass)"},
                          "kernel": kname,
                          "kernel_ms_in_flight": round(avg_kernel_s * 1000.0, 4),
                          "frame_kernels_ms_in_flight": round(avg_frame_s * 1000.0, 4),

@@ -18,12 +18,22 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_line_c2(tmp_path):
+def bench_auto(pixels, spp, hwq):
+    sys.path.insert(0, ROOT)
+    import bench
+    fif, grid = bench.auto_pipeline(pixels, spp, False, True, hwq)
+    return fif, (grid if fif >= 3 else 0)
+
+
+@pytest.mark.parametrize("workload,side,spp,steps", [("c2", 384, 10, 6), ("c3", 1024, 30, 4)])
+def test_bench_line(tmp_path, workload, side, spp, steps):
+    """C2 (4 frames in flight or the hardware queues' limit, full grid) and C3 (3 in flight
+    on 3 waves per SIMD, bench.auto_pipeline)."""
     frame_path = tmp_path / "frame.npy"
     env = dict(os.environ)
     env.pop("RVCP_LIB", None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c2",
-                        "--steps", "6", "--warmup", "2", "--no-cpu-baseline",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload,
+                        "--steps", str(steps), "--warmup", "2", "--no-cpu-baseline",
                         "--save-frame", str(frame_path)],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -33,8 +43,10 @@ def test_bench_line_c2(tmp_path):
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
               "roofline", "cpu_baseline"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == 6 and d["warmup"] == 2
-    W, H, spp = 384, 384, 10
+    assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == 2
+    W = H = side
+    fif, grid = d["config"]["frames_in_flight"], d["config"]["grid_waves_per_simd"]
+    assert (fif, grid) == bench_auto(W * H, spp, d["config"]["gpu_max_hw_queues"])
     assert d["value"] == pytest.approx(W * H * spp / (d["ms_per_step"] / 1000.0) / 1e6, rel=2e-3)
     rl = d["roofline"]
     assert rl["bound"] == "valu" and rl["peak"] == 157.3
@@ -48,7 +60,7 @@ def test_bench_line_c2(tmp_path):
     frame = np.load(frame_path)
     sc = rvcp_amd.Scene.default()
     cfg = rvcp_amd.abi.make_config(spp=spp)
-    for y in (0, 131, 200, 383):
+    for y in (0, 131, 200, H - 1):
         _, o_rgba, _ = O.render(scene_arrays(sc), sc.push_constant(123.0), cfg, W, H,
                                 rect=(0, y, W, 1), want_linear=False)
         assert np.array_equal(frame[y:y + 1], o_rgba), y

@@ -38,6 +38,8 @@ for s in $STEPS; do
         tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
         parity) run pytest_parity 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_specialize.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         bvh) run pytest_bvh 600 python -u -m pytest tests/test_gpu_bvh.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread -k "bvh or BVH" ;;
+        benchtest) run pytest_bench 600 python -u -m pytest tests/test_gpu_bench.py -m gpu -x -v --timeout 280 --timeout-method thread ;;
+        rankshare) run rank_share 300 python -u tools/rank_share.py ;;
         abi) run pytest_abi 300 python -u -m pytest tests/test_gpu_abi.py tests/test_gpu_specialize.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         bench) run bench_c3 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) run bench_c3q 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline ;;
