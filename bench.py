@@ -259,7 +259,7 @@ def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe=None):
     return "rccl", None
 
 
-def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues):
+def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none"):
     """Frames in flight and the path kernel's grid per frame (rvcp_config_t.grid_waves_per_simd,
     0 = every resident slot) for a rank-frame of `pixels` pixels.
 
@@ -290,7 +290,8 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues):
         fif = max(1, min(fif, int(hw_queues) - 1))
     except ValueError:
         pass
-    return fif, grid
+    batch = 1
+    return fif, grid, batch
 
 
 def main():
@@ -314,6 +315,9 @@ def main():
                     help="rvcp_config_t.kernel_variant (0 = the library's automatic choice; with "
                          "--accel bvh, 3 = the persistent BVH path kernel instead of the "
                          "wavefront form)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per path kernel (rvcp_render_frames_async; 1 = one frame per "
+                         "rvcp_render_shard_async call; 0 = auto, see auto_pipeline)")
     ap.add_argument("--grid-waves", type=int, default=-1,
                     help="rvcp_config_t.grid_waves_per_simd: the path kernel's persistent grid "
                          "per frame in waves per SIMD (0 = every resident slot; -1 = auto, "
@@ -381,9 +385,10 @@ def main():
     # (small frames, 8 hardware queues: C2 4 in flight 0.269 ms vs 3 in flight 0.284 ms,
     # profiles/r02_hwq_fif_sweep.log; C3 2 and 3 equal)
     small_scene = args.accel == "none" and not wl["extra_tris"]
-    fif_auto, grid_auto = auto_pipeline(W * rvcp_amd.shard_rows(H, rank, world), spp, legacy,
-                                        small_scene, hw_queues)
+    fif_auto, grid_auto, batch_auto = auto_pipeline(W * rvcp_amd.shard_rows(H, rank, world), spp,
+                                                    legacy, small_scene, hw_queues, args.accel)
     fif = 1 if rehearsal else (args.frames_in_flight or fif_auto)
+    batch = 1 if rehearsal else (args.batch or batch_auto)
     # (the smaller grid leaves room for frames beside it: with fewer in flight, the full grid)
     grid_waves = args.grid_waves if args.grid_waves >= 0 else (grid_auto if fif >= 3 else 0)
     cfg_kw["grid_waves_per_simd"] = grid_waves
@@ -401,8 +406,10 @@ def main():
     rows = rvcp_amd.shard_rows(H, rank, world)
     slot = rvcp_amd.shard_rows(H, 0, world)          # shard 0 has the most rows
     dev = torch.device("cuda", local_rank)
-    shard_bufs = [torch.zeros((slot, W), dtype=torch.int32, device=dev) for _ in range(fif)]
-    frames = [torch.zeros((H, W), dtype=torch.int32, device=dev) if rank == 0 else None
+    # frame k of a context's batch at [k] (rvcp_render_frames_async's layout: shard slots of the
+    # largest shard's rows)
+    shard_bufs = [torch.zeros((batch, slot, W), dtype=torch.int32, device=dev) for _ in range(fif)]
+    frames = [torch.zeros((batch, H, W), dtype=torch.int32, device=dev) if rank == 0 else None
               for _ in range(fif)]
     gat_flats = [torch.zeros((world, slot, W), dtype=torch.int32, device=dev)
                  if (world > 1 and rank == 0) else None for _ in range(fif)]
@@ -440,51 +447,60 @@ def main():
             lambda i, uid: rts[i].rccl_init(uid, world, rank), probe)
     host_gather = world > 1 and gather_mode != "rccl"
     torch.cuda.synchronize()
-    pending = [False] * fif
+    pending = [0] * fif                 # frames in flight on each context
     gather_ms = []
 
-    def enqueue(i):
-        """Enqueue one frame on context i's own stream (stream 0 = the context's stream)."""
-        r, frame, shard_buf, gat_flat = rts[i], frames[i], shard_bufs[i], gat_flats[i]
-        if world == 1:
-            r.render_shard_async(push, W, H, 0, 1, frame.data_ptr())
+    def enqueue(i, nb):
+        """Enqueue nb frames (one call) on context i's own stream (stream 0 = its stream)."""
+        r, shard_buf, gat_flat = rts[i], shard_bufs[i], gat_flats[i]
+        out = frames[i] if world == 1 else shard_buf
+        k, n = (0, 1) if world == 1 else (rank, world)
+        if batch == 1:
+            r.render_shard_async(push, W, H, k, n, out.data_ptr())
+        else:
+            r.render_frames_async([push] * nb, W, H, k, n, out.data_ptr())
+        if world == 1 or host_gather:
             return
-        r.render_shard_async(push, W, H, rank, world, shard_buf.data_ptr())
-        if host_gather:
-            return
-        # RCCL gather + device assembly, enqueued behind the render without a host sync
-        r.gather_frame_async(shard_buf.data_ptr(), W, H,
-                             gat_flat.data_ptr() if rank == 0 else 0,
-                             frame.data_ptr() if rank == 0 else 0)
+        # RCCL gather + device assembly of each frame, enqueued behind the render without a
+        # host sync (the gathers of a batch reuse gat_flat in stream order)
+        for j in range(nb):
+            r.gather_frame_async(shard_buf[j].data_ptr(), W, H,
+                                 gat_flat.data_ptr() if rank == 0 else 0,
+                                 frames[i][j].data_ptr() if rank == 0 else 0)
 
     def finish(i):
-        """Wait for context i's frame; return its stats."""
+        """Wait for context i's frames; return their stats (one entry per call)."""
         st = rts[i].sync_stats()
-        pending[i] = False
+        nb, pending[i] = pending[i], 0
         if world > 1 and not host_gather:
             gather_ms.append(rts[i].gather_wait()[0])
         if host_gather:    # gloo gather through host memory (rehearsal / no usable RCCL)
-            got = rvcp_amd.frame.gather_shards(shard_bufs[i].cpu(), rank, world, dst=0)
-            if rank == 0:
-                gat_flats[i].copy_(torch.stack(got))
-                rts[i].assemble_frame_async(gat_flats[i].data_ptr(), slot, W, H, world,
-                                            frames[i].data_ptr())
-                torch.cuda.synchronize()
+            for j in range(nb):
+                got = rvcp_amd.frame.gather_shards(shard_bufs[i][j].cpu(), rank, world, dst=0)
+                if rank == 0:
+                    gat_flats[i].copy_(torch.stack(got))
+                    rts[i].assemble_frame_async(gat_flats[i].data_ptr(), slot, W, H, world,
+                                                frames[i][j].data_ptr())
+                    torch.cuda.synchronize()
         return st
 
-    def step(f):
-        """Frame f: returns the stats of the frame it waited for (or None)."""
-        i = f % fif
+    def step(c, nb):
+        """Call c (nb frames): returns the stats of the call it waited for (or None)."""
+        i = c % fif
         st = finish(i) if pending[i] else None
-        enqueue(i)
-        pending[i] = True
+        enqueue(i, nb)
+        pending[i] = nb
         return st
 
     def drain():
         return [finish(i) for i in range(fif) if pending[i]]
 
-    for f in range(args.warmup):
-        step(f)
+    def calls(n):
+        """n frames as calls of `batch` frames (the last one shorter)."""
+        return [batch] * (n // batch) + ([n % batch] if n % batch else [])
+
+    for c, nb in enumerate(calls(args.warmup)):
+        step(c, nb)
     drain()
     gather_ms.clear()
     torch.cuda.synchronize()
@@ -494,14 +510,14 @@ def main():
     stats = []
     t0 = time.perf_counter()
     step_ms = []
-    for f in range(args.steps):
+    for c, nb in enumerate(calls(args.steps)):
         ts = time.perf_counter()
-        st = step(f)
-        step_ms.append((time.perf_counter() - ts) * 1000.0)
+        st = step(c, nb)
+        step_ms.append((time.perf_counter() - ts) * 1000.0 / nb)
         if st is not None:
             stats.append(st)
     stats += drain()
-    frame = frames[0]
+    frame = frames[0][0] if rank == 0 else None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -512,7 +528,7 @@ def main():
     trav = sum(int(st["traversals"]) for st in stats)
     trav_exec = sum(int(st["traversals_executed"]) for st in stats)
     variant = int(stats[-1]["kernel_variant"])
-    assert len(stats) == args.steps
+    assert sum(int(st["samples"]) for st in stats) == args.steps * W * rows * spp
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -526,15 +542,17 @@ def main():
     # so its HIP-event time is its own (roofline.per_launch), on the full resident grid -- the
     # launch a one-frame-at-a-time caller makes (a grid left partly free for the next frame,
     # grid_waves_per_simd, only pays off with frames beside it)
-    iso_ms = []
+    iso_ms, latency_ms = [], []
     if args.launch_pass > 0:
         rt_iso = rt if grid_waves == 0 else rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0))
         if rt_iso is not rt:
             rt_iso.upload_scene(sc)
         for _ in range(max(1, min(args.launch_pass, args.steps))):
+            tl = time.perf_counter()
             rt_iso.render_shard_async(push, W, H, rank, world,
                                       (frames[0] if world == 1 else shard_bufs[0]).data_ptr())
             iso_ms.append(float(rt_iso.sync_stats()["main_kernel_ms"]))
+            latency_ms.append((time.perf_counter() - tl) * 1000.0)
         if rt_iso is not rt:
             rt_iso.close()
 
@@ -568,7 +586,7 @@ def main():
         # (outside timing); the same frame rendered by this GPU alone, pipelined the way a
         # one-GPU run of that frame is (auto_pipeline for the whole frame, unless the command
         # line fixed fif / grid for both), is the single-GPU reference for the speedup
-        fif1, grid1 = auto_pipeline(W * H, spp, legacy, small_scene, hw_queues)
+        fif1, grid1, _ = auto_pipeline(W * H, spp, legacy, small_scene, hw_queues, args.accel)
         fif1 = args.frames_in_flight or fif1
         grid1 = args.grid_waves if args.grid_waves >= 0 else (grid1 if fif1 >= 3 else 0)
         if (fif1, grid1) == (fif, grid_waves):
@@ -646,6 +664,11 @@ def main():
                                 if variant & rvcp_amd.abi.VARIANT_SPECIALIZED else "generic"),
                        "upload_s": round(upload_s, 3),
                        "frames_in_flight": fif, "grid_waves_per_simd": grid_waves,
+                       "frames_per_launch": batch,
+                       # one frame alone, enqueue to completion (the latency of a synchronous
+                       # rvcp_render of this rank's frame; ms_per_step is the pipelined rate)
+                       "frame_latency_ms_alone": (round(float(np.median(latency_ms)), 4)
+                                                  if latency_ms else None),
                        "gpu_max_hw_queues": hw_queues,
                        "gather": ("none" if world == 1 else
                                   "gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
@@ -676,6 +699,7 @@ def main():
                                            "(post-timing pass)"},
                          "kernel": kname,
                          "kernel_ms_in_flight": round(avg_kernel_s * 1000.0, 4),
+                         "frames_per_launch": batch,
                          "frame_kernels_ms_in_flight": round(avg_frame_s * 1000.0, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,

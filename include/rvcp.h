@@ -348,6 +348,26 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
                             uint32_t shard_index, uint32_t shard_count,
                             void *d_rgba8, void *d_linear_rgb, void *stream);
 
+/* A batch of n_frames consecutive frames of one shard (frame k rendered with pushes[k]: its
+ * camera and its time seed), enqueued as one unit on `stream`.  The swapchain loop of
+ * vulkan.rs:367-369, 392-401 keeps one frame per swapchain image in flight; here the frames
+ * of a batch share one surface list and one persistent path kernel, so lanes whose pixels of
+ * frame k are done take pixels of frame k+1 while the last sample chains of frame k finish
+ *  -- frames in flight at lane granularity instead of wave granularity.
+ * Layout: frame k's packed shard rows start at pixel k * S of d_rgba8 (and of d_linear_rgb,
+ * 3 floats per pixel, optional), S = rvcp_shard_rows(height, 0, shard_count) * width, the
+ * largest shard's pixels (for a smaller shard the rows after its own are padding and hold
+ * unspecified values); with shard_count = 1, S = W*H and the frames are simply consecutive.
+ * Every frame is bit-identical to rvcp_render_shard_async with the same push.  One pending
+ * batch per context; rvcp_sync_stats covers the whole batch (samples = n_frames x shard
+ * pixels x spp).  Needs a pre-pass schedule of the games101 integrator (automatic schedules
+ * for it, 3-6, 10, and the persistent BVH path kernel; else RVCP_E_UNSUPPORTED unless
+ * n_frames = 1) and a one-GPU context. */
+int rvcp_render_frames_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes,
+                             uint32_t n_frames, uint32_t width, uint32_t height,
+                             uint32_t shard_index, uint32_t shard_count,
+                             void *d_rgba8, void *d_linear_rgb, void *stream);
+
 /* Wait for the last async render of ctx and fetch its statistics. */
 int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats);
 

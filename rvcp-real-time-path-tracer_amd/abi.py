@@ -51,7 +51,7 @@ EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "r
             "rvcp_sync_stats", "rvcp_shard_rows", "rvcp_assemble_frame_async",
             "rvcp_upload_scene_file", "rvcp_mandelbrot", "rvcp_render_async", "rvcp_wait",
             "rvcp_rccl_unique_id", "rvcp_rccl_init", "rvcp_rccl_attach", "rvcp_gather_frame_async",
-            "rvcp_gather_wait"]
+            "rvcp_gather_wait", "rvcp_render_frames_async"]
 
 
 # Integrator mode 2 (ray_tracer.comp ray_trace): its own #defines (ray_tracer.comp:5-13).
@@ -128,6 +128,7 @@ def load():
     L.rvcp_mandelbrot.argtypes = [P, P, u32, u32, P, P, P]
     L.rvcp_render.argtypes = [P, P, u32, u32, P, P, P]
     L.rvcp_render_shard_async.argtypes = [P, P, u32, u32, u32, u32, P, P, P]
+    L.rvcp_render_frames_async.argtypes = [P, P, u32, u32, u32, u32, u32, P, P, P]
     L.rvcp_sync_stats.argtypes = [P, P]
     L.rvcp_render_async.argtypes = [P, P, u32, u32, P, P, P]
     L.rvcp_wait.argtypes = [P, P]
@@ -143,7 +144,8 @@ def load():
                  "rvcp_render", "rvcp_render_shard_async", "rvcp_sync_stats",
                  "rvcp_assemble_frame_async", "rvcp_upload_scene_file", "rvcp_mandelbrot",
                  "rvcp_render_async", "rvcp_wait", "rvcp_rccl_unique_id", "rvcp_rccl_init",
-                 "rvcp_rccl_attach", "rvcp_gather_frame_async", "rvcp_gather_wait"):
+                 "rvcp_rccl_attach", "rvcp_gather_frame_async", "rvcp_gather_wait",
+                 "rvcp_render_frames_async"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -658,16 +658,26 @@ static int wf_reserve(rvcp_ctx_t *ctx, uint32_t n_pixels)
     return RVCP_OK;
 }
 
-static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
-                            uint32_t height, uint32_t shard_index, uint32_t shard_count,
-                            void *d_rgba8, void *d_linear_rgb, void *stream)
+// n_frames consecutive frames of one shard (pushes[k] for frame k) into outputs laid out frame
+// after frame, `slot` = the largest shard's rows apart (rvcp_render_frames_async); n_frames = 1
+// is rvcp_render_shard_async.
+static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, uint32_t n_frames,
+                         uint32_t width, uint32_t height, uint32_t shard_index,
+                         uint32_t shard_count, void *d_rgba8, void *d_linear_rgb, void *stream)
 {
     if (!ctx) return RVCP_E_INVALID;
-    if (!push || !d_rgba8 || width == 0 || height == 0 || shard_count == 0 ||
+    const rvcp_push_constant_t *push = pushes;
+    if (!push || n_frames == 0 || !d_rgba8 || width == 0 || height == 0 || shard_count == 0 ||
         shard_index >= shard_count)
         return fail(ctx, RVCP_E_INVALID, "invalid render arguments");
     if ((uint64_t)width * height >= (1ull << 31))
         return fail(ctx, RVCP_E_INVALID, "frame too large (W*H must be < 2^31)");
+    // frame k of a batch starts `stride` pixels after frame k-1 (the largest shard's pixels)
+    const uint32_t stride = rvcp_shard_rows(height, 0, shard_count) * width;
+    if ((uint64_t)n_frames * stride >= (1ull << 31))
+        return fail(ctx, RVCP_E_INVALID, "batch too large (n_frames x shard pixels must be < 2^31)");
+    if (n_frames > 1 && !ctx->subs.empty())
+        return fail(ctx, RVCP_E_UNSUPPORTED, "frame batches drive one GPU (n_gpus = 1)");
     if (!ctx->has_scene) return fail(ctx, RVCP_E_NO_SCENE, "render before rvcp_upload_scene");
     // one frame in flight per context: its surface list, counters and events are the frame's
     if (ctx->pending)
@@ -719,6 +729,13 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     // first traversal (:413-419): the frame is black.  ray_tracer.comp has no attenuation
     // test before its first traversal (:629-634).
     const bool trivial = A.max_bounces == 0 || (!legacy && 1.0f < A.att_stop);
+    // a batch shares one surface list and one path kernel: the pre-pass schedules (3-6, 10 and
+    // the persistent BVH path kernel) only
+    if (n_frames > 1 && !trivial && (legacy || A.variant < 3 ||
+                                     (A.accel && ctx->cfg.kernel_variant == 9)))
+        return fail(ctx, RVCP_E_UNSUPPORTED, "frame batches need a pre-pass schedule of the games101 "
+                    "integrator (schedules 3-6, 10, or the persistent BVH path kernel)");
+    std::vector<FrameArgs> FA;          // per frame of the batch (camera, time, pixel base)
     ctx->last_spec = false;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(unsigned long long), s));
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
@@ -726,8 +743,8 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
         int rc;
         if (trivial) {
             HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
-            rc = rvcp_launch_fill((uint32_t *)d_rgba8, (float *)d_linear_rgb, A.n_pixels,
-                                  0xFF000000u, s);
+            rc = rvcp_launch_fill((uint32_t *)d_rgba8, (float *)d_linear_rgb,
+                                  n_frames > 1 ? n_frames * stride : A.n_pixels, 0xFF000000u, s);
         } else {
             // the scene-specialised path kernel (§4.7) replaces schedules 3 and 6 when the
             // upload compiled one; its exactness argument needs t_min > 0
@@ -750,7 +767,7 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                 const uint64_t lim = (uint64_t)ctx->cfg.grid_waves_per_simd * ctx->n_simds / wpb;
                 if (lim < cap) cap = lim > 0 ? (uint32_t)lim : 1u;
             }
-            rvcp_static_split(A.n_pixels, cap * wpb, A.n_simds, &waves, &chunk);
+            rvcp_static_split(A.n_pixels * n_frames, cap * wpb, A.n_simds, &waves, &chunk);
             uint32_t blocks = (waves + wpb - 1) / wpb;
             if (blocks > cap) blocks = cap;
             if (blocks == 0) blocks = 1;
@@ -789,13 +806,14 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
             // the mode-2 and v3-family kernels leave linear colours and tonemap_kernel stores
             // the bytes: into the caller's linear buffer, else the context's scratch
             float *lin = (float *)d_linear_rgb;
+            const uint32_t n_lin = n_frames > 1 ? n_frames * stride : A.n_pixels;
             if (!lin && (legacy || A.variant >= 3)) {
-                if (ctx->cap_acc < A.n_pixels) {
+                if (ctx->cap_acc < n_lin) {
                     (void)hipFree(ctx->d_acc);
                     ctx->d_acc = nullptr;
                     ctx->cap_acc = 0;
-                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_acc, (size_t)A.n_pixels * 12));
-                    ctx->cap_acc = A.n_pixels;
+                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_acc, (size_t)n_lin * 12));
+                    ctx->cap_acc = n_lin;
                 }
                 lin = ctx->d_acc;
             }
@@ -807,12 +825,13 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                                         spec_legacy ? (void *)jk->legacy : nullptr);
                 if (spec_legacy) ctx->last_spec = true;
             } else if (A.variant >= 3) {
-                if (ctx->cap_surf < A.n_pixels) {
+                const uint32_t n_surf = A.n_pixels * n_frames;
+                if (ctx->cap_surf < n_surf) {
                     (void)hipFree(ctx->d_surf);
                     ctx->d_surf = nullptr;
                     ctx->cap_surf = 0;
-                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)A.n_pixels * sizeof(SurfRecord)));
-                    ctx->cap_surf = A.n_pixels;
+                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)n_surf * sizeof(SurfRecord)));
+                    ctx->cap_surf = n_surf;
                 }
                 if (A.accel && ctx->cfg.kernel_variant == 9) {
                     // the BVH path in wavefront form (shade / trace generations; measured
@@ -825,7 +844,13 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
                                                    ctx->d_bvh_tris, s, ctx->evm, &ctx->wf);
                     if (rc == -3) return fail(ctx, RVCP_E_HIP, "wavefront BVH frame did not finish");
                 } else {
-                    rc = rvcp_launch_games101_v3(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
+                    FA.assign(n_frames, A);
+                    for (uint32_t k = 1; k < n_frames; ++k) {
+                        camera_constants(pushes[k], width, height, FA[k]);
+                        FA[k].pix_base = k * stride;
+                    }
+                    rc = rvcp_launch_games101_v3(FA.data(), n_frames, stride, ctx->d_tri,
+                                                 ctx->d_faces, ctx->d_verts,
                                                  ctx->d_mats, ctx->d_lights, ctx->d_gamma,
                                                  (uint32_t *)d_rgba8, lin,
                                                  ctx->d_counters, ctx->d_surf, ctx->d_shade,
@@ -853,13 +878,30 @@ static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *
     ctx->last_variant = (trivial || A.n_pixels == 0) ? 0 : legacy ? 8
                       : A.accel ? (ctx->cfg.kernel_variant == 9 ? 9 : 7) : A.variant;
     if (ctx->last_spec && ctx->last_variant != 0) ctx->last_variant |= RVCP_VARIANT_SPECIALIZED;
-    ctx->last_pixels = A.n_pixels;
+    ctx->last_pixels = (uint64_t)A.n_pixels * n_frames;     // stats cover the whole batch
     ctx->last_spp = A.spp;
     ctx->last_shard_index = shard_index;
     ctx->last_shard_count = shard_count;
     ctx->last_width = width;
     ctx->last_height = height;
     return RVCP_OK;
+}
+
+static int impl_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
+                                   uint32_t height, uint32_t shard_index, uint32_t shard_count,
+                                   void *d_rgba8, void *d_linear_rgb, void *stream)
+{
+    return render_frames(ctx, push, 1, width, height, shard_index, shard_count, d_rgba8,
+                         d_linear_rgb, stream);
+}
+
+static int impl_render_frames_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes,
+                                    uint32_t n_frames, uint32_t width, uint32_t height,
+                                    uint32_t shard_index, uint32_t shard_count, void *d_rgba8,
+                                    void *d_linear_rgb, void *stream)
+{
+    return render_frames(ctx, pushes, n_frames, width, height, shard_index, shard_count, d_rgba8,
+                         d_linear_rgb, stream);
 }
 
 static int impl_render_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,
@@ -1262,6 +1304,16 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, u
 {
     return barrier(ctx, [&] { return impl_render_shard_async(ctx, push, width, height,
         shard_index, shard_count, d_rgba8, d_linear_rgb, stream); });
+}
+
+int rvcp_render_frames_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, uint32_t n_frames,
+                             uint32_t width, uint32_t height, uint32_t shard_index,
+                             uint32_t shard_count, void *d_rgba8, void *d_linear_rgb, void *stream)
+{
+    return barrier(ctx, [&] {
+        return impl_render_frames_async(ctx, pushes, n_frames, width, height, shard_index,
+                                        shard_count, d_rgba8, d_linear_rgb, stream);
+    });
 }
 
 int rvcp_render_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint32_t width,

@@ -214,6 +214,9 @@ struct FrameArgs {
     // iteration (early_tail), not only once the queue is empty
     uint32_t spread_min;
     uint32_t early_tail;
+    // index of this frame's first pixel in the outputs (rvcp_render_frames_async: frame k of a
+    // batch starts at k x the largest shard's pixels; 0 for a single frame)
+    uint32_t pix_base;
     // debug build of the library only: per-wave {start, queue exhausted, end, iterations,
     // shader-clock start, shader-clock end}
     // of the path kernel, s_memrealtime ticks (100 MHz); nullptr otherwise
@@ -259,7 +262,11 @@ int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri
                          const rvcp::LightRecord *lights, const float *gamma_t,
                          uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
                          uint32_t grid_blocks, void *stream);
-int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
+// args[0 .. n_frames): one FrameArgs per frame of the batch (pix_base = k x frame_stride);
+// one pre-pass per frame into one surface list, one path kernel, one tone map over
+// n_frames x frame_stride pixels (n_pixels when n_frames == 1)
+int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_frames, uint32_t frame_stride,
+                            const rvcp::TriRecord *tri,
                             const void *faces, const void *verts, const rvcp::MatRecord *mats,
                             const rvcp::LightRecord *lights, const float *gamma_t,
                             uint32_t *out_rgba, float *out_lin, unsigned long long *counters,

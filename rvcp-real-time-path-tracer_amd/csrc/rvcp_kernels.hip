@@ -1391,7 +1391,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
             const f3 Ls = divs(L, (float)A.spp);
             f3 acc = mk(0, 0, 0);
             for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, Ls);
-            store_acc(pix, acc, out_lin);
+            store_acc(A.pix_base + pix, acc, out_lin);
         } else {
             is_surf = true;
         }
@@ -1410,7 +1410,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     __syncthreads();
     if (is_surf) {
         SurfRecord r;
-        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.pix = pix;
+        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.pix = A.pix_base + pix;
         r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.seed = pixel_seed(A, u_, v_);
         r.alb_pi[0] = halb.x; r.alb_pi[1] = halb.y; r.alb_pi[2] = halb.z; r.mat = hmat;
         surf[block_base + wave_off + rank_in(m)] = r;
@@ -3032,7 +3032,8 @@ extern "C" int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::Tri
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
+extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_frames,
+                                       uint32_t frame_stride, const rvcp::TriRecord *tri,
                                        const void *faces, const void *verts,
                                        const rvcp::MatRecord *mats,
                                        const rvcp::LightRecord *lights, const float *gamma_t,
@@ -3046,10 +3047,12 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
 {
     const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
     auto pre = args->accel ? rvcp::games101_primary_kernel<true> : rvcp::games101_primary_kernel<false>;
-    hipLaunchKernelGGL(pre, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
-                       (hipStream_t)stream, *args, tri, (const rvcp_face_t *)faces,
-                       (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
-                       surf, shade, bvh_nodes, bvh_tris);
+    // the frames' pre-passes append to one surface list (stream order: frame 0's pixels first)
+    for (uint32_t k = 0; k < n_frames; ++k)
+        hipLaunchKernelGGL(pre, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
+                           (hipStream_t)stream, args[k], tri, (const rvcp_face_t *)faces,
+                           (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
+                           surf, shade, bvh_nodes, bvh_tris);
     if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
         return -2;
     if (spec_path_fn) {
@@ -3083,11 +3086,13 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, const rvcp::
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade);
     if (hipGetLastError() != hipSuccess) return -2;
-    // the frame's UNORM8 store from the linear colours (out_lin is never null here)
-    uint32_t tb = (args->n_pixels + rvcp::kToneBlock - 1) / rvcp::kToneBlock;
+    // the frame's UNORM8 store from the linear colours (out_lin is never null here); a batch's
+    // frames lie frame_stride pixels apart (the rows of a smaller shard's slot are padding)
+    const uint32_t n_tone = n_frames > 1 ? n_frames * frame_stride : args->n_pixels;
+    uint32_t tb = (n_tone + rvcp::kToneBlock - 1) / rvcp::kToneBlock;
     if (tb > 8192u) tb = 8192u;
     hipLaunchKernelGGL(rvcp::tonemap_kernel, dim3(tb), dim3(rvcp::kToneBlock), 0, (hipStream_t)stream,
-                       out_lin, args->n_pixels, gamma_t, out_rgba);
+                       out_lin, n_tone, gamma_t, out_rgba);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -148,6 +148,18 @@ class RayTracer:
             ctypes.c_void_p(d_rgba), ctypes.c_void_p(d_linear) if d_linear else None,
             ctypes.c_void_p(stream) if stream else None))
 
+    def render_frames_async(self, pushes, width, height, shard_index, shard_count, d_rgba: int,
+                            d_linear: int = 0, stream: int = 0):
+        """rvcp_render_frames_async: a batch of len(pushes) consecutive frames of one shard in
+        one path kernel; frame k's rows start at pixel k * shard_rows(height, 0, shard_count) *
+        width of d_rgba (and of d_linear).  Wait with sync_stats() / wait()."""
+        pushes = np.ascontiguousarray(pushes, dtype=PUSH_DTYPE).reshape(-1)
+        self._push_keepalive = pushes
+        self._check(self._lib.rvcp_render_frames_async(
+            self._ctx, abi.ptr(pushes), len(pushes), width, height, shard_index, shard_count,
+            ctypes.c_void_p(d_rgba), ctypes.c_void_p(d_linear) if d_linear else None,
+            ctypes.c_void_p(stream) if stream else None))
+
     def render_async(self, push, width, height, d_rgba: int, d_linear: int = 0, stream: int = 0):
         """rvcp_render_async: enqueue one full frame into device memory; see wait()."""
         push = np.ascontiguousarray(push, dtype=PUSH_DTYPE)

@@ -36,7 +36,8 @@ def test_auto_pipeline():
     the full grid, up to 1.5 Mpixel of a small scene 3 in flight on 3 waves per SIMD (C3, the
     N=4 / N=8 shares of C4, the sphere room), larger frames the full grid; never more contexts
     than the hardware queues minus one."""
-    ap = bench.auto_pipeline
+    def ap(*a):
+        return bench.auto_pipeline(*a)[:2]
     assert ap(384 * 384, 10, False, True, "8") == (4, 0)                 # C2
     assert ap(384 * 384, 10, False, True, "4") == (3, 0)                 # the box's 4 queues
     assert ap(1024 * 1024, 30, False, True, "4") == (3, 3)               # C3

@@ -1,0 +1,88 @@
+"""rvcp_render_frames_async (include/rvcp.h): a batch of frames in one path kernel is, frame
+by frame, bit-identical to rendering each frame alone -- with a different time seed per frame
+(the reference's per-frame `time`, vulkan.rs:418-421), for whole frames and for shards whose
+rows differ (the padded slot layout), on the schedules that share one surface list; the stats
+cover the whole batch; other integrators / schedules refuse a batch."""
+import numpy as np
+import pytest
+
+import rvcp_amd
+
+pytestmark = pytest.mark.gpu
+TIMES = (123.0, 7.5, 123.0, 301.25)
+
+
+def _single(rt, sc, W, H, k, n, t, torch):
+    rows = rvcp_amd.shard_rows(H, k, n)
+    out = torch.zeros((rows, W), dtype=torch.int32, device="cuda")
+    lin = torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda")
+    rt.render_shard_async(sc.push_constant(t), W, H, k, n, out.data_ptr(), lin.data_ptr())
+    st = rt.sync_stats()
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), lin.cpu().numpy(), st
+
+
+@pytest.mark.parametrize("W,H,spp,k,n,variant", [
+    (160, 96, 5, 0, 1, 0),        # whole frames, the automatic (specialised) schedule
+    (200, 83, 4, 2, 3, 0),        # shard 2 of 3 has fewer rows than the slot: padded layout
+    (200, 83, 4, 0, 3, 0),
+    (96, 64, 3, 0, 1, 4),         # LDS-tiled scan
+    (96, 64, 3, 1, 2, 10),        # tiled + workgroup ray pool
+    (128, 72, 3, 0, 1, 3),        # generic schedule 3
+])
+def test_batch_equals_single_frames(cornell, W, H, spp, k, n, variant):
+    torch = pytest.importorskip("torch")
+    kw = dict(spp=spp)
+    if variant:
+        kw["kernel_variant"] = variant
+        if variant == 3:
+            kw["specialize"] = rvcp_amd.abi.SPECIALIZE_OFF
+    slot = rvcp_amd.shard_rows(H, 0, n)
+    rows = rvcp_amd.shard_rows(H, k, n)
+    with rvcp_amd.RayTracer(**kw) as rt:
+        rt.upload_scene(cornell)
+        singles = [_single(rt, cornell, W, H, k, n, t, torch) for t in TIMES]
+        out = torch.zeros((len(TIMES), slot, W), dtype=torch.int32, device="cuda")
+        lin = torch.zeros((len(TIMES), slot, W, 3), dtype=torch.float32, device="cuda")
+        rt.render_frames_async([cornell.push_constant(t) for t in TIMES], W, H, k, n,
+                               out.data_ptr(), lin.data_ptr())
+        st = rt.sync_stats()
+        torch.cuda.synchronize()
+    out, lin = out.cpu().numpy(), lin.cpu().numpy()
+    for f, (o1, l1, _) in enumerate(singles):
+        assert np.array_equal(out[f, :rows], o1), f
+        assert np.array_equal(lin[f, :rows].view(np.uint32), l1.view(np.uint32)), f
+    assert not np.array_equal(singles[0][0], singles[1][0])      # the seeds differ
+    assert int(st["samples"]) == len(TIMES) * rows * W * spp
+    assert int(st["traversals"]) == sum(int(s["traversals"]) for _, _, s in singles)
+    assert int(st["traversals_executed"]) == sum(int(s["traversals_executed"]) for _, _, s in singles)
+
+
+def test_batch_bvh_equals_single_frames(cornell):
+    torch = pytest.importorskip("torch")
+    sc = rvcp_amd.scene.with_random_triangles(cornell, 300)
+    W, H = 96, 80
+    with rvcp_amd.RayTracer(spp=3, accel=rvcp_amd.abi.ACCEL_BVH) as rt:
+        rt.upload_scene(sc)
+        singles = [_single(rt, sc, W, H, 0, 1, t, torch)[0] for t in TIMES[:3]]
+        out = torch.zeros((3, H, W), dtype=torch.int32, device="cuda")
+        rt.render_frames_async([sc.push_constant(t) for t in TIMES[:3]], W, H, 0, 1, out.data_ptr())
+        rt.sync_stats()
+        torch.cuda.synchronize()
+    for f in range(3):
+        assert np.array_equal(out[f].cpu().numpy(), singles[f]), f
+
+
+def test_batch_refused_where_unsupported(cornell):
+    torch = pytest.importorskip("torch")
+    out = torch.zeros((2, 32, 32), dtype=torch.int32, device="cuda")
+    push = [cornell.push_constant(1.0), cornell.push_constant(2.0)]
+    for kw in (dict(integrator=1), dict(kernel_variant=2)):
+        with rvcp_amd.RayTracer(spp=2, **kw) as rt:
+            rt.upload_scene(cornell)
+            with pytest.raises(rvcp_amd.abi.RvcpError) as e:
+                rt.render_frames_async(push, 32, 32, 0, 1, out.data_ptr())
+            assert e.value.code == rvcp_amd.abi.RVCP_E_UNSUPPORTED
+            # a batch of one is rvcp_render_shard_async
+            rt.render_frames_async(push[:1], 32, 32, 0, 1, out.data_ptr())
+            rt.sync_stats()

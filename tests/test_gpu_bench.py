@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def bench_auto(pixels, spp, hwq):
     sys.path.insert(0, ROOT)
     import bench
-    fif, grid = bench.auto_pipeline(pixels, spp, False, True, hwq)
+    fif, grid, _ = bench.auto_pipeline(pixels, spp, False, True, hwq)
     return fif, (grid if fif >= 3 else 0)
 
 

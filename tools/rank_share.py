@@ -21,23 +21,34 @@ import rvcp_amd  # noqa: E402
 import bench  # noqa: E402
 
 
-def time_share(torch, rts, push, W, H, rank, world, frames):
+def time_share(torch, rts, push, W, H, rank, world, frames, batch=1):
+    """ms per frame of `frames` frames (rounded up to whole batches of `batch` frames per
+    rvcp_render_frames_async call), round-robin over the contexts."""
     fif = len(rts)
-    rows = rvcp_amd.shard_rows(H, rank, world)
-    bufs = [torch.zeros((rows, W), dtype=torch.int32, device="cuda") for _ in range(fif)]
+    slot = rvcp_amd.shard_rows(H, 0, world)
+    bufs = [torch.zeros((batch, slot, W), dtype=torch.int32, device="cuda") for _ in range(fif)]
+    pushes = [push] * batch
+
+    def enqueue(i):
+        if batch == 1:
+            rts[i].render_shard_async(push, W, H, rank, world, bufs[i].data_ptr())
+        else:
+            rts[i].render_frames_async(pushes, W, H, rank, world, bufs[i].data_ptr())
     for i in range(fif):                                   # warm-up, one per context
-        rts[i].render_shard_async(push, W, H, rank, world, bufs[i].data_ptr())
+        enqueue(i)
     for i in range(fif):
         rts[i].sync_stats()
     torch.cuda.synchronize()
     pending = [False] * fif
     kms = []
+    calls = (frames + batch - 1) // batch
+    frames = calls * batch
     t0 = time.perf_counter()
-    for f in range(frames):
+    for f in range(calls):
         i = f % fif
         if pending[i]:
             kms.append(float(rts[i].sync_stats()["main_kernel_ms"]))
-        rts[i].render_shard_async(push, W, H, rank, world, bufs[i].data_ptr())
+        enqueue(i)
         pending[i] = True
     for i in range(fif):
         if pending[i]:
@@ -55,6 +66,8 @@ def main():
     ap.add_argument("--size", type=int, default=2048)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--schedule", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=1,
+                    help="frames per rvcp_render_frames_async call (1 = rvcp_render_shard_async)")
     ap.add_argument("--grid", type=int, default=-1,
                     help="rvcp_config_t.grid_waves_per_simd (0 = every resident slot, -1 = "
                          "bench.py's automatic choice)")
@@ -69,17 +82,18 @@ def main():
     one = None
     for n in [int(x) for x in a.ns.split(",")]:
         rank_samples = W * a.spp * rvcp_amd.shard_rows(H, 0, n)
-        fif, grid = bench.auto_pipeline(W * rvcp_amd.shard_rows(H, 0, n), a.spp, False, True,
+        fif, grid, _ = bench.auto_pipeline(W * rvcp_amd.shard_rows(H, 0, n), a.spp, False, True,
                                         os.environ["GPU_MAX_HW_QUEUES"])
         fif = a.fif or fif
         grid = a.grid if a.grid >= 0 else grid
         rts = [rvcp_amd.RayTracer(grid_waves_per_simd=grid, **kw) for _ in range(fif)]
         for r in rts:
             r.upload_scene(sc)
-        wall, kern = time_share(torch, rts, push, W, H, 0, n, a.frames)
+        wall, kern = time_share(torch, rts, push, W, H, 0, n, a.frames, a.batch)
         if n == 1:
             one = wall
-        out = dict(n=n, rows=rvcp_amd.shard_rows(H, 0, n), fif=fif, grid=grid, ms_per_frame=round(wall, 3),
+        out = dict(n=n, rows=rvcp_amd.shard_rows(H, 0, n), fif=fif, grid=grid, batch=a.batch,
+                   ms_per_frame=round(wall, 3),
                    path_kernel_ms=round(kern, 3),
                    msamples_s=round(rank_samples / wall / 1e3, 1))
         if one is not None:
