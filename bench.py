@@ -260,37 +260,44 @@ def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe=None):
 
 
 def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none"):
-    """Frames in flight and the path kernel's grid per frame (rvcp_config_t.grid_waves_per_simd,
-    0 = every resident slot) for a rank-frame of `pixels` pixels.
+    """Frames in flight, the path kernel's grid per frame (rvcp_config_t.grid_waves_per_simd,
+    0 = every resident slot) and frames per path kernel (rvcp_render_frames_async) for a
+    rank-frame of `pixels` pixels.
 
-    `fif` contexts render consecutive frames on their own streams, so frame f+1's pre-pass and
-    path kernel fill the CUs that frame f's tail leaves idle -- the per-image fences of the
-    reference's swapchain loop (vulkan.rs:367-369).  A context holds one frame at a time
-    (rvcp.h), so frame f waits, at its enqueue, for the frame its context rendered fif steps
+    `fif` contexts render consecutive launches on their own streams, so launch f+1's pre-pass
+    and path kernel fill the CUs that launch f's tail leaves idle -- the per-image fences of the
+    reference's swapchain loop (vulkan.rs:367-369).  A context holds one launch at a time
+    (rvcp.h), so launch f waits, at its enqueue, for the one its context ran fif launches
     earlier.  A pixel is a serial chain of SPP samples: a frame of P surface pixels on L
     resident lanes ends in a tail once P/L is small (C3: ~2.6 pixels per lane, the N=8 share of
-    C4: ~1.3), and a smaller grid per frame with a third frame beside it lets the next frame's
-    waves start in that tail.  Measured (profiles/r03zp_grid_bench_ab.log, r03zp_grid_share.log):
-      - up to 1.5 Mpixel, brute-force scan of a small scene: 3 in flight on 3 waves per SIMD --
-        C3 3.35 -> 3.25 ms, mode 2 on the C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269
-        ms, the N=8 share of C4 3.80 -> 3.63 ms, the N=4 share 7.05 -> 6.92 ms;
-      - larger frames keep the full grid: C4 on one GPU 26.35 ms, 26.91 with 3 / 3;
-      - below 4 Msamples (C2): 4 in flight (C2 0.59/0.32/0.27/0.33 ms for 1/2/3/4 in flight,
-        profiles/r02_fif_sweep.log), the full grid (3 waves measured equal);
-      - otherwise 2 in flight, 3 in mode 2 (one kernel per frame, no pre-pass: C3 frame
-        2.84/2.40/2.29/2.46 ms for 1/2/3/4 in flight, profiles/r02_m2_fif_sweep.log).
+    C4: ~1.3).  Two remedies, measured (profiles/r03zt_batch_sweep.log, r03zu_batch_sweep2.log,
+    r03zp_grid_bench_ab.log): a batch of frames in one path kernel, whose lanes take frame k+1's
+    pixels while frame k's last chains finish (games101 pre-pass schedules), and else a smaller
+    grid per frame with a third frame beside it, whose waves start in the tail:
+      - games101, brute-force scan of a small scene, up to 1.5 Mpixel or below 4 Msamples:
+        batches of 3 frames, 2 in flight -- C3 3.31 -> 3.20 ms, the N=8 share of C4
+        3.65 -> 3.46 ms, C2 0.232 -> 0.208 ms against 3 single frames in flight on 3 waves per
+        SIMD (batches of 2: 3.24 / 3.56 / 0.226);
+      - mode 2 (no pre-pass, no batches), up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD --
+        mode 2 on the C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms;
+      - larger frames: full grid, one frame per launch, 2 in flight (3 in mode 2: one kernel per
+        frame, no pre-pass): C4 on one GPU 26.35 ms (batches of 2: 26.16, 3 in flight 26.50);
+      - other small frames (below 4 Msamples): 4 in flight (C2 0.59/0.32/0.27/0.33 ms for
+        1/2/3/4 in flight, profiles/r02_fif_sweep.log).
     Contexts beyond the hardware queues minus one contend for queues."""
-    if pixels * spp < (4 << 20):
-        fif, grid = 4, 0
+    mid = pixels <= 1536 * 1024 or pixels * spp < (4 << 20)
+    if small_scene and not legacy and accel == "none" and mid:
+        fif, grid, batch = 2, 0, 3
+    elif pixels * spp < (4 << 20):
+        fif, grid, batch = 4, 0, 1
     elif small_scene and pixels <= 1536 * 1024:
-        fif, grid = 3, 3
+        fif, grid, batch = 3, 3, 1
     else:
-        fif, grid = (3 if legacy else 2), 0
+        fif, grid, batch = (3 if legacy else 2), 0, 1
     try:
         fif = max(1, min(fif, int(hw_queues) - 1))
     except ValueError:
         pass
-    batch = 1
     return fif, grid, batch
 
 
@@ -388,7 +395,7 @@ def main():
     fif_auto, grid_auto, batch_auto = auto_pipeline(W * rvcp_amd.shard_rows(H, rank, world), spp,
                                                     legacy, small_scene, hw_queues, args.accel)
     fif = 1 if rehearsal else (args.frames_in_flight or fif_auto)
-    batch = 1 if rehearsal else (args.batch or batch_auto)
+    batch = args.batch or batch_auto
     # (the smaller grid leaves room for frames beside it: with fewer in flight, the full grid)
     grid_waves = args.grid_waves if args.grid_waves >= 0 else (grid_auto if fif >= 3 else 0)
     cfg_kw["grid_waves_per_simd"] = grid_waves

@@ -86,3 +86,45 @@ def test_batch_refused_where_unsupported(cornell):
             # a batch of one is rvcp_render_shard_async
             rt.render_frames_async(push[:1], 32, 32, 0, 1, out.data_ptr())
             rt.sync_stats()
+
+
+def test_batch_with_rccl_gathers(cornell):
+    """bench.py's N>1 pattern with batches, at world size 1: two contexts, each with its own
+    communicator, alternate batches of 3 frames (different seeds) and gather every frame of a
+    batch (one rvcp_gather_frame_async per frame, sharing the gather buffer in stream order);
+    every assembled frame equals the direct render of its seed."""
+    torch = pytest.importorskip("torch")
+    W, H = 120, 64
+    times = TIMES[:3]
+    rts = [rvcp_amd.RayTracer(spp=3) for _ in range(2)]
+    try:
+        for rt in rts:
+            rt.upload_scene(cornell)
+            rt.rccl_init(rvcp_amd.rccl_unique_id(), 1, 0)
+        refs = [rts[0].render(W, H, t) for t in times]
+        slot = rvcp_amd.shard_rows(H, 0, 1)
+        shards = [torch.zeros((3, slot, W), dtype=torch.int32, device="cuda") for _ in range(2)]
+        gath = [torch.zeros((1, slot, W), dtype=torch.int32, device="cuda") for _ in range(2)]
+        frames = [torch.zeros((3, H, W), dtype=torch.int32, device="cuda") for _ in range(2)]
+        pending = [False, False]
+        pushes = [cornell.push_constant(t) for t in times]
+        for c in range(5):
+            i = c % 2
+            if pending[i]:
+                rts[i].sync_stats()
+                rts[i].gather_wait()
+            rts[i].render_frames_async(pushes, W, H, 0, 1, shards[i].data_ptr())
+            for j in range(3):
+                rts[i].gather_frame_async(shards[i][j].data_ptr(), W, H, gath[i].data_ptr(),
+                                          frames[i][j].data_ptr())
+            pending[i] = True
+        for i in range(2):
+            rts[i].sync_stats()
+            rts[i].gather_wait()
+        torch.cuda.synchronize()
+        for fr in frames:
+            for j in range(3):
+                assert np.array_equal(fr[j].cpu().numpy().view(np.uint8).reshape(H, W, 4), refs[j]), j
+    finally:
+        for rt in rts:
+            rt.close()

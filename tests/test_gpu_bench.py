@@ -21,14 +21,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def bench_auto(pixels, spp, hwq):
     sys.path.insert(0, ROOT)
     import bench
-    fif, grid, _ = bench.auto_pipeline(pixels, spp, False, True, hwq)
-    return fif, (grid if fif >= 3 else 0)
+    fif, grid, batch = bench.auto_pipeline(pixels, spp, False, True, hwq)
+    return fif, (grid if fif >= 3 else 0), batch
 
 
 @pytest.mark.parametrize("workload,side,spp,steps", [("c2", 384, 10, 6), ("c3", 1024, 30, 4)])
 def test_bench_line(tmp_path, workload, side, spp, steps):
-    """C2 (4 frames in flight or the hardware queues' limit, full grid) and C3 (3 in flight
-    on 3 waves per SIMD, bench.auto_pipeline)."""
+    """C2 and C3 (bench.auto_pipeline: batches of 3 frames per path kernel, 2 in flight); the
+    saved frame -- the first of a batch -- is the oracle's."""
     frame_path = tmp_path / "frame.npy"
     env = dict(os.environ)
     env.pop("RVCP_LIB", None)
@@ -45,8 +45,10 @@ def test_bench_line(tmp_path, workload, side, spp, steps):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == 2
     W = H = side
-    fif, grid = d["config"]["frames_in_flight"], d["config"]["grid_waves_per_simd"]
-    assert (fif, grid) == bench_auto(W * H, spp, d["config"]["gpu_max_hw_queues"])
+    c = d["config"]
+    assert (c["frames_in_flight"], c["grid_waves_per_simd"], c["frames_per_launch"]) == \
+        bench_auto(W * H, spp, c["gpu_max_hw_queues"])
+    assert c["frame_latency_ms_alone"] > 0
     assert d["value"] == pytest.approx(W * H * spp / (d["ms_per_step"] / 1000.0) / 1e6, rel=2e-3)
     rl = d["roofline"]
     assert rl["bound"] == "valu" and rl["peak"] == 157.3

@@ -66,8 +66,9 @@ def main():
     ap.add_argument("--size", type=int, default=2048)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--schedule", type=int, default=0)
-    ap.add_argument("--batch", type=int, default=1,
-                    help="frames per rvcp_render_frames_async call (1 = rvcp_render_shard_async)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per rvcp_render_frames_async call (1 = rvcp_render_shard_async, "
+                         "0 = bench.py's automatic choice)")
     ap.add_argument("--grid", type=int, default=-1,
                     help="rvcp_config_t.grid_waves_per_simd (0 = every resident slot, -1 = "
                          "bench.py's automatic choice)")
@@ -82,17 +83,18 @@ def main():
     one = None
     for n in [int(x) for x in a.ns.split(",")]:
         rank_samples = W * a.spp * rvcp_amd.shard_rows(H, 0, n)
-        fif, grid, _ = bench.auto_pipeline(W * rvcp_amd.shard_rows(H, 0, n), a.spp, False, True,
+        fif, grid, batch = bench.auto_pipeline(W * rvcp_amd.shard_rows(H, 0, n), a.spp, False, True,
                                         os.environ["GPU_MAX_HW_QUEUES"])
         fif = a.fif or fif
-        grid = a.grid if a.grid >= 0 else grid
+        grid = a.grid if a.grid >= 0 else (grid if fif >= 3 else 0)
+        batch = a.batch or batch
         rts = [rvcp_amd.RayTracer(grid_waves_per_simd=grid, **kw) for _ in range(fif)]
         for r in rts:
             r.upload_scene(sc)
-        wall, kern = time_share(torch, rts, push, W, H, 0, n, a.frames, a.batch)
+        wall, kern = time_share(torch, rts, push, W, H, 0, n, a.frames, batch)
         if n == 1:
             one = wall
-        out = dict(n=n, rows=rvcp_amd.shard_rows(H, 0, n), fif=fif, grid=grid, batch=a.batch,
+        out = dict(n=n, rows=rvcp_amd.shard_rows(H, 0, n), fif=fif, grid=grid, batch=batch,
                    ms_per_frame=round(wall, 3),
                    path_kernel_ms=round(kern, 3),
                    msamples_s=round(rank_samples / wall / 1e3, 1))
