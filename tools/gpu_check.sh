@@ -52,22 +52,23 @@ for s in $STEPS; do
         # the headline command under rocprofv3: default frames in flight, and one frame in flight
         # (per-launch durations that do not overlap -- roofline.per_launch)
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
-        prof1) run prof1 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof1_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --frames-in-flight 1 ;;
-        # PMC passes, one counter group per run (one frame in flight, so each dispatch is its own)
-        pmcf) run pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
-        pmcw) run pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
-        sqpmc) run sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
-        sqpmc2) run sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
-        c5pmcf) run c5pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5pmcf_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
-        c5pmcw) run c5pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5pmcw_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
-        c5sqpmc) run c5sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c5sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
-        c5sqpmc2) run c5sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d "$OUT/c5sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
-        bvhsqpmc) run bvhsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/bvhsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
-        bvhsqpmc2) run bvhsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/bvhsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 ;;
-        m2sqpmc) run m2sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/m2sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
-        m2sqpmc2) run m2sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/m2sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 ;;
-        spsqpmc) run spsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/spsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --frames-in-flight 1 ;;
-        spsqpmc2) run spsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/spsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --frames-in-flight 1 ;;
+        prof1) run prof1 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof1_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        # PMC passes, one counter group per run (one frame in flight and one frame per launch, so
+        # each dispatch is one frame of its own)
+        pmcf) run pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        pmcw) run pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        sqpmc) run sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        sqpmc2) run sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        c5pmcf) run c5pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5pmcf_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        c5pmcw) run c5pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5pmcw_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        c5sqpmc) run c5sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c5sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        c5sqpmc2) run c5sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d "$OUT/c5sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        bvhsqpmc) run bvhsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/bvhsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        bvhsqpmc2) run bvhsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/bvhsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        m2sqpmc) run m2sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/m2sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        m2sqpmc2) run m2sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/m2sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        spsqpmc) run spsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/spsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        spsqpmc2) run spsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/spsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
         # the chip's VALU issue ceiling and its in-kernel clock; the C3 kernel's in-kernel clock
         valu) run valu_rate 180 tools/build/valu_rate ;;
         valupmc) run valupmc 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/valupmc_$TAG" -o run --output-format csv -- tools/build/valu_rate ;;
