@@ -274,10 +274,11 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none"):
     r03zp_grid_bench_ab.log): a batch of frames in one path kernel, whose lanes take frame k+1's
     pixels while frame k's last chains finish (games101 pre-pass schedules), and else a smaller
     grid per frame with a third frame beside it, whose waves start in the tail:
-      - games101, brute-force scan of a small scene, up to 1.5 Mpixel or below 4 Msamples:
-        batches of 3 frames, 2 in flight -- C3 3.31 -> 3.20 ms, the N=8 share of C4
-        3.65 -> 3.46 ms, C2 0.232 -> 0.208 ms against 3 single frames in flight on 3 waves per
-        SIMD (batches of 2: 3.24 / 3.56 / 0.226);
+      - games101, brute-force scan of a small scene or the opt-in BVH, up to 1.5 Mpixel or
+        below 4 Msamples: batches of 3 frames, 2 in flight -- C3 3.31 -> 3.20 ms, the N=8
+        share of C4 3.65 -> 3.46 ms, C2 0.232 -> 0.208 ms against 3 single frames in flight on
+        3 waves per SIMD (batches of 2: 3.24 / 3.56 / 0.226); C5 with the BVH 97.6 -> 92.0 ms
+        against single frames, 2 in flight (profiles/r03zw_bvh_batch_ab.log);
       - mode 2 (no pre-pass, no batches), up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD --
         mode 2 on the C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms;
       - larger frames: full grid, one frame per launch, 2 in flight (3 in mode 2: one kernel per
@@ -286,7 +287,7 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none"):
         1/2/3/4 in flight, profiles/r02_fif_sweep.log).
     Contexts beyond the hardware queues minus one contend for queues."""
     mid = pixels <= 1536 * 1024 or pixels * spp < (4 << 20)
-    if small_scene and not legacy and accel == "none" and mid:
+    if not legacy and (small_scene or accel == "bvh") and mid:
         fif, grid, batch = 2, 0, 3
     elif pixels * spp < (4 << 20):
         fif, grid, batch = 4, 0, 1

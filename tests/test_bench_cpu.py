@@ -48,7 +48,7 @@ def test_auto_pipeline():
     assert ap(384 * 384, 5, True, True, "8") == (4, 0, 1)                # small mode-2 frame
     assert ap(384 * 384, 5, True, True, "4") == (3, 0, 1)                # ... on 4 queues
     assert ap(1024 * 1024, 30, False, False, "4") == (2, 0, 1)           # C5 (mesh)
-    assert ap(1024 * 1024, 30, False, False, "4", "bvh") == (2, 0, 1)    # BVH (not a small-scene scan)
+    assert ap(1024 * 1024, 30, False, False, "4", "bvh") == (2, 0, 3)    # C5 with the BVH
     assert ap(1024 * 1024, 30, False, True, "2") == (1, 0, 3)
     assert ap(1024 * 1024, 30, False, True, "x") == (2, 0, 3)
 
