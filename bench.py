@@ -259,7 +259,7 @@ def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe=None):
     return "rccl", None
 
 
-def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none"):
+def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", steps=0):
     """Frames in flight, the path kernel's grid per frame (rvcp_config_t.grid_waves_per_simd,
     0 = every resident slot) and frames per path kernel (rvcp_render_frames_async) for a
     rank-frame of `pixels` pixels.
@@ -275,10 +275,13 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none"):
     pixels while frame k's last chains finish (games101 pre-pass schedules), and else a smaller
     grid per frame with a third frame beside it, whose waves start in the tail:
       - games101, brute-force scan of a small scene or the opt-in BVH, up to 1.5 Mpixel or
-        below 4 Msamples: batches of 3 frames, 2 in flight -- C3 3.31 -> 3.20 ms, the N=8
-        share of C4 3.65 -> 3.46 ms, C2 0.232 -> 0.208 ms against 3 single frames in flight on
-        3 waves per SIMD (batches of 2: 3.24 / 3.56 / 0.226); C5 with the BVH 97.6 -> 92.0 ms
-        against single frames, 2 in flight (profiles/r03zw_bvh_batch_ab.log);
+        below 4 Msamples: batches of about 3 Mpixel (at most 16 frames, and at most a quarter
+        of the timed steps), 2 in flight.  Batches of 3 against 3 single frames in flight on
+        3 waves per SIMD: C3 3.31 -> 3.20 ms, the N=8 share of C4 3.65 -> 3.46 ms, C2
+        0.232 -> 0.208 ms (batches of 2: 3.24 / 3.56 / 0.226); deeper batches for smaller
+        launches (r03zx_batch_sweep3.log): the N=8 share 3.42 / 3.37 / 3.33 ms with 3 / 4 / 6
+        frames, C2 0.195 / 0.173 / 0.162 / 0.158 ms with 3 / 6 / 10 / 16; C5 with the BVH
+        97.6 -> 92.0 ms with 3 (profiles/r03zw_bvh_batch_ab.log);
       - mode 2 (no pre-pass, no batches), up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD --
         mode 2 on the C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms;
       - larger frames: full grid, one frame per launch, 2 in flight (3 in mode 2: one kernel per
@@ -288,7 +291,10 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none"):
     Contexts beyond the hardware queues minus one contend for queues."""
     mid = pixels <= 1536 * 1024 or pixels * spp < (4 << 20)
     if not legacy and (small_scene or accel == "bvh") and mid:
-        fif, grid, batch = 2, 0, 3
+        # about 3 Mpixel per launch, at most 16 frames, and at least 4 launches in the run
+        batch = max(1, min(-(-3 * 1024 * 1024 // max(1, pixels)), 16,
+                           steps // 4 if steps else 16))
+        fif, grid = 2, 0
     elif pixels * spp < (4 << 20):
         fif, grid, batch = 4, 0, 1
     elif small_scene and pixels <= 1536 * 1024:
@@ -394,7 +400,8 @@ def main():
     # profiles/r02_hwq_fif_sweep.log; C3 2 and 3 equal)
     small_scene = args.accel == "none" and not wl["extra_tris"]
     fif_auto, grid_auto, batch_auto = auto_pipeline(W * rvcp_amd.shard_rows(H, rank, world), spp,
-                                                    legacy, small_scene, hw_queues, args.accel)
+                                                    legacy, small_scene, hw_queues, args.accel,
+                                                    args.steps)
     fif = 1 if rehearsal else (args.frames_in_flight or fif_auto)
     batch = args.batch or batch_auto
     # (the smaller grid leaves room for frames beside it: with fewer in flight, the full grid)

@@ -33,24 +33,29 @@ def test_workloads_match_baseline_configs():
 
 def test_auto_pipeline():
     """Frames in flight, grid per frame and frames per launch: games101 on a
-    small scene up to 1.5 Mpixel (C2, C3, the N=4 / N=8 shares of C4) in batches of 3 frames,
-    2 in flight; mode 2 there 3 in flight on 3 waves per SIMD; larger frames the full grid,
-    one frame per launch; never more contexts than the hardware queues minus one."""
+    small scene (or the BVH) up to 1.5 Mpixel in batches of about 3 Mpixel (at most 16 frames,
+    at most a quarter of the timed steps), 2 in flight; mode 2 there 3 in flight on 3 waves per
+    SIMD; larger frames the full grid, one frame per launch; never more contexts than the
+    hardware queues minus one."""
     ap = bench.auto_pipeline
-    assert ap(384 * 384, 10, False, True, "4") == (2, 0, 3)              # C2
-    assert ap(1024 * 1024, 30, False, True, "4") == (2, 0, 3)            # C3
-    assert ap(2048 * 256, 64, False, True, "4") == (2, 0, 3)             # C4, N=8 share
-    assert ap(2048 * 512, 64, False, True, "4") == (2, 0, 3)             # C4, N=4 share
-    assert ap(2048 * 1024, 64, False, True, "4") == (2, 0, 1)            # C4, N=2 share
-    assert ap(2048 * 2048, 64, False, True, "4") == (2, 0, 1)            # C4, one GPU
-    assert ap(1024 * 1024, 30, True, True, "4") == (3, 3, 1)             # mode 2 on the C3 frame
-    assert ap(1024 * 1024, 5, True, True, "4") == (3, 3, 1)              # sphere room
-    assert ap(384 * 384, 5, True, True, "8") == (4, 0, 1)                # small mode-2 frame
-    assert ap(384 * 384, 5, True, True, "4") == (3, 0, 1)                # ... on 4 queues
-    assert ap(1024 * 1024, 30, False, False, "4") == (2, 0, 1)           # C5 (mesh)
-    assert ap(1024 * 1024, 30, False, False, "4", "bvh") == (2, 0, 3)    # C5 with the BVH
-    assert ap(1024 * 1024, 30, False, True, "2") == (1, 0, 3)
-    assert ap(1024 * 1024, 30, False, True, "x") == (2, 0, 3)
+    assert ap(1024 * 1024, 30, False, True, "4", "none", 20) == (2, 0, 3)          # C3
+    assert ap(1024 * 1024, 30, False, True, "4") == (2, 0, 3)
+    assert ap(2048 * 256, 64, False, True, "4", "none", 40) == (2, 0, 6)           # C4, N=8 share
+    assert ap(2048 * 256, 64, False, True, "4", "none", 20) == (2, 0, 5)
+    assert ap(2048 * 512, 64, False, True, "4", "none", 20) == (2, 0, 3)           # C4, N=4 share
+    assert ap(2048 * 1024, 64, False, True, "4", "none", 20) == (2, 0, 1)          # C4, N=2 share
+    assert ap(2048 * 2048, 64, False, True, "4", "none", 20) == (2, 0, 1)          # C4, one GPU
+    assert ap(384 * 384, 10, False, True, "4", "none", 200) == (2, 0, 16)          # C2
+    assert ap(384 * 384, 10, False, True, "4", "none", 20) == (2, 0, 5)
+    assert ap(384 * 384, 10, False, True, "4", "none", 3) == (2, 0, 1)
+    assert ap(1024 * 1024, 30, True, True, "4", "none", 20) == (3, 3, 1)           # mode 2, C3 frame
+    assert ap(1024 * 1024, 5, True, True, "4", "none", 20) == (3, 3, 1)            # sphere room
+    assert ap(384 * 384, 5, True, True, "8", "none", 20) == (4, 0, 1)              # small mode-2 frame
+    assert ap(384 * 384, 5, True, True, "4", "none", 20) == (3, 0, 1)              # ... on 4 queues
+    assert ap(1024 * 1024, 30, False, False, "4", "none", 20) == (2, 0, 1)         # C5 (mesh)
+    assert ap(1024 * 1024, 30, False, False, "4", "bvh", 20) == (2, 0, 3)          # C5 with the BVH
+    assert ap(1024 * 1024, 30, False, True, "2", "none", 20) == (1, 0, 3)
+    assert ap(1024 * 1024, 30, False, True, "x", "none", 20) == (2, 0, 3)
 
 
 def test_roofline_constants():

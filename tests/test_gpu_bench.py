@@ -18,17 +18,18 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def bench_auto(pixels, spp, hwq):
+def bench_auto(pixels, spp, hwq, steps):
     sys.path.insert(0, ROOT)
     import bench
-    fif, grid, batch = bench.auto_pipeline(pixels, spp, False, True, hwq)
+    fif, grid, batch = bench.auto_pipeline(pixels, spp, False, True, hwq, "none", steps)
     return fif, (grid if fif >= 3 else 0), batch
 
 
-@pytest.mark.parametrize("workload,side,spp,steps", [("c2", 384, 10, 6), ("c3", 1024, 30, 4)])
+@pytest.mark.parametrize("workload,side,spp,steps", [("c2", 384, 10, 26), ("c3", 1024, 30, 13)])
 def test_bench_line(tmp_path, workload, side, spp, steps):
-    """C2 and C3 (bench.auto_pipeline: batches of 3 frames per path kernel, 2 in flight); the
-    saved frame -- the first of a batch -- is the oracle's."""
+    """C2 and C3 (bench.auto_pipeline: batches of frames per path kernel, 2 in flight; step
+    counts that leave a shorter last batch); the saved frame -- the first of a batch -- is the
+    oracle's."""
     frame_path = tmp_path / "frame.npy"
     env = dict(os.environ)
     env.pop("RVCP_LIB", None)
@@ -47,7 +48,8 @@ def test_bench_line(tmp_path, workload, side, spp, steps):
     W = H = side
     c = d["config"]
     assert (c["frames_in_flight"], c["grid_waves_per_simd"], c["frames_per_launch"]) == \
-        bench_auto(W * H, spp, c["gpu_max_hw_queues"])
+        bench_auto(W * H, spp, c["gpu_max_hw_queues"], steps)
+    assert c["frames_per_launch"] > 1          # batches of 6 / 3, the last one shorter
     assert c["frame_latency_ms_alone"] > 0
     assert d["value"] == pytest.approx(W * H * spp / (d["ms_per_step"] / 1000.0) / 1e6, rel=2e-3)
     rl = d["roofline"]

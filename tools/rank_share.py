@@ -84,7 +84,7 @@ def main():
     for n in [int(x) for x in a.ns.split(",")]:
         rank_samples = W * a.spp * rvcp_amd.shard_rows(H, 0, n)
         fif, grid, batch = bench.auto_pipeline(W * rvcp_amd.shard_rows(H, 0, n), a.spp, False, True,
-                                        os.environ["GPU_MAX_HW_QUEUES"])
+                                               os.environ["GPU_MAX_HW_QUEUES"], "none", a.frames)
         fif = a.fif or fif
         grid = a.grid if a.grid >= 0 else (grid if fif >= 3 else 0)
         batch = a.batch or batch
