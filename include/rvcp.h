@@ -360,9 +360,11 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
  * unspecified values); with shard_count = 1, S = W*H and the frames are simply consecutive.
  * Every frame is bit-identical to rvcp_render_shard_async with the same push.  One pending
  * batch per context; rvcp_sync_stats covers the whole batch (samples = n_frames x shard
- * pixels x spp).  Needs a pre-pass schedule of the games101 integrator (automatic schedules
- * for it, 3-6, 10, and the persistent BVH path kernel; else RVCP_E_UNSUPPORTED unless
- * n_frames = 1) and a one-GPU context. */
+ * pixels x spp).  Integrator mode 2 (RVCP_INTEGRATOR_LEGACY) has no pre-pass: its one kernel
+ * queues the batch's pixels frame after frame, reading each frame's camera and time from a
+ * table the call uploads.  Needs a one-GPU context and, for games101, a pre-pass schedule (the
+ * automatic ones: 3-6, 10, the persistent BVH path kernel); schedules 1, 2 and the BVH
+ * wavefront form return RVCP_E_UNSUPPORTED unless n_frames = 1. */
 int rvcp_render_frames_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes,
                              uint32_t n_frames, uint32_t width, uint32_t height,
                              uint32_t shard_index, uint32_t shard_count,

@@ -81,6 +81,10 @@ struct rvcp_ctx {
     size_t cap_surf = 0;
     float *d_acc = nullptr;         // linear colours for tonemap_kernel when the caller wants none
     size_t cap_acc = 0;
+    // mode-2 batches: the frames' FrameCam records (16 floats each), staged through pinned
+    // host memory (one render in flight per context, so the staging is free again at the next)
+    float *d_cams = nullptr, *h_cams = nullptr;
+    uint32_t cap_cams = 0;
     // wavefront BVH path (rvcp_launch_bvh_wavefront): slot state, ray list, results, counters,
     // trace stacks, the pinned read-back words and their events; allocated on the first BVH frame
     WfBuffers wf{};
@@ -453,6 +457,8 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     (void)hipFree(ctx->d_lin);
     (void)hipFree(ctx->d_surf);
     (void)hipFree(ctx->d_acc);
+    (void)hipFree(ctx->d_cams);
+    (void)hipHostFree(ctx->h_cams);
     (void)hipFree(ctx->wf.st);
     (void)hipFree(ctx->wf.rays);
     (void)hipFree(ctx->wf.res);
@@ -731,11 +737,46 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     const bool trivial = A.max_bounces == 0 || (!legacy && 1.0f < A.att_stop);
     // a batch shares one surface list and one path kernel: the pre-pass schedules (3-6, 10 and
     // the persistent BVH path kernel) only
-    if (n_frames > 1 && !trivial && (legacy || A.variant < 3 ||
-                                     (A.accel && ctx->cfg.kernel_variant == 9)))
+    if (n_frames > 1 && !trivial && !legacy && (A.variant < 3 ||
+                                               (A.accel && ctx->cfg.kernel_variant == 9)))
         return fail(ctx, RVCP_E_UNSUPPORTED, "frame batches need a pre-pass schedule of the games101 "
-                    "integrator (schedules 3-6, 10, or the persistent BVH path kernel)");
+                    "integrator (schedules 3-6, 10, or the persistent BVH path kernel) or mode 2");
     std::vector<FrameArgs> FA;          // per frame of the batch (camera, time, pixel base)
+    const uint32_t frame_px = A.n_pixels;
+    const uint32_t split_px = frame_px * n_frames;          // the queue of the whole batch
+    if (n_frames > 1 && !trivial && legacy && frame_px > 0) {
+        // mode 2 has no pre-pass: its one kernel queues the batch's pixels frame after frame
+        // and reads each frame's camera and time from d_cams (FrameArgs::batch_cams)
+        if (ctx->cap_cams < n_frames) {
+            (void)hipFree(ctx->d_cams);
+            (void)hipHostFree(ctx->h_cams);
+            ctx->d_cams = ctx->h_cams = nullptr;
+            ctx->cap_cams = 0;
+            HIP_TRY(ctx, hipMalloc((void **)&ctx->d_cams, (size_t)n_frames * 64));
+            HIP_TRY(ctx, hipHostMalloc((void **)&ctx->h_cams, (size_t)n_frames * 64));
+            ctx->cap_cams = n_frames;
+        }
+        for (uint32_t k = 0; k < n_frames; ++k) {
+            FrameArgs C;
+            std::memset(&C, 0, sizeof(C));
+            camera_constants(pushes[k], width, height, C);
+            float *c = ctx->h_cams + 16 * (size_t)k;
+            std::memcpy(c, C.cam_pos, 12);
+            std::memcpy(c + 3, C.u, 12);
+            std::memcpy(c + 6, C.v, 12);
+            std::memcpy(c + 9, C.pos, 12);
+            c[12] = C.base_len;
+            c[13] = C.t_near;
+            c[14] = C.t_far;
+            c[15] = C.time;
+        }
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_cams, ctx->h_cams, (size_t)n_frames * 64,
+                                    hipMemcpyHostToDevice, s));
+        A.batch_cams = ctx->d_cams;
+        A.frame_pixels = frame_px;
+        A.frame_stride = stride;
+        A.n_pixels = split_px;
+    }
     ctx->last_spec = false;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(unsigned long long), s));
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
@@ -767,7 +808,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                 const uint64_t lim = (uint64_t)ctx->cfg.grid_waves_per_simd * ctx->n_simds / wpb;
                 if (lim < cap) cap = lim > 0 ? (uint32_t)lim : 1u;
             }
-            rvcp_static_split(A.n_pixels * n_frames, cap * wpb, A.n_simds, &waves, &chunk);
+            rvcp_static_split(split_px, cap * wpb, A.n_simds, &waves, &chunk);
             uint32_t blocks = (waves + wpb - 1) / wpb;
             if (blocks > cap) blocks = cap;
             if (blocks == 0) blocks = 1;
@@ -825,7 +866,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                                         spec_legacy ? (void *)jk->legacy : nullptr);
                 if (spec_legacy) ctx->last_spec = true;
             } else if (A.variant >= 3) {
-                const uint32_t n_surf = A.n_pixels * n_frames;
+                const uint32_t n_surf = split_px;
                 if (ctx->cap_surf < n_surf) {
                     (void)hipFree(ctx->d_surf);
                     ctx->d_surf = nullptr;
@@ -878,7 +919,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     ctx->last_variant = (trivial || A.n_pixels == 0) ? 0 : legacy ? 8
                       : A.accel ? (ctx->cfg.kernel_variant == 9 ? 9 : 7) : A.variant;
     if (ctx->last_spec && ctx->last_variant != 0) ctx->last_variant |= RVCP_VARIANT_SPECIALIZED;
-    ctx->last_pixels = (uint64_t)A.n_pixels * n_frames;     // stats cover the whole batch
+    ctx->last_pixels = (uint64_t)frame_px * n_frames;       // stats cover the whole batch
     ctx->last_spp = A.spp;
     ctx->last_shard_index = shard_index;
     ctx->last_shard_count = shard_count;

@@ -217,6 +217,13 @@ struct FrameArgs {
     // index of this frame's first pixel in the outputs (rvcp_render_frames_async: frame k of a
     // batch starts at k x the largest shard's pixels; 0 for a single frame)
     uint32_t pix_base;
+    // integrator mode 2 batches (one kernel over n frames; rvcp_render_frames_async): queue
+    // pixel p is pixel p % frame_pixels of frame p / frame_pixels, whose camera and time are
+    // the 16 floats at batch_cams + 16 * frame (FrameCam order: cam_pos, u, v, pos, base_len,
+    // t_near, t_far, time) and whose outputs start frame_stride pixels after the previous
+    // frame's; batch_cams == nullptr for a single frame
+    uint32_t frame_pixels, frame_stride;
+    const float *batch_cams;
     // debug build of the library only: per-wave {start, queue exhausted, end, iterations,
     // shader-clock start, shader-clock end}
     // of the path kernel, s_memrealtime ticks (100 MHz); nullptr otherwise

@@ -725,24 +725,44 @@ __device__ __forceinline__ void pixel_uv(const FrameArgs &A, uint32_t pix, float
     v_ = ((float)gy + 0.5f) / (float)A.height;
 }
 
+// A frame's camera constants and time seed: FrameArgs' own, or a batch frame's FrameCam
+// (FrameArgs::batch_cams, integrator mode 2 batches)
+struct Cam {
+    f3 cam_pos, u, v, pos;
+    float base_len, t_near, t_far, time;
+};
+__device__ __forceinline__ Cam cam_of(const FrameArgs &A) {
+    return Cam{ld3(A.cam_pos), ld3(A.u), ld3(A.v), ld3(A.pos), A.base_len, A.t_near, A.t_far, A.time};
+}
+__device__ __forceinline__ Cam cam_load(const float *__restrict__ c) {
+    return Cam{ld3(c), ld3(c + 3), ld3(c + 6), ld3(c + 9), c[12], c[13], c[14], c[15]};
+}
+
 // srand, :153-155
-__device__ __forceinline__ float pixel_seed(const FrameArgs &A, float u_, float v_) {
-    const float sa = fractf(pt_sinf(A.time) * 43758.5453f);
+__device__ __forceinline__ float pixel_seed(const Cam &C, float u_, float v_) {
+    const float sa = fractf(pt_sinf(C.time) * 43758.5453f);
     const float sb = fractf(pt_sinf(u_) * 22578.5453f);
     const float sc = fractf(pt_sinf(v_) * 114514.1919f);
     return fractf(sa + sb + sc);
 }
+__device__ __forceinline__ float pixel_seed(const FrameArgs &A, float u_, float v_) {
+    return pixel_seed(cam_of(A), u_, v_);
+}
 
 // sample_ray, :217-235 (frame constants from the host)
+__device__ __forceinline__ void primary_ray(const Cam &C, float u_, float v_, f3 &o, f3 &d,
+                                            float &tmin, float &tmax) {
+    const f3 uv_pos = add(add(C.pos, muls(C.u, u_ - 0.5f)), muls(C.v, v_ - 0.5f));
+    const f3 dv = sub(uv_pos, C.cam_pos);
+    const float t_coef = len(dv) / C.base_len;
+    o = C.cam_pos;
+    d = normalize(dv);
+    tmin = C.t_near * t_coef;
+    tmax = C.t_far * t_coef;
+}
 __device__ __forceinline__ void primary_ray(const FrameArgs &A, float u_, float v_, f3 &o, f3 &d,
                                             float &tmin, float &tmax) {
-    const f3 uv_pos = add(add(ld3(A.pos), muls(ld3(A.u), u_ - 0.5f)), muls(ld3(A.v), v_ - 0.5f));
-    const f3 dv = sub(uv_pos, ld3(A.cam_pos));
-    const float t_coef = len(dv) / A.base_len;
-    o = ld3(A.cam_pos);
-    d = normalize(dv);
-    tmin = A.t_near * t_coef;
-    tmax = A.t_far * t_coef;
+    primary_ray(cam_of(A), u_, v_, o, d, tmin, tmax);
 }
 
 // Hit record of face `best` from its FaceShade record (same arithmetic as hit_record).
@@ -772,6 +792,25 @@ __device__ __forceinline__ void start_pixel(const FrameArgs &A, uint32_t pix, fl
     seed = pixel_seed(A, u_, v_);
     ridx = 0.0f;
     primary_ray(A, u_, v_, o, d, tmin, tmax);
+}
+// The same for queue pixel `pix` of a mode-2 batch (FrameArgs::batch_cams): pixel
+// pix % frame_pixels of frame pix / frame_pixels, with that frame's camera and time.
+__device__ __forceinline__ void start_batch_pixel(const FrameArgs &A, uint32_t pix, float &seed,
+                                                  float &ridx, f3 &o, f3 &d, float &tmin,
+                                                  float &tmax) {
+    const uint32_t f = pix / A.frame_pixels;
+    const Cam C = cam_load(A.batch_cams + 16u * f);
+    float u_, v_;
+    pixel_uv(A, pix - f * A.frame_pixels, u_, v_);
+    seed = pixel_seed(C, u_, v_);
+    ridx = 0.0f;
+    primary_ray(C, u_, v_, o, d, tmin, tmax);
+}
+// Output index of queue pixel `pix` (frame f's outputs start f * frame_stride pixels in).
+__device__ __forceinline__ uint32_t batch_out(const FrameArgs &A, uint32_t pix) {
+    if (!A.batch_cams) return pix;
+    const uint32_t f = pix / A.frame_pixels;
+    return pix + f * (A.frame_stride - A.frame_pixels);
 }
 
 // NEE half of a surface event (:431-440 + sample_light_games101 :384-404): the light sample,
@@ -2741,7 +2780,7 @@ __device__ __forceinline__ void legacy_body(
                 acc = add(acc, col);
                 k += 1;
                 if (k >= A.spp) {
-                    store_acc(pix, divs_y(acc, sppf, inv_spp), out_lin);   // :819-821
+                    store_acc(batch_out(A, pix), divs_y(acc, sppf, inv_spp), out_lin);   // :819-821
                     need_pixel = true;
                     st = L_IDLE;
                 } else {                                            // next sample, cached hit
@@ -2758,7 +2797,8 @@ __device__ __forceinline__ void legacy_body(
                 queue_take(q, __ballot(need_pixel && !done), lane, A, counters, got, np);
                 if (got) {
                     pix = np;
-                    start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
+                    if (A.batch_cams) start_batch_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
+                    else start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
                     primary = true;
                     need_pixel = false;
                     k = 0;
@@ -2939,7 +2979,7 @@ __device__ __forceinline__ void legacy_body(
                     // miss / light: every sample returns this same color without touching the
                     // RNG; sum it SPP times in order (:816-818)
                     for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, col);
-                    store_acc(pix, divs_y(acc, sppf, inv_spp), out_lin);
+                    store_acc(batch_out(A, pix), divs_y(acc, sppf, inv_spp), out_lin);
                     need_pixel = true;
                     st = L_IDLE;
                 } else {
@@ -3233,11 +3273,14 @@ extern "C" int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRe
                            (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters);
         if (hipGetLastError() != hipSuccess) return -2;
     }
-    // the frame's UNORM8 store (no gamma in mode 2) from the linear colours
-    uint32_t tb = (args->n_pixels + rvcp::kToneBlock - 1) / rvcp::kToneBlock;
+    // the frame's UNORM8 store (no gamma in mode 2) from the linear colours (a batch's frames
+    // frame_stride pixels apart)
+    const uint32_t n_tone = args->batch_cams ? args->n_pixels / args->frame_pixels * args->frame_stride
+                                             : args->n_pixels;
+    uint32_t tb = (n_tone + rvcp::kToneBlock - 1) / rvcp::kToneBlock;
     if (tb > 8192u) tb = 8192u;
     hipLaunchKernelGGL(rvcp::tonemap_kernel, dim3(tb), dim3(rvcp::kToneBlock), 0, (hipStream_t)stream,
-                       out_lin, args->n_pixels, unorm_t, out_rgba);
+                       out_lin, n_tone, unorm_t, out_rgba);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

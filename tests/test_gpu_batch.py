@@ -2,7 +2,8 @@
 by frame, bit-identical to rendering each frame alone -- with a different time seed per frame
 (the reference's per-frame `time`, vulkan.rs:418-421), for whole frames and for shards whose
 rows differ (the padded slot layout), on the schedules that share one surface list; the stats
-cover the whole batch; other integrators / schedules refuse a batch."""
+cover the whole batch; integrator mode 2 batches too (per-frame cameras); the schedules
+without a pre-pass refuse a batch."""
 import numpy as np
 import pytest
 
@@ -73,11 +74,47 @@ def test_batch_bvh_equals_single_frames(cornell):
         assert np.array_equal(out[f].cpu().numpy(), singles[f]), f
 
 
+@pytest.mark.parametrize("scene,W,H,spp,k,n,spec", [
+    ("spheres", 128, 96, 3, 0, 1, 0),     # the sphere room, scene-specialised mode-2 kernel
+    ("spheres", 128, 96, 3, 0, 1, 1),     # ... the generic one
+    ("cornell", 150, 83, 4, 1, 3, 0),     # Cornell box, shard 1 of 3 (padded slots)
+])
+def test_mode2_batch_equals_single_frames(cornell, scene, W, H, spp, k, n, spec):
+    """Integrator mode 2 (ray_tracer.comp) batches: one kernel queues the frames' pixels frame
+    after frame, each frame with its own camera and time (FrameArgs::batch_cams); every frame
+    equals its single render."""
+    torch = pytest.importorskip("torch")
+    sc = cornell if scene == "cornell" else rvcp_amd.scene.sphere_scene()
+    slot = rvcp_amd.shard_rows(H, 0, n)
+    rows = rvcp_amd.shard_rows(H, k, n)
+    times = TIMES[:3]
+    pushes = [sc.push_constant(t) for t in times]
+    # a moved camera for the last frame: the batch carries per-frame cameras, not only times
+    cam = pushes[2]["camera"]
+    cam["position"][0] += 7.0
+    with rvcp_amd.RayTracer(spp=spp, integrator=1, specialize=spec) as rt:
+        rt.upload_scene(sc)
+        singles = []
+        for p in pushes:
+            o = torch.zeros((rows, W), dtype=torch.int32, device="cuda")
+            rt.render_shard_async(p, W, H, k, n, o.data_ptr())
+            singles.append((o, rt.sync_stats()))
+        out = torch.zeros((3, slot, W), dtype=torch.int32, device="cuda")
+        rt.render_frames_async(pushes, W, H, k, n, out.data_ptr())
+        st = rt.sync_stats()
+        torch.cuda.synchronize()
+    for f, (o, _) in enumerate(singles):
+        assert np.array_equal(out[f, :rows].cpu().numpy(), o.cpu().numpy()), f
+    assert not np.array_equal(singles[0][0].cpu().numpy(), singles[2][0].cpu().numpy())
+    assert int(st["samples"]) == 3 * rows * W * spp
+    assert int(st["traversals"]) == sum(int(x["traversals"]) for _, x in singles)
+
+
 def test_batch_refused_where_unsupported(cornell):
     torch = pytest.importorskip("torch")
     out = torch.zeros((2, 32, 32), dtype=torch.int32, device="cuda")
     push = [cornell.push_constant(1.0), cornell.push_constant(2.0)]
-    for kw in (dict(integrator=1), dict(kernel_variant=2)):
+    for kw in (dict(kernel_variant=2), dict(kernel_variant=1)):
         with rvcp_amd.RayTracer(spp=2, **kw) as rt:
             rt.upload_scene(cornell)
             with pytest.raises(rvcp_amd.abi.RvcpError) as e:
