@@ -75,6 +75,7 @@ for s in $STEPS; do
         tlc3) tl tlc3 40 ;;
         tlc2) tl tlc2 40 --size 384 --spp 10 ;;
         rehearse8c4) run rehearse8c4 400 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 --workload c4 --steps 5 --warmup 1 ;;
+        rehearse8c4b) run rehearse8c4b 500 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29539 bench.py --gpus 8 --workload c4 --steps 20 --warmup 4 ;;
         rehearse2) run rehearse2 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
         frames) run frames 300 python tools/frames.py --frames 20 ;;
         poolab) run poolab 600 bash tools/sched_ab.sh "3 9" "--frames 20" "--size 384 --spp 10 --frames 40" "--size 2048 --spp 64 --frames 6" "--size 128 --spp 30 --frames 40" ;;
