@@ -178,6 +178,17 @@ def test_create_rejects_bad_config_without_device():
         assert L.rvcp_create(abi.ptr(bad), ctypes.byref(h)) == abi.RVCP_E_INVALID, (v, accel)
 
 
+def test_render_entry_points_reject_a_null_context():
+    """The render entry points (including the frame batch) return RVCP_E_INVALID for a NULL
+    context without touching a device."""
+    L = abi.load()
+    p = ctypes.c_void_p(1)
+    assert L.rvcp_render_frames_async(None, p, 3, 64, 64, 0, 1, p, None, None) == abi.RVCP_E_INVALID
+    assert L.rvcp_render_shard_async(None, p, 64, 64, 0, 1, p, None, None) == abi.RVCP_E_INVALID
+    assert L.rvcp_render_async(None, p, 64, 64, p, None, None) == abi.RVCP_E_INVALID
+    assert L.rvcp_sync_stats(None, None) == abi.RVCP_E_INVALID
+
+
 def test_shard_rows_library_matches_python():
     L = abi.load()
     for H in (1, 7, 8, 9, 83, 1024, 1448, 2896):
