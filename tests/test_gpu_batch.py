@@ -172,3 +172,29 @@ def test_batch_with_rccl_gathers(cornell):
     finally:
         for rt in rts:
             rt.close()
+
+
+def test_eight_shard_batches_assemble(cornell):
+    """The N=8 bench pattern with batches on one GPU: each of 8 shards renders a batch of 3
+    frames (different seeds) in one call, the slots of each frame are gathered (here: copied
+    into the gather layout) and assembled on the device; every assembled frame equals the
+    1-shard render of its seed."""
+    torch = pytest.importorskip("torch")
+    W, H, n, spp = 160, 203, 8, 2
+    times = TIMES[:3]
+    pushes = [cornell.push_constant(t) for t in times]
+    slot = rvcp_amd.shard_rows(H, 0, n)
+    with rvcp_amd.RayTracer(spp=spp) as rt:
+        rt.upload_scene(cornell)
+        refs = [rt.render(W, H, t) for t in times]
+        shards = torch.zeros((n, len(times), slot, W), dtype=torch.int32, device="cuda")
+        for k in range(n):
+            rt.render_frames_async(pushes, W, H, k, n, shards[k].data_ptr())
+            rt.sync_stats()
+        frames = torch.zeros((len(times), H, W), dtype=torch.int32, device="cuda")
+        for j in range(len(times)):
+            gathered = shards[:, j].contiguous()               # (n, slot, W): the gather layout
+            rt.assemble_frame_async(gathered.data_ptr(), slot, W, H, n, frames[j].data_ptr())
+        torch.cuda.synchronize()
+    for j in range(len(times)):
+        assert np.array_equal(frames[j].cpu().numpy().view(np.uint8).reshape(H, W, 4), refs[j]), j
