@@ -281,18 +281,20 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
         0.232 -> 0.208 ms (batches of 2: 3.24 / 3.56 / 0.226); deeper batches for smaller
         launches (r03zx_batch_sweep3.log): the N=8 share 3.42 / 3.37 / 3.33 ms with 3 / 4 / 6
         frames, C2 0.195 / 0.173 / 0.162 / 0.158 ms with 3 / 6 / 10 / 16; C5 with the BVH
-        97.6 -> 92.0 ms with 3 (profiles/r03zw_bvh_batch_ab.log);
+        97.6 -> 92.0 ms with 3 (profiles/r03zw_bvh_batch_ab.log); and 2 for larger frames
+        (r03zze_batch_sweep4.log): the N=2 share of C4 13.47 -> 13.29-13.36 ms, the whole C4
+        frame 26.28-26.30 -> 26.13-26.15 ms;
       - mode 2 (no pre-pass, no batches), up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD --
         mode 2 on the C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms;
-      - larger frames: full grid, one frame per launch, 2 in flight (3 in mode 2: one kernel per
-        frame, no pre-pass): C4 on one GPU 26.35 ms (batches of 2: 26.16, 3 in flight 26.50);
+      - larger mode-2 frames and meshes: full grid, one frame per launch, 2 in flight (3 in
+        mode 2: one kernel per frame, no pre-pass);
       - other small frames (below 4 Msamples): 4 in flight (C2 0.59/0.32/0.27/0.33 ms for
         1/2/3/4 in flight, profiles/r02_fif_sweep.log).
     Contexts beyond the hardware queues minus one contend for queues."""
-    mid = pixels <= 1536 * 1024 or pixels * spp < (4 << 20)
-    if not legacy and (small_scene or accel == "bvh") and mid:
-        # about 3 Mpixel per launch, at most 16 frames, and at least 4 launches in the run
-        batch = max(1, min(-(-3 * 1024 * 1024 // max(1, pixels)), 16,
+    if not legacy and (small_scene or accel == "bvh"):
+        # about 3 Mpixel per launch and at least 2 frames, at most 16 frames, and at least 4
+        # launches in the run
+        batch = max(1, min(max(2, -(-3 * 1024 * 1024 // max(1, pixels))), 16,
                            steps // 4 if steps else 16))
         fif, grid = 2, 0
     elif pixels * spp < (4 << 20):
@@ -601,9 +603,11 @@ def main():
         # (outside timing); the same frame rendered by this GPU alone, pipelined the way a
         # one-GPU run of that frame is (auto_pipeline for the whole frame, unless the command
         # line fixed fif / grid for both), is the single-GPU reference for the speedup
-        fif1, grid1, _ = auto_pipeline(W * H, spp, legacy, small_scene, hw_queues, args.accel)
+        fif1, grid1, batch1 = auto_pipeline(W * H, spp, legacy, small_scene, hw_queues,
+                                            args.accel, 3 * 4 * 2)
         fif1 = args.frames_in_flight or fif1
         grid1 = args.grid_waves if args.grid_waves >= 0 else (grid1 if fif1 >= 3 else 0)
+        batch1 = args.batch or batch1
         if (fif1, grid1) == (fif, grid_waves):
             rts1, own1 = rts, False
         else:
@@ -611,10 +615,16 @@ def main():
             for r in rts1:
                 r.upload_scene(sc)
             own1 = True
-        singles = [torch.zeros((H, W), dtype=torch.int32, device=dev) for _ in range(fif1)]
-        n1 = 3 * fif1
+        singles = [torch.zeros((batch1, H, W), dtype=torch.int32, device=dev) for _ in range(fif1)]
+
+        def render1(i):
+            if batch1 == 1:
+                rts1[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
+            else:
+                rts1[i].render_frames_async([push] * batch1, W, H, 0, 1, singles[i].data_ptr())
+        n1 = 3 * fif1                                      # launches of batch1 frames
         for i in range(fif1):                              # warm-up, one per context
-            rts1[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
+            render1(i)
         for i in range(fif1):
             rts1[i].sync_stats()
         torch.cuda.synchronize()
@@ -624,14 +634,14 @@ def main():
             i = f % fif1
             if busy[i]:
                 rts1[i].sync_stats()
-            rts1[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
+            render1(i)
             busy[i] = True
         for i in range(fif1):
             if busy[i]:
                 rts1[i].sync_stats()
         torch.cuda.synchronize()
-        one_gpu_ms = (time.perf_counter() - ts) * 1000.0 / n1
-        frame_check = bool(torch.equal(singles[0], frame))
+        one_gpu_ms = (time.perf_counter() - ts) * 1000.0 / (n1 * batch1)
+        frame_check = bool(torch.equal(singles[0][0], frame))
         if own1:
             for r in rts1:
                 r.close()
@@ -742,6 +752,7 @@ def main():
             out["config"]["one_gpu_ms"] = round(one_gpu_ms, 4)
             out["config"]["one_gpu_frames_in_flight"] = fif1
             out["config"]["one_gpu_grid_waves_per_simd"] = grid1
+            out["config"]["one_gpu_frames_per_launch"] = batch1
             out["config"]["speedup_vs_one_gpu_same_frame"] = round(one_gpu_ms / ms_per_step, 3)
             if rehearsal:
                 out["config"]["physical_gpus"] = 1
