@@ -401,7 +401,9 @@ def main():
     # (small frames, 8 hardware queues: C2 4 in flight 0.269 ms vs 3 in flight 0.284 ms,
     # profiles/r02_hwq_fif_sweep.log; C3 2 and 3 equal)
     small_scene = args.accel == "none" and not wl["extra_tris"]
-    fif_auto, grid_auto, batch_auto = auto_pipeline(W * rvcp_amd.shard_rows(H, rank, world), spp,
+    # from the largest shard's size, so that every rank picks the same pipeline: the contexts'
+    # communicators must see the ranks' gathers in the same order
+    fif_auto, grid_auto, batch_auto = auto_pipeline(W * rvcp_amd.shard_rows(H, 0, world), spp,
                                                     legacy, small_scene, hw_queues, args.accel,
                                                     args.steps)
     fif = 1 if rehearsal else (args.frames_in_flight or fif_auto)
