@@ -46,7 +46,7 @@ for s in $STEPS; do
         benchall) run bench_c3 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline && run bench_c2 300 python bench.py --workload c2 --steps 100 --warmup 10 --no-cpu-baseline && run bench_c4 300 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         benchc4) run bench_c4 300 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         benchc5) run bench_c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
-        benchc5bvh) run bench_c5_bvh 600 python bench.py --workload c5 --steps 3 --warmup 1 --accel bvh --no-cpu-baseline ;;
+        benchc5bvh) run bench_c5_bvh 600 python bench.py --workload c5 --steps 12 --warmup 3 --accel bvh --no-cpu-baseline ;;
         benchc3m2) run bench_c3m2 300 python bench.py --workload c3m2 --steps 20 --warmup 3 --no-cpu-baseline ;;
         benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 --no-cpu-baseline ;;
         # the headline command under rocprofv3: default frames in flight, and one frame in flight
