@@ -284,6 +284,8 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
         97.6 -> 92.0 ms with 3 (profiles/r03zw_bvh_batch_ab.log); and 2 for larger frames
         (r03zze_batch_sweep4.log): the N=2 share of C4 13.47 -> 13.29-13.36 ms, the whole C4
         frame 26.28-26.30 -> 26.13-26.15 ms;
+      - runs with too few steps for a batch (fewer than 8): frames up to 1.5 Mpixel as mode 2
+        below;
       - mode 2 (no pre-pass, no batches), up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD --
         mode 2 on the C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms;
       - larger mode-2 frames and meshes: full grid, one frame per launch, 2 in flight (3 in
@@ -297,6 +299,8 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
         batch = max(1, min(max(2, -(-3 * 1024 * 1024 // max(1, pixels))), 16,
                            steps // 4 if steps else 16))
         fif, grid = 2, 0
+        if batch == 1 and pixels <= 1536 * 1024:
+            fif, grid = 3, 3        # too few steps for batches: single frames, smaller grid
     elif pixels * spp < (4 << 20):
         fif, grid, batch = 4, 0, 1
     elif small_scene and pixels <= 1536 * 1024:

@@ -48,7 +48,8 @@ def test_auto_pipeline():
     assert ap(2048 * 2048, 64, False, True, "4", "none", 4) == (2, 0, 1)           # 4 steps
     assert ap(384 * 384, 10, False, True, "4", "none", 200) == (2, 0, 16)          # C2
     assert ap(384 * 384, 10, False, True, "4", "none", 20) == (2, 0, 5)
-    assert ap(384 * 384, 10, False, True, "4", "none", 3) == (2, 0, 1)
+    assert ap(384 * 384, 10, False, True, "4", "none", 3) == (3, 3, 1)             # too few steps
+    assert ap(1024 * 1024, 30, False, True, "4", "none", 5) == (3, 3, 1)
     assert ap(1024 * 1024, 30, True, True, "4", "none", 20) == (3, 3, 1)           # mode 2, C3 frame
     assert ap(1024 * 1024, 5, True, True, "4", "none", 20) == (3, 3, 1)            # sphere room
     assert ap(384 * 384, 5, True, True, "8", "none", 20) == (4, 0, 1)              # small mode-2 frame
