@@ -25,6 +25,9 @@ Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
       1024x1024 at its SPP=5 (not a BASELINE config; reported for coverage).
   c3m2: the C3 frame (Cornell 1024x1024 SPP=30) through integrator mode 2 (ray_tracer.comp,
       the shader north_star names) instead of the games101 branch the current host binds.
+  c3rot: the C3 frame of the Cornell box turned off-axis with its camera (scene.rotated_scene):
+      no exact-zero triangle component is left for the scene-specialised scan to drop.
+  c3gen: the C3 frame with the generic scan (rvcp_config_t.specialize = OFF).
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the path-tracing kernel,
 >99% of the frame's GPU time), whose bound is FP32 VALU issue:
@@ -67,7 +70,31 @@ FLOP_PER_SPHERE_TEST = 25      # ray_tracer.comp:300-321
 # C2 row (README.md:22, 51 fps), as Msamples/s
 REFERENCE_MSAMPLES = {"c3": 94.4, "c2": 75.2}
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (spec)
+# VALU issue: 1,024 SIMDs (256 CUs x 4) issuing one wave64 instruction per 2 cycles
+# (MI355X_MICROARCH.md) at the shader clock measured under this load, 2.29 GHz (in-kernel
+# s_memtime / s_memrealtime stamps of the C3 path kernel)
+N_SIMDS = 1024
+VALU_ISSUE_PER_CLK = 0.5
+SHADER_CLOCK_GHZ = 2.29
 FLOP_PER_TEST = 52
+# the time seed of frame 0 (the tests' fixed seed); frame f renders with
+# TIME0 + f, as the reference re-stamps `time` every frame (vulkan.rs:418-421)
+TIME0 = 123.0
+
+
+BASELINE_METRIC = "Msamples/sec (pixels*SPP/s) + frame ms, Cornell Box 1024^2 SPP=30"
+
+
+def metric_name(wl, world):
+    """BASELINE.json's metric for the headline (C3 on one GPU); other workloads name their own
+    frame, and N > 1 names the GPU count the frame is sharded over."""
+    if wl["workload"] == "cornell_1024sq_spp30" and world == 1:
+        return BASELINE_METRIC
+    what = f"{wl['W']}^2 SPP={wl['spp']}, {wl['workload']}"
+    if world > 1:
+        what += (f", frame sharded over {world} GPUs" if wl["scaling"] == "strong" else
+                 f", {world} GPUs (weak scaling)")
+    return f"Msamples/sec (pixels*SPP/s) + frame ms, {what}"
 
 
 def workload(name, n_gpus):
@@ -91,25 +118,36 @@ def workload(name, n_gpus):
     if name == "spheres":
         return dict(workload="spheres_mode2_1024sq_spp5", W=1024, H=1024, spp=5, extra_tris=0,
                     scaling="strong", integrator=1, scene="spheres")
+    if name == "c3rot":
+        return dict(workload="cornell_rotated_1024sq_spp30", W=1024, H=1024, spp=30, extra_tris=0,
+                    scaling="strong", rotate=True)
+    if name == "c3gen":
+        return dict(workload="cornell_generic_scan_1024sq_spp30", W=1024, H=1024, spp=30,
+                    extra_tris=0, scaling="strong", specialize_off=True)
     if name == "c3m2":
         return dict(workload="cornell_mode2_1024sq_spp30", W=1024, H=1024, spp=30, extra_tris=0,
                     scaling="strong", integrator=1, scene="cornell")
     raise SystemExit(f"unknown workload {name}")
 
 
-def load_valu_busy(workload_name, kernel_name):
+def load_valu_busy(workload_name, kernel_name, want_insts=False):
     """VALU issue utilisation of the dominant kernel from the newest committed SQ PMC summary:
-    (busy at 2 cycles per wave64 instruction, fraction of the measured issue peak)."""
+    (busy at 2 cycles per wave64 instruction, fraction of the measured issue peak), and with
+    want_insts also (wave64 VALU instructions per launch, summary file)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_valu_{workload_name}.json")))
+    none = (None, None, None, None) if want_insts else (None, None)
     if not files:
-        return None, None
+        return none
     with open(files[-1]) as f:
         d = json.load(f)
     for name, k in d.get("kernels", {}).items():
         if kernel_name in name:
+            if want_insts:
+                return (k.get("valu_busy"), k.get("issue_frac"), k.get("valu_insts"),
+                        os.path.relpath(files[-1], ROOT))
             return k.get("valu_busy"), k.get("issue_frac")
-    return None, None
+    return none
 
 
 def load_traffic(workload_name, kernel_name):
@@ -177,29 +215,30 @@ def cpu_baseline(sc, cfg_kw, W, H, threads):
                   spheres=sc.aligned_spheres())
     push = sc.push_constant(123.0)
     common = dict(unit="Msamples/s", cores=threads, kind="port",
-                  implementation="C port of the shader (oracle/rvcp_oracle.c); the image has no "
-                                 "Rust toolchain, so not a Rust re-execution",
+                  implementation="C port of the shader (oracle/rvcp_oracle.c, gcc -O3 "
+                                 "-ffp-contract=off); the image has no Rust toolchain, so not a "
+                                 "Rust re-execution",
                   host_threads=host_threads(), cgroup_cpu_quota=cgroup_cpu_quota(),
                   cpu=cpu_model())
     O.render(arrays, push, cfg, W, H, rect=(0, H // 2, min(W, 64), 1), threads=threads,
-             want_linear=False)                                   # warm-up (page-in, threads)
+             want_linear=False, o3=True)                                   # warm-up (page-in, threads)
     if len(arrays["faces"]) > 1000:          # C5 on CPU: 128^2 SPP=1 frame only
         t0 = time.perf_counter()
         O.render(arrays, push, rvcp_amd.abi.make_config(**dict(cfg_kw, spp=1)), 128, 128,
-                 threads=threads, want_linear=False)
+                 threads=threads, want_linear=False, o3=True)
         dt = time.perf_counter() - t0
         return dict(value=round(128 * 128 / dt / 1e6, 4), sample="128x128 SPP=1 frame of the same scene",
                     seconds=round(dt, 3), **common)
     # the whole frame on `threads` threads (a few seconds), then a single-thread figure on
     # every 64th row
     t0 = time.perf_counter()
-    O.render(arrays, push, cfg, W, H, threads=threads, want_linear=False)
+    O.render(arrays, push, cfg, W, H, threads=threads, want_linear=False, o3=True)
     dt = time.perf_counter() - t0
     samples = W * H * cfg_kw["spp"]
     rows1 = list(range(0, H, 64 if H >= 256 else 8))
     t1 = time.perf_counter()
     for y in rows1:
-        O.render(arrays, push, cfg, W, H, rect=(0, y, W, 1), threads=1, want_linear=False)
+        O.render(arrays, push, cfg, W, H, rect=(0, y, W, 1), threads=1, want_linear=False, o3=True)
     dt1 = time.perf_counter() - t1
     return dict(value=round(samples / dt / 1e6, 4),
                 sample=f"the full {W}x{H} SPP={cfg_kw['spp']} frame on {threads} threads",
@@ -217,7 +256,8 @@ def _all_ok(dist, ok, why):
     return (not bad), (None if not bad else "; ".join(str(w) for w in bad))
 
 
-def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe=None):
+def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe_render=None,
+                     probe_gather=None):
     """Decide, on every rank alike, whether the frame moves over RCCL or through host memory.
 
     1. every rank creates RCCL ids (a local call that loads librccl: a rank without a usable
@@ -225,7 +265,10 @@ def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe=None):
        the control plane (gloo);
     2. rank 0's ids are broadcast and every rank joins each communicator (init_comm(i, id));
        agreed;
-    3. `probe()` (a tiny render + gather + check) on every rank; agreed.
+    3. `probe_render()` (a tiny frame's render on every context, local); agreed -- so that no
+       rank enters the collective gather while another rank's render already failed (its
+       peers would wait in the gather forever);
+    4. `probe_gather()` (the tiny frame's RCCL gather + rank 0's check); agreed.
     Any failure on any rank sends every rank to the host gather, with the reasons.  (A rank
     whose ncclCommInitRank fails while the others succeed leaves them blocked inside RCCL
     itself; such asymmetric init failures are outside what a blocking init can recover.)
@@ -248,11 +291,13 @@ def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe=None):
     ok, reason = _all_ok(dist, why is None, why)
     if not ok:
         return "host", reason
-    if probe is not None:
+    for stage, fn in (("probe render", probe_render), ("gather probe", probe_gather)):
+        if fn is None:
+            continue
         try:
-            probe()
+            fn()
         except Exception as e:          # noqa: BLE001
-            why = f"rank {rank}: gather probe: {e!r}"
+            why = f"rank {rank}: {stage}: {e!r}"
         ok, reason = _all_ok(dist, why is None, why)
         if not ok:
             return "host", reason
@@ -314,12 +359,38 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
     return fif, grid, batch
 
 
+def free_port():
+    """A TCP port on 127.0.0.1 that is free right now (for the ranks' rendezvous)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n, argv, script=None):
+    """`bench.py --gpus N` (N > 1) started as a plain process: start the N ranks as a
+    torch.distributed.run child (one process per GPU, rendezvous on 127.0.0.1) and return its
+    exit status -- non-zero when any rank failed.  This process never imports torch, so it
+    never touches the GPU (no HIP initialisation before the ranks start, and no exec from a
+    process that holds the GPU); the ranks inherit stdout, so rank 0's one JSON line is this
+    command's output."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           script or os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    print(f"bench: self-launch of {n} ranks (parent pid {os.getpid()}, "
+          f"torch imported: {'torch' in sys.modules})", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "spheres", "c3m2"],
+    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "spheres", "c3m2", "c3rot", "c3gen"],
                     help="default: c3 at N=1 (headline), c4 at N>1 (BASELINE's 8-GPU config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -348,6 +419,11 @@ def main():
                          "(roofline.per_launch; 0 = skip)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's form `python bench.py --gpus N`: start the ranks ourselves, before
+        # anything here touches the GPU
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+
     # Hardware queues per process: HIP's default is 4; with 4 frames in flight on small frames
     # (C2) the contexts' streams then share queues and serialise.  8 queues let C2 take a fourth
     # frame: 0.284 -> 0.269 ms (profiles/r02_hwq_fif_sweep.log).  Only when the variable is unset
@@ -363,9 +439,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} launched with WORLD_SIZE={world}")
     # Rehearsal (RVCP_BENCH_REHEARSAL=1): every rank on device 0 and the gather through host
     # memory over gloo (RCCL refuses two ranks on one GPU), to exercise the N>1 code path on
     # a 1-GPU box.  Never used for reported numbers.
@@ -386,7 +461,11 @@ def main():
     sc = rvcp_amd.scene.sphere_scene() if wl.get("scene") == "spheres" else rvcp_amd.Scene.default()
     if wl["extra_tris"]:
         sc = rvcp_amd.scene.with_random_triangles(sc, wl["extra_tris"])
+    if wl.get("rotate"):
+        sc = rvcp_amd.scene.rotated_scene(sc)
     cfg_kw = dict(spp=spp, device=local_rank)
+    if wl.get("specialize_off"):
+        cfg_kw["specialize"] = 1
     if legacy:
         cfg_kw["integrator"] = 1
     if args.accel == "bvh":
@@ -422,7 +501,7 @@ def main():
     for r in rts[1:]:
         r.upload_scene(sc)               # (the compiled module is cached per process)
     rt = rts[0]
-    push = sc.push_constant(123.0)
+    push = sc.push_constant(TIME0)
     n_faces = len(sc.mesh.aligned_faces())
     n_spheres = len(sc.spheres) if legacy else 0
 
@@ -442,20 +521,25 @@ def main():
     # otherwise every rank gathers through host memory over gloo, labelled in the JSON line.
     gather_mode, gather_error = ("none", None) if world == 1 else ("host", "rehearsal")
     if world > 1 and not rehearsal:
-        def probe():
-            # a tiny frame (8 rows per rank) rendered, gathered and checked against rank 0's own
-            # render of it, on every context
-            pW, pH = 16, 8 * world
-            p_slot = rvcp_amd.shard_rows(pH, 0, world)
-            p_shard = torch.zeros((p_slot, pW), dtype=torch.int32, device=dev)
+        # a tiny frame (8 rows per rank) rendered on every context, gathered and checked
+        # against rank 0's own render of it
+        pW, pH = 16, 8 * world
+        p_slot = rvcp_amd.shard_rows(pH, 0, world)
+        p_shards = [torch.zeros((p_slot, pW), dtype=torch.int32, device=dev) for _ in rts]
+
+        def probe_render():
+            for r, p_shard in zip(rts, p_shards):
+                r.render_shard_async(push, pW, pH, rank, world, p_shard.data_ptr())
+                r.sync_stats()
+            torch.cuda.synchronize()
+
+        def probe_gather():
             p_gat = torch.zeros((world, p_slot, pW), dtype=torch.int32, device=dev) if rank == 0 else None
             p_frame = torch.zeros((pH, pW), dtype=torch.int32, device=dev) if rank == 0 else None
-            for r in rts:
-                r.render_shard_async(push, pW, pH, rank, world, p_shard.data_ptr())
+            for r, p_shard in zip(rts, p_shards):
                 r.gather_frame_async(p_shard.data_ptr(), pW, pH,
                                      p_gat.data_ptr() if rank == 0 else 0,
                                      p_frame.data_ptr() if rank == 0 else 0)
-                r.sync_stats()
                 r.gather_wait()
                 if rank == 0:
                     ref = torch.zeros((pH, pW), dtype=torch.int32, device=dev)
@@ -467,21 +551,36 @@ def main():
             torch.cuda.synchronize()
         gather_mode, gather_error = negotiate_gather(
             dist, rank, fif, rvcp_amd.rccl_unique_id,
-            lambda i, uid: rts[i].rccl_init(uid, world, rank), probe)
+            lambda i, uid: rts[i].rccl_init(uid, world, rank), probe_render, probe_gather)
     host_gather = world > 1 and gather_mode != "rccl"
     torch.cuda.synchronize()
     pending = [0] * fif                 # frames in flight on each context
     gather_ms = []
+    # Every frame has its own time seed, as the reference re-stamps `time` in the push
+    # constant of every frame it submits (vulkan.rs:418-421): frame f (warm-up frames first,
+    # then the timed ones, the same numbering on every rank) renders with time TIME0 + f, so
+    # no two frames of the run share an RNG stream.  slot_time[i][j]: the seed of the frame in
+    # context i's output slot j.
+    n_frames_run = [0]
+    slot_time = [[None] * batch for _ in range(fif)]
+    done_t = []                         # (host time a call's frames were complete, frames)
+
+    def next_pushes(i, nb):
+        ts_ = [TIME0 + float(n_frames_run[0] + j) for j in range(nb)]
+        n_frames_run[0] += nb
+        slot_time[i][:nb] = ts_
+        return [sc.push_constant(t) for t in ts_]
 
     def enqueue(i, nb):
         """Enqueue nb frames (one call) on context i's own stream (stream 0 = its stream)."""
         r, shard_buf, gat_flat = rts[i], shard_bufs[i], gat_flats[i]
         out = frames[i] if world == 1 else shard_buf
         k, n = (0, 1) if world == 1 else (rank, world)
+        pushes = next_pushes(i, nb)
         if batch == 1:
-            r.render_shard_async(push, W, H, k, n, out.data_ptr())
+            r.render_shard_async(pushes[0], W, H, k, n, out.data_ptr())
         else:
-            r.render_frames_async([push] * nb, W, H, k, n, out.data_ptr())
+            r.render_frames_async(pushes, W, H, k, n, out.data_ptr())
         if world == 1 or host_gather:
             return
         # RCCL gather + device assembly of each frame, enqueued behind the render without a
@@ -505,6 +604,7 @@ def main():
                     rts[i].assemble_frame_async(gat_flats[i].data_ptr(), slot, W, H, world,
                                                 frames[i][j].data_ptr())
                     torch.cuda.synchronize()
+        done_t.append((time.perf_counter(), nb))
         return st
 
     def step(c, nb):
@@ -522,7 +622,13 @@ def main():
         """n frames as calls of `batch` frames (the last one shorter)."""
         return [batch] * (n // batch) + ([n % batch] if n % batch else [])
 
-    for c, nb in enumerate(calls(args.warmup)):
+    # Warm-up: at least one full batch on every context, so that each context's surface list,
+    # accumulator and camera buffers have their full size before timing (growing one inside the
+    # timed region frees device memory, which synchronises the device and drains the other
+    # context's frames)
+    warm = max(args.warmup, fif * batch)
+    warm = -(-warm // batch) * batch
+    for c, nb in enumerate(calls(warm)):
         step(c, nb)
     drain()
     gather_ms.clear()
@@ -532,15 +638,16 @@ def main():
     torch.cuda.synchronize()
     stats = []
     t0 = time.perf_counter()
-    step_ms = []
+    done_t.clear()
+    done_t.append((t0, 0))
     for c, nb in enumerate(calls(args.steps)):
-        ts = time.perf_counter()
         st = step(c, nb)
-        step_ms.append((time.perf_counter() - ts) * 1000.0 / nb)
         if st is not None:
             stats.append(st)
     stats += drain()
-    frame = frames[0][0] if rank == 0 else None
+    # (a copy: the post-timing passes below render into the same buffers)
+    frame = frames[0][0].clone() if rank == 0 else None
+    frame_time = slot_time[0][0]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -557,6 +664,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    intervals = [(b[0] - a[0]) * 1000.0 / b[1] for a, b in zip(done_t, done_t[1:]) if b[1]]
     samples_total = W * H * spp * args.steps
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -570,9 +678,9 @@ def main():
         rt_iso = rt if grid_waves == 0 else rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0))
         if rt_iso is not rt:
             rt_iso.upload_scene(sc)
-        for _ in range(max(1, min(args.launch_pass, args.steps))):
+        for f in range(max(1, min(args.launch_pass, args.steps))):
             tl = time.perf_counter()
-            rt_iso.render_shard_async(push, W, H, rank, world,
+            rt_iso.render_shard_async(sc.push_constant(TIME0 + float(f)), W, H, rank, world,
                                       (frames[0] if world == 1 else shard_bufs[0]).data_ptr())
             iso_ms.append(float(rt_iso.sync_stats()["main_kernel_ms"]))
             latency_ms.append((time.perf_counter() - tl) * 1000.0)
@@ -599,7 +707,12 @@ def main():
     algo_gbs = bytes_per_launch / wall_s / 1e9
     kname = rvcp_amd.abi.KERNEL_NAMES.get(variant, "?")
     traffic, traffic_src = load_traffic(wl["workload"], kname)
-    valu_busy, valu_issue_frac = load_valu_busy(wl["workload"], kname)
+    valu_busy, valu_issue_frac, valu_insts, valu_src = load_valu_busy(wl["workload"], kname,
+                                                                      want_insts=True)
+    # the committed PMC pass's VALU instructions per frame (one frame per launch there) over
+    # the issue slots of one timed frame: how close the wall clock is to the issue floor
+    valu_wall = (None if not valu_insts or world != 1 else
+                 valu_insts / (ms_per_step * 1e-3 * SHADER_CLOCK_GHZ * 1e9 * N_SIMDS * VALU_ISSUE_PER_CLK))
     bvh = args.accel == "bvh"
     iso_s = (float(np.mean(iso_ms)) / 1000.0) if iso_ms else None
 
@@ -623,14 +736,16 @@ def main():
             own1 = True
         singles = [torch.zeros((batch1, H, W), dtype=torch.int32, device=dev) for _ in range(fif1)]
 
-        def render1(i):
-            if batch1 == 1:
-                rts1[i].render_shard_async(push, W, H, 0, 1, singles[i].data_ptr())
+        def render1(i, f0, nb=batch1):
+            # frames f0 .. f0 + nb - 1 of the one-GPU run, each with its own time seed
+            pushes = [sc.push_constant(TIME0 + float(f0 + j)) for j in range(nb)]
+            if nb == 1:
+                rts1[i].render_shard_async(pushes[0], W, H, 0, 1, singles[i].data_ptr())
             else:
-                rts1[i].render_frames_async([push] * batch1, W, H, 0, 1, singles[i].data_ptr())
+                rts1[i].render_frames_async(pushes, W, H, 0, 1, singles[i].data_ptr())
         n1 = 3 * fif1                                      # launches of batch1 frames
         for i in range(fif1):                              # warm-up, one per context
-            render1(i)
+            render1(i, 0)
         for i in range(fif1):
             rts1[i].sync_stats()
         torch.cuda.synchronize()
@@ -640,13 +755,18 @@ def main():
             i = f % fif1
             if busy[i]:
                 rts1[i].sync_stats()
-            render1(i)
+            render1(i, f * batch1)
             busy[i] = True
         for i in range(fif1):
             if busy[i]:
                 rts1[i].sync_stats()
         torch.cuda.synchronize()
         one_gpu_ms = (time.perf_counter() - ts) * 1000.0 / (n1 * batch1)
+        # the check: the assembled frame of context 0's slot 0 against this GPU's render of
+        # the same time seed
+        rts1[0].render_shard_async(sc.push_constant(frame_time), W, H, 0, 1, singles[0].data_ptr())
+        rts1[0].sync_stats()
+        torch.cuda.synchronize()
         frame_check = bool(torch.equal(singles[0][0], frame))
         if own1:
             for r in rts1:
@@ -668,7 +788,7 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "Msamples/sec (pixels*SPP/s) + frame ms, Cornell Box 1024^2 SPP=30",
+            "metric": metric_name(wl, world),
             "value": round(value, 2),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -676,24 +796,31 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(1000.0 / ms_per_step, 2),
-            "frame_ms_median": round(float(np.median(step_ms)), 4),
+            # median of the intervals between consecutive calls' completions (host clock),
+            # per frame of the later call: the pipelined frame interval, not a frame latency
+            # (that is config.frame_latency_ms_alone)
+            "frame_interval_ms_median": round(float(np.median(intervals)), 4) if intervals else None,
             "higher_is_better": True,
             "scaling": wl["scaling"],
             # the reference's published rows are single-GPU (RTX 3060) C3 / C2 frames
             "vs_baseline": (round(value / REFERENCE_MSAMPLES[wname], 2)
                             if world == 1 and wname in REFERENCE_MSAMPLES else None),
             "dtype": "f32",
-            "data": ("synthetic (the reference's deprecated sphere-room scene, integrator mode 2, "
-                     "fixed time seed 123.0)" if wl.get("scene") == "spheres" else
-                     "synthetic (the reference's built-in Cornell box scene, integrator mode 2, "
-                     "fixed time seed 123.0)" if legacy else
-                     "synthetic (the reference's built-in Cornell box scene, fixed time seed 123.0)"),
+            "data": ("synthetic (the reference's deprecated sphere-room scene, integrator mode 2"
+                     if wl.get("scene") == "spheres" else
+                     "synthetic (the reference's built-in Cornell box scene, integrator mode 2"
+                     if legacy else
+                     "synthetic (the reference's built-in Cornell box scene") +
+                    f"{', rotated off-axis' if wl.get('rotate') else ''}; time seed {TIME0} + frame "
+                    "index, a new RNG stream every frame)",
             "config": {"workload": wl["workload"], "width": W, "height": H, "spp": spp,
                        "faces": n_faces, "parallelism": f"pixel-stripes x{world}",
                        "accel": args.accel, "kernel_schedule": variant & ~rvcp_amd.abi.VARIANT_SPECIALIZED,
                        "scan": ("scene-specialised (hipRTC at upload, DESIGN.md §4.7)"
                                 if variant & rvcp_amd.abi.VARIANT_SPECIALIZED else "generic"),
                        "upload_s": round(upload_s, 3),
+                       # warm-up frames actually run: at least one full batch per context
+                       "warmup_frames": warm,
                        "frames_in_flight": fif, "grid_waves_per_simd": grid_waves,
                        "frames_per_launch": batch,
                        # one frame alone, enqueue to completion (the latency of a synchronous
@@ -748,11 +875,19 @@ def main():
                          if world == 1 else None,
                          "executed_traversal_frac": round(trav_exec / max(trav, 1), 4),
                          "valu_issue_frac_pmc_guide": valu_busy,
-                         "valu_issue_frac_pmc_measured_ceiling": valu_issue_frac},
+                         "valu_issue_frac_pmc_measured_ceiling": valu_issue_frac,
+                         "valu_insts_per_frame_pmc": None if not valu_insts else round(valu_insts),
+                         "valu_issue_frac_wall": None if valu_wall is None else round(valu_wall, 4),
+                         "valu_issue_frac_wall_definition": (
+                             "PMC SQ_INSTS_VALU of the dominant kernel per frame (" + str(valu_src) +
+                             f") / (ms_per_step x {SHADER_CLOCK_GHZ} GHz x {N_SIMDS} SIMDs x "
+                             f"{VALU_ISSUE_PER_CLK} wave-instructions per SIMD-cycle)")},
             "cpu_baseline": None,
         }
         if world > 1:
             out["config"]["per_rank"] = per_rank
+        if args.save_frame:
+            out["config"]["saved_frame_time"] = frame_time      # the saved frame's time seed
         if frame_check is not None:
             out["config"]["assembled_frame_bitexact_vs_1gpu"] = frame_check
             out["config"]["one_gpu_ms"] = round(one_gpu_ms, 4)
@@ -760,6 +895,9 @@ def main():
             out["config"]["one_gpu_grid_waves_per_simd"] = grid1
             out["config"]["one_gpu_frames_per_launch"] = batch1
             out["config"]["speedup_vs_one_gpu_same_frame"] = round(one_gpu_ms / ms_per_step, 3)
+            # the same frame's Msamples/s on this GPU alone: value / one_gpu_value is the
+            # scaling curve of this frame
+            out["config"]["one_gpu_value"] = round(W * H * spp / (one_gpu_ms / 1000.0) / 1e6, 2)
             if rehearsal:
                 out["config"]["physical_gpus"] = 1
         if world == 1 and not args.no_cpu_baseline:

@@ -424,8 +424,11 @@ int rvcp_rccl_attach(rvcp_ctx_t *ctx, void *nccl_comm, uint32_t world, uint32_t 
  * shards to rank 0 (ncclGather, root 0, shard k at slot k of d_gathered) and, on rank 0,
  * assemble the W x H RGBA8 frame into d_frame.  d_shard_rgba8: rvcp_shard_rows(H, 0, world)
  * * W * 4 bytes on every rank; d_gathered (world times that) and d_frame (W*H*4 bytes) are
- * needed on rank 0 only (NULL elsewhere).  Enqueued on `stream` (NULL: ctx's stream); the
- * frame is bit-identical to a single-GPU render.  The preceding render on ctx must have been
+ * needed on rank 0 only (NULL elsewhere).  Enqueued on `stream`, behind the caller's own
+ * ordering; with stream = NULL on ctx's gather stream (highest priority), after the
+ * preceding render by an event, and the next render on ctx waits for the gather by an event,
+ * so the render stream is free for the next frame meanwhile.  The frame is bit-identical to
+ * a single-GPU render.  The preceding render on ctx must have been
  * shard_index = rank, shard_count = world of the same W x H frame (else RVCP_E_INVALID). */
 int rvcp_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, uint32_t width,
                             uint32_t height, void *d_gathered, void *d_frame, void *stream);

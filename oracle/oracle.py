@@ -13,22 +13,25 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "build", "librvcp_oracle.so")
-_lib = None
+# the same source at -O3: the copy bench.py's cpu_baseline times
+LIB_PATH_O3 = os.path.join(_HERE, "build", "librvcp_oracle_o3.so")
+_libs = {}
 
 
 def build(force: bool = False) -> str:
     """Compile the oracle with its Makefile (gcc); returns the .so path."""
-    if force or not os.path.exists(LIB_PATH):
+    if force or not os.path.exists(LIB_PATH) or not os.path.exists(LIB_PATH_O3):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def lib(o3: bool = False):
+    """The checker (-O2), or with o3 the timing copy (-O3)."""
+    path = LIB_PATH_O3 if o3 else LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         P = ctypes.c_void_p
         L.rvcp_oracle_sinf.argtypes = [ctypes.c_float]
         L.rvcp_oracle_sinf.restype = ctypes.c_float
@@ -57,8 +60,8 @@ def lib():
         L.rvcp_oracle_render.restype = ctypes.c_int
         L.rvcp_oracle_mandelbrot.argtypes = [P, u32, u32, ctypes.c_int, P, P]
         L.rvcp_oracle_mandelbrot.restype = ctypes.c_int
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def _ptr(a):
@@ -117,11 +120,12 @@ def default_threads() -> int:
         return os.cpu_count() or 1
 
 
-def render(scene_arrays: dict, push, cfg, W, H, rect=None, threads=None, want_linear=True):
+def render(scene_arrays: dict, push, cfg, W, H, rect=None, threads=None, want_linear=True,
+           o3=False):
     """Render with the oracle.  scene_arrays: materials/vertices/faces/lum_face_ids numpy
     record arrays (scene.py dtypes); push: PUSH_DTYPE record; cfg: rvcp_config_t bytes
     (numpy record of CONFIG_DTYPE).  Returns (linear [th,tw,3] f32 | None, rgba [th,tw,4] u8,
-    traversals)."""
+    traversals).  o3: render with the -O3 timing copy (same bits)."""
     x0, y0, tw, th = rect if rect is not None else (0, 0, W, H)
     threads = threads or default_threads()
     mats = np.ascontiguousarray(scene_arrays["materials"])
@@ -135,7 +139,7 @@ def render(scene_arrays: dict, push, cfg, W, H, rect=None, threads=None, want_li
     lin = np.zeros((th, tw, 3), dtype=np.float32) if want_linear else None
     rgba = np.zeros((th, tw, 4), dtype=np.uint8)
     trav = np.zeros(1, dtype=np.uint64)
-    rc = lib().rvcp_oracle_render(_ptr(mats), len(mats), _ptr(verts), len(verts), _ptr(faces),
+    rc = lib(o3).rvcp_oracle_render(_ptr(mats), len(mats), _ptr(verts), len(verts), _ptr(faces),
                                   len(faces), _ptr(sph), 0 if sph is None else len(sph),
                                   _ptr(lum), len(lum), _ptr(push), _ptr(cfg),
                                   W, H, x0, y0, tw, th, _ptr(lin), _ptr(rgba), _ptr(trav),

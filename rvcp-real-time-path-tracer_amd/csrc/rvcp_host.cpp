@@ -44,6 +44,13 @@ struct rvcp_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;   // start, main kernel, end
     hipEvent_t evg0 = nullptr, evg1 = nullptr;                // gather start / end
+    // rvcp_gather_frame_async without a caller stream runs on gstream (high priority), joined
+    // to the render stream by events: evr (render done) before the gather, evg1 (gather done)
+    // before the next render on this context overwrites the shard buffer the gather reads
+    hipStream_t gstream = nullptr;
+    hipStream_t render_stream = nullptr;     // the stream of the last render (the caller's or ours)
+    hipEvent_t evr = nullptr;
+    bool gather_on_gstream = false;
     bool gather_pending = false;
     int grid_capacity[kMaxVariant + 1] = {};   // resident workgroups per kernel variant
     int legacy_capacity = 0;                   // ... of the RVCP_INTEGRATOR_LEGACY kernel
@@ -347,8 +354,16 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->evm) != hipSuccess ||
         hipEventCreate(&ctx->ev1) != hipSuccess || hipEventCreate(&ctx->evg0) != hipSuccess ||
-        hipEventCreate(&ctx->evg1) != hipSuccess)
+        hipEventCreate(&ctx->evg1) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->evr, hipEventDisableTiming) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "stream/event creation failed"));
+    {   // the frame gather's own stream, at the device's highest priority: its RCCL and
+        // assembly kernels are dispatched ahead of other streams' queued work
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+            hipStreamCreateWithPriority(&ctx->gstream, hipStreamNonBlocking, greatest) != hipSuccess)
+            return bail(fail(ctx, RVCP_E_HIP, "gather stream creation failed"));
+    }
 
     // UNORM8 thresholds on the stored value g: u8 >= k  <=>  g >= G[k].
     // RVCP_UNORM_DRIVER: u8 = (floor(4096 g) * 255 + 2048) >> 12, so G[k] = m_k / 4096 with
@@ -475,6 +490,8 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->evg0) (void)hipEventDestroy(ctx->evg0);
     if (ctx->evg1) (void)hipEventDestroy(ctx->evg1);
+    if (ctx->evr) (void)hipEventDestroy(ctx->evr);
+    if (ctx->gstream) (void)hipStreamDestroy(ctx->gstream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return RVCP_OK;
@@ -778,6 +795,8 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
         A.n_pixels = split_px;
     }
     ctx->last_spec = false;
+    // a gather of this context's previous frame may still read the caller's shard buffer
+    if (ctx->gather_on_gstream) HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->evg1, 0));
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(unsigned long long), s));
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     if (A.n_pixels > 0) {
@@ -915,6 +934,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     }
     HIP_TRY(ctx, hipEventRecord(ctx->ev1, s));
     ctx->pending = true;
+    ctx->render_stream = s;
     ctx->last_trivial = trivial;
     ctx->last_variant = (trivial || A.n_pixels == 0) ? 0 : legacy ? 8
                       : A.accel ? (ctx->cfg.kernel_variant == 9 ? 9 : 7) : A.variant;
@@ -1262,7 +1282,13 @@ static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, u
         return fail(ctx, RVCP_E_INVALID, "gather after a render of another shard / frame size "
                     "(rvcp_render_shard_async must use shard_index = rank, shard_count = world)");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    // the caller's stream, or the context's gather stream behind the render (evr): the
+    // gather and rank 0's assembly then leave the render stream free for the next frame
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->gstream;
+    if (!stream) {
+        HIP_TRY(ctx, hipEventRecord(ctx->evr, ctx->render_stream ? ctx->render_stream : ctx->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->evr, 0));
+    }
     const uint32_t N = ctx->comm_world;
     const uint32_t slot = rvcp_shard_rows(height, 0, N);      // shard 0 has the most rows
     HIP_TRY(ctx, hipEventRecord(ctx->evg0, s));
@@ -1274,6 +1300,7 @@ static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, u
         return fail(ctx, RVCP_E_HIP, "assemble launch failed");
     HIP_TRY(ctx, hipEventRecord(ctx->evg1, s));
     ctx->gather_pending = true;
+    ctx->gather_on_gstream = !stream;
     return RVCP_OK;
 }
 

@@ -341,6 +341,39 @@ def cornell_box() -> Scene:
     return Scene(camera, materials, [], Mesh(V, F))
 
 
+def rotated_scene(base: Scene, yaw_deg: float = 23.0, pitch_deg: float = 17.0,
+                  roll_deg: float = 11.0, center=(0.0, 274.4, 0.0)) -> Scene:
+    """`base` with its mesh AND camera turned by R = Rz(roll) Rx(pitch) Ry(yaw) about `center` (the
+    Cornell box's middle): every vertex p -> f32(c + R (p - c)) and normal n ->
+    normalize(f32(R n)) (rotation in float64, one rounding), the camera re-built by
+    Camera::new from its turned position and look-at point.  The camera keeps the world up
+    axis (camera.rs:62-68), so the box appears turned in the frame, with the same content.
+    No triangle of the Cornell box keeps an exact-zero position or edge component, so the
+    scene-specialised scan has no product to drop: this is the bench's
+    off-axis workload (`bench.py --workload c3rot`)."""
+    a, b, g = np.radians(yaw_deg), np.radians(pitch_deg), np.radians(roll_deg)
+    ry = np.array([[np.cos(a), 0.0, np.sin(a)], [0.0, 1.0, 0.0], [-np.sin(a), 0.0, np.cos(a)]])
+    rx = np.array([[1.0, 0.0, 0.0], [0.0, np.cos(b), -np.sin(b)], [0.0, np.sin(b), np.cos(b)]])
+    rz = np.array([[np.cos(g), -np.sin(g), 0.0], [np.sin(g), np.cos(g), 0.0], [0.0, 0.0, 1.0]])
+    R = rz @ rx @ ry
+    c = np.asarray(center, dtype=np.float64)
+
+    def turn(p):
+        return (c + R @ (np.asarray(p, dtype=np.float64) - c)).astype(f32)
+
+    bv = base.mesh.aligned_vertices().copy()
+    pos = bv["position"][:, :3].astype(np.float64)
+    bv["position"][:, :3] = (c + (pos - c) @ R.T).astype(f32)
+    nr = (bv["normal"][:, :3].astype(np.float64) @ R.T).astype(f32)
+    bv["normal"][:, :3] = np.stack([normalize(n) for n in nr])
+    cam = base.camera
+    look = (cam.position.astype(np.float64) + 1050.0 * cam.forward.astype(np.float64))
+    camera = Camera.new(turn(cam.position), turn(look), cam.t_near, cam.t_far, cam.vertical_fov,
+                        cam.move_speed, cam.rotate_speed)
+    mesh = ArrayMesh(bv, base.mesh.aligned_faces().copy())
+    return Scene(camera, list(base.materials), list(base.spheres), mesh)
+
+
 # --------------------------------------------------------------------------------------
 # Synthetic large-mesh workload (BASELINE.json configs[4]; SURVEY.md §8(d) "C5 generator")
 # --------------------------------------------------------------------------------------

@@ -88,8 +88,10 @@ def _negotiate_worker(rank, world, port, outdir):
     results = {}
     try:
         for case, bad_rank, stage in [("ok", -1, ""), ("id", 3, "id"), ("init", 5, "init"),
-                                      ("probe", 7, "probe"), ("init_all", -2, "init")]:
+                                      ("render", 6, "render"), ("probe", 7, "probe"),
+                                      ("init_all", -2, "init")]:
             inited = []
+            gathered = []
 
             def fails(st):
                 return stage == st and (bad_rank == rank or bad_rank == -2)
@@ -105,12 +107,18 @@ def _negotiate_worker(rank, world, port, outdir):
                 assert uid == bytes([0]) * 128          # every rank joins rank 0's ids
                 inited.append(i)
 
-            def probe():
+            def probe_render():
+                if fails("render"):
+                    raise RuntimeError("render: out of memory")
+
+            def probe_gather():
+                gathered.append(True)
                 if fails("probe"):
                     raise RuntimeError("ncclGather: internal error")
 
-            mode, why = bench.negotiate_gather(dist, rank, 2, make_id, init_comm, probe)
-            results[case] = (mode, why, inited)
+            mode, why = bench.negotiate_gather(dist, rank, 2, make_id, init_comm, probe_render,
+                                               probe_gather)
+            results[case] = (mode, why, inited, gathered)
         import pickle
         with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
             pickle.dump(results, f)
@@ -135,10 +143,68 @@ def test_negotiate_gather_world8_injected_failures(tmp_path):
             res.append(pickle.load(f))
     for r in range(8):
         assert res[r]["ok"][0] == "rccl" and res[r]["ok"][1] is None and res[r]["ok"][2] == [0, 1]
-        for case, bad in [("id", "rank 3"), ("init", "rank 5"), ("probe", "rank 7")]:
-            mode, why, _ = res[r][case]
+        for case, bad in [("id", "rank 3"), ("init", "rank 5"), ("render", "rank 6"),
+                          ("probe", "rank 7")]:
+            mode, why, _, _ = res[r][case]
             assert mode == "host" and bad in why, (r, case, why)
-        mode, why, _ = res[r]["init_all"]
+        mode, why, _, _ = res[r]["init_all"]
         assert mode == "host" and all(f"rank {k}" in why for k in range(8))
+        # a render failure on one rank keeps EVERY rank out of the collective gather (its
+        # peers would otherwise wait in it forever)
+        assert res[r]["render"][3] == [] and res[r]["ok"][3] == [True]
     # the id failure stops before any communicator is joined
     assert all(res[r]["id"][2] == [] for r in range(8))
+
+
+_RANK_STUB = '''
+import json, os, sys
+import torch
+import torch.distributed as dist
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+t = torch.tensor([float(r)])
+dist.all_reduce(t)
+if r == 0:
+    print(json.dumps({"n_gpus": w, "sum": float(t.item()), "argv": sys.argv[1:],
+                      "master": os.environ["MASTER_ADDR"]}), flush=True)
+fail = os.environ.get("STUB_FAIL_RANK")
+dist.destroy_process_group()
+if fail is not None and int(fail) == r:
+    sys.exit(3)
+'''
+
+
+def _self_launch(tmp_path, extra_env=None):
+    import subprocess
+    import sys
+    stub = tmp_path / "rank_stub.py"
+    stub.write_text(_RANK_STUB)
+    code = ("import sys, bench\n"
+            f"rc = bench.self_launch(2, ['--gpus', '2', '--steps', '3'], script={str(stub)!r})\n"
+            "print('PARENT_TORCH', 'torch' in sys.modules, flush=True)\n"
+            "sys.exit(rc)\n")
+    env = dict(os.environ, **(extra_env or {}))
+    env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True,
+                          text=True, timeout=180, env=env)
+
+
+def test_self_launch_relays_rank0_line(tmp_path):
+    """`python bench.py --gpus N` without a launcher (the driver's form): bench.self_launch
+    starts N ranks under torch.distributed.run on 127.0.0.1 and its stdout carries rank 0's
+    one JSON line; the parent never imports torch, so it never initialises the GPU (here the
+    ranks are a gloo stand-in for bench.py's own main)."""
+    r = _self_launch(tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["sum"] == 1.0 and d["master"] == "127.0.0.1"
+    assert d["argv"] == ["--gpus", "2", "--steps", "3"]
+    assert "PARENT_TORCH False" in r.stdout
+
+
+def test_self_launch_fails_with_a_rank(tmp_path):
+    """A failing rank makes the whole command fail (non-zero exit status)."""
+    r = _self_launch(tmp_path, {"STUB_FAIL_RANK": "1"})
+    assert r.returncode != 0

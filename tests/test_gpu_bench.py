@@ -60,11 +60,14 @@ def test_bench_line(tmp_path, workload, side, spp, steps):
     pl = rl["per_launch"]
     assert pl["frames"] >= 1 and 0 < pl["frac"] <= 1
     assert pl["kernel_ms_min"] <= pl["kernel_ms"]
-    # the saved frame is the oracle's
+    # every frame has its own seed (123.0 + frame index); the saved frame is the oracle's
+    # render of its seed
+    assert c["saved_frame_time"] >= 123.0
+    assert d["frame_interval_ms_median"] > 0 and "frame_ms_median" not in d
     frame = np.load(frame_path)
     sc = rvcp_amd.Scene.default()
     cfg = rvcp_amd.abi.make_config(spp=spp)
     for y in (0, 131, 200, H - 1):
-        _, o_rgba, _ = O.render(scene_arrays(sc), sc.push_constant(123.0), cfg, W, H,
+        _, o_rgba, _ = O.render(scene_arrays(sc), sc.push_constant(c["saved_frame_time"]), cfg, W, H,
                                 rect=(0, y, W, 1), want_linear=False)
         assert np.array_equal(frame[y:y + 1], o_rgba), y

@@ -177,3 +177,17 @@ def test_sample_ray_default_camera():
     # pixel (0, 0) is the top-left; u = fwd x up = -x, so image-left is +x (which is why the
     # green x = -275 wall appears on the right of the README screenshot); v = fwd x u = -y
     assert r[3] > 0 and r[4] > 0
+
+
+def test_o3_timing_copy_same_bits():
+    """bench.py's cpu_baseline times the -O3 build of the oracle; it renders
+    the same bits as the -O2 checker (the Cornell box and the off-axis rotated box)."""
+    from rvcp_amd import scene as S
+    for sc in (rvcp_amd.Scene.default(), S.rotated_scene(rvcp_amd.Scene.default())):
+        arrays = dict(materials=sc.aligned_materials(), vertices=sc.mesh.aligned_vertices(),
+                      faces=sc.mesh.aligned_faces(), lum_face_ids=sc.luminous_face_ids())
+        cfg = rvcp_amd.abi.make_config(spp=3)
+        a = O.render(arrays, sc.push_constant(123.0), cfg, 48, 40)
+        b = O.render(arrays, sc.push_constant(123.0), cfg, 48, 40, o3=True)
+        assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+        assert np.array_equal(a[1], b[1]) and a[2] == b[2]
