@@ -403,9 +403,7 @@ def main():
     ap.add_argument("--accel", default="none", choices=["none", "bvh"],
                     help="bvh: the opt-in BVH (not the parity path; never the default line)")
     ap.add_argument("--schedule", type=int, default=0,
-                    help="rvcp_config_t.kernel_variant (0 = the library's automatic choice; with "
-                         "--accel bvh, 3 = the persistent BVH path kernel instead of the "
-                         "wavefront form)")
+                    help="rvcp_config_t.kernel_variant (0 = the library's automatic choice)")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per path kernel (rvcp_render_frames_async; 1 = one frame per "
                          "rvcp_render_shard_async call; 0 = auto, see auto_pipeline)")

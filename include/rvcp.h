@@ -165,10 +165,9 @@ typedef struct rvcp_config {
      * 4 = 3 with the scan staged through LDS tiles shared by the workgroup, 5 = 4 with one ray
      * per lane per iteration (shadow ray, then path ray: no empty ray slots), 6 = 3 compiled
      * for 6 waves per SIMD, 10 = 4 with the workgroup's rays pooled in LDS and scanned in
-     * 64-ray passes (7 and 8 are not schedules; 9 only with RVCP_ACCEL_BVH: the BVH path in
-     * wavefront form, shade / trace kernel generations -- measured slower than the default
-     * persistent BVH path kernel, kept for A/B).  Every schedule produces bit-identical
-     * frames. */
+     * 64-ray passes (7, 8 and 9 are not schedules: the BVH wavefront form that held 9 was
+     * measured 2.8x slower than the BVH path kernel and removed in round 4).  Every schedule
+     * produces bit-identical frames. */
     int32_t kernel_variant;
     /* Acceleration structure: RVCP_ACCEL_NONE (default) scans every triangle like the
      * shader (bit-exact, the parity path).  RVCP_ACCEL_BVH (opt-in, games101 only) builds a
@@ -219,7 +218,6 @@ typedef struct rvcp_stats {
     uint32_t faces;                   /* F, triangles tested per traversal */
     int32_t kernel_variant;           /* the kernel schedule that ran (rvcp_config_t::
                                          kernel_variant resolved; 7 = BVH path kernel,
-                                         9 = BVH wavefront form,
                                          8 = RVCP_INTEGRATOR_LEGACY kernel, 0 = none), plus
                                          RVCP_VARIANT_SPECIALIZED when the scene-specialised
                                          path kernel ran */
@@ -363,8 +361,8 @@ int rvcp_render_shard_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push,
  * pixels x spp).  Integrator mode 2 (RVCP_INTEGRATOR_LEGACY) has no pre-pass: its one kernel
  * queues the batch's pixels frame after frame, reading each frame's camera and time from a
  * table the call uploads.  Needs a one-GPU context and, for games101, a pre-pass schedule (the
- * automatic ones: 3-6, 10, the persistent BVH path kernel); schedules 1, 2 and the BVH
- * wavefront form return RVCP_E_UNSUPPORTED unless n_frames = 1. */
+ * automatic ones: 3-6, 10, the BVH path kernel); schedules 1 and 2 return
+ * RVCP_E_UNSUPPORTED unless n_frames = 1. */
 int rvcp_render_frames_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes,
                              uint32_t n_frames, uint32_t width, uint32_t height,
                              uint32_t shard_index, uint32_t shard_count,

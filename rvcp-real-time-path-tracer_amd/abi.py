@@ -30,7 +30,7 @@ assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 56
 KERNEL_NAMES = {1: "games101_kernel", 2: "games101_dual_kernel", 3: "games101_path_kernel<5>",
                 4: "games101_tiled_kernel", 5: "games101_tiled_single_kernel",
                 6: "games101_path_kernel<6>", 7: "games101_bvh_path_kernel", 8: "legacy_kernel",
-                9: "wf_trace_kernel", 10: "games101_tiled_pool_kernel",
+                10: "games101_tiled_pool_kernel",
                 # + RVCP_VARIANT_SPECIALIZED (16): the scene-specialised module (rvcp_jit.cpp)
                 19: "rvcp_spec_path_kernel5", 22: "rvcp_spec_path_kernel6", 24: "rvcp_spec_legacy_kernel"}
 VARIANT_SPECIALIZED = 16

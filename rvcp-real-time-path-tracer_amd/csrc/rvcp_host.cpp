@@ -92,11 +92,6 @@ struct rvcp_ctx {
     // host memory (one render in flight per context, so the staging is free again at the next)
     float *d_cams = nullptr, *h_cams = nullptr;
     uint32_t cap_cams = 0;
-    // wavefront BVH path (rvcp_launch_bvh_wavefront): slot state, ray list, results, counters,
-    // trace stacks, the pinned read-back words and their events; allocated on the first BVH frame
-    WfBuffers wf{};
-    size_t cap_wf = 0;
-    int wf_trace_per_cu = 0;
 
     // staging for the synchronous host API
     uint32_t *d_rgba = nullptr;
@@ -319,7 +314,7 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         return fail(nullptr, RVCP_E_UNSUPPORTED, "unsupported integrator");
     if (cfg->spp == 0) return fail(nullptr, RVCP_E_INVALID, "spp must be > 0");
     if (cfg->kernel_variant < 0 || cfg->kernel_variant > kMaxVariant || cfg->kernel_variant == 7 ||
-        cfg->kernel_variant == 8 || (cfg->kernel_variant == 9 && cfg->accel != RVCP_ACCEL_BVH))
+        cfg->kernel_variant == 8 || cfg->kernel_variant == 9)
         return fail(nullptr, RVCP_E_INVALID, "unknown kernel_variant");
     if (cfg->n_gpus < 0 || cfg->n_gpus > 64)
         return fail(nullptr, RVCP_E_INVALID, "n_gpus must be in [0, 64]");
@@ -407,9 +402,6 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         if (rvcp_games101_occupancy(kOccupancyBvh, &per_cu) != 0 || per_cu <= 0) per_cu = 1;
         if (cap > 0 && cap < per_cu) per_cu = cap;
         ctx->bvh_capacity = per_cu * cus;
-        per_cu = 0;
-        if (rvcp_wf_trace_occupancy(&per_cu) != 0 || per_cu <= 0) per_cu = 1;
-        ctx->wf_trace_per_cu = per_cu * cus;
     }
     if (cfg->n_gpus > 1) {   // one sub-context per further GPU (shards 1..N-1)
         for (int i = 1; i < cfg->n_gpus; i++) {
@@ -474,14 +466,6 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     (void)hipFree(ctx->d_acc);
     (void)hipFree(ctx->d_cams);
     (void)hipHostFree(ctx->h_cams);
-    (void)hipFree(ctx->wf.st);
-    (void)hipFree(ctx->wf.rays);
-    (void)hipFree(ctx->wf.res);
-    (void)hipFree(ctx->wf.counters);
-    (void)hipFree(ctx->wf.gstk);
-    if (ctx->wf.pinned) (void)hipHostFree(ctx->wf.pinned);
-    for (void *e : ctx->wf.ev)
-        if (e) (void)hipEventDestroy((hipEvent_t)e);
     (void)hipFree(ctx->d_timeline);
     (void)hipFree(ctx->d_pack_rgba);
     (void)hipFree(ctx->d_pack_lin);
@@ -651,36 +635,6 @@ uint32_t rvcp_shard_rows(uint32_t height, uint32_t shard_index, uint32_t shard_c
     return rows;
 }
 
-// Buffers of the wavefront BVH path for a frame of n pixels: min(n, kWfMaxSlots) path slots.
-static constexpr uint32_t kWfMaxSlots = 1u << 19;
-static int wf_reserve(rvcp_ctx_t *ctx, uint32_t n_pixels)
-{
-    const uint32_t N = n_pixels < kWfMaxSlots ? n_pixels : kWfMaxSlots;
-    WfBuffers &w = ctx->wf;
-    if (!w.counters) {
-        HIP_TRY(ctx, hipMalloc(&w.counters, kWfCountersBytes));
-        HIP_TRY(ctx, hipHostMalloc((void **)&w.pinned, 2 * sizeof(uint32_t), hipHostMallocDefault));
-        for (void *&e : w.ev) HIP_TRY(ctx, hipEventCreateWithFlags((hipEvent_t *)&e, hipEventDisableTiming));
-        w.trace_blocks = (uint32_t)ctx->wf_trace_per_cu;
-        HIP_TRY(ctx, hipMalloc((void **)&w.gstk, (size_t)w.trace_blocks * kWfTraceThreads *
-                                                     kWfStackGlobal * sizeof(int32_t)));
-    }
-    if (ctx->cap_wf < N) {
-        (void)hipFree(w.st);
-        (void)hipFree(w.rays);
-        (void)hipFree(w.res);
-        w.st = nullptr;
-        w.rays = w.res = nullptr;
-        ctx->cap_wf = 0;
-        HIP_TRY(ctx, hipMalloc((void **)&w.st, (size_t)N * kWfStateFields * sizeof(float)));
-        HIP_TRY(ctx, hipMalloc(&w.rays, (size_t)N * 64));      // two lists (generation parity)
-        HIP_TRY(ctx, hipMalloc(&w.res, (size_t)N * 8));
-        ctx->cap_wf = N;
-    }
-    w.n_slots = N;
-    return RVCP_OK;
-}
-
 // n_frames consecutive frames of one shard (pushes[k] for frame k) into outputs laid out frame
 // after frame, `slot` = the largest shard's rows apart (rvcp_render_frames_async); n_frames = 1
 // is rvcp_render_shard_async.
@@ -754,10 +708,9 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     const bool trivial = A.max_bounces == 0 || (!legacy && 1.0f < A.att_stop);
     // a batch shares one surface list and one path kernel: the pre-pass schedules (3-6, 10 and
     // the persistent BVH path kernel) only
-    if (n_frames > 1 && !trivial && !legacy && (A.variant < 3 ||
-                                               (A.accel && ctx->cfg.kernel_variant == 9)))
+    if (n_frames > 1 && !trivial && !legacy && A.variant < 3)
         return fail(ctx, RVCP_E_UNSUPPORTED, "frame batches need a pre-pass schedule of the games101 "
-                    "integrator (schedules 3-6, 10, or the persistent BVH path kernel) or mode 2");
+                    "integrator (schedules 3-6, 10, or the BVH path kernel) or mode 2");
     std::vector<FrameArgs> FA;          // per frame of the batch (camera, time, pixel base)
     const uint32_t frame_px = A.n_pixels;
     const uint32_t split_px = frame_px * n_frames;          // the queue of the whole batch
@@ -893,17 +846,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                     HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)n_surf * sizeof(SurfRecord)));
                     ctx->cap_surf = n_surf;
                 }
-                if (A.accel && ctx->cfg.kernel_variant == 9) {
-                    // the BVH path in wavefront form (shade / trace generations; measured
-                    // slower than the persistent BVH path kernel)
-                    if ((rc = wf_reserve(ctx, A.n_pixels)) != RVCP_OK) return rc;
-                    rc = rvcp_launch_bvh_wavefront(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts,
-                                                   ctx->d_mats, ctx->d_lights, ctx->d_gamma,
-                                                   (uint32_t *)d_rgba8, lin, ctx->d_counters,
-                                                   ctx->d_surf, ctx->d_shade, ctx->d_bvh_nodes,
-                                                   ctx->d_bvh_tris, s, ctx->evm, &ctx->wf);
-                    if (rc == -3) return fail(ctx, RVCP_E_HIP, "wavefront BVH frame did not finish");
-                } else {
+                {
                     FA.assign(n_frames, A);
                     for (uint32_t k = 1; k < n_frames; ++k) {
                         camera_constants(pushes[k], width, height, FA[k]);
@@ -937,7 +880,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     ctx->render_stream = s;
     ctx->last_trivial = trivial;
     ctx->last_variant = (trivial || A.n_pixels == 0) ? 0 : legacy ? 8
-                      : A.accel ? (ctx->cfg.kernel_variant == 9 ? 9 : 7) : A.variant;
+                      : A.accel ? 7 : A.variant;
     if (ctx->last_spec && ctx->last_variant != 0) ctx->last_variant |= RVCP_VARIANT_SPECIALIZED;
     ctx->last_pixels = (uint64_t)frame_px * n_frames;       // stats cover the whole batch
     ctx->last_spp = A.spp;

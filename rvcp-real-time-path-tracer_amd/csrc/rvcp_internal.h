@@ -230,23 +230,6 @@ struct FrameArgs {
     unsigned long long *timeline;
 };
 
-// Buffers of the wavefront BVH path (rvcp_launch_bvh_wavefront), owned by the context.
-struct WfBuffers {
-    float *st;                  // WF_FIELDS x n_slots path-slot state (structure of arrays)
-    uint32_t n_slots;
-    void *rays;                 // 2 lists (generation parity) of 2 float4 per slot: the rays
-    void *res;                  // float2 per slot: (t, face) of each listed ray
-    void *counters;             // WfCounters
-    int32_t *gstk;              // the trace lanes' stack entries beyond the LDS part
-    uint32_t trace_blocks;      // persistent trace grid
-    uint32_t *pinned;           // 2 host-pinned words: live-slot counts read back per batch
-    void *ev[2];                // hipEvent_t per batch
-};
-constexpr uint32_t kWfStateFields = 29;      // WF_FIELDS (rvcp_kernels.hip)
-constexpr uint32_t kWfTraceThreads = 256;    // kWfTraceBlock
-constexpr uint32_t kWfStackGlobal = 16;      // kBvhStack - kWfShort entries per trace lane
-constexpr uint32_t kWfCountersBytes = 32;    // sizeof(WfCounters)
-
 #ifndef __HIPCC_RTC__
 // rvcp_bvh.cpp: build the BVH over n faces (three vertex positions each); returns the depth.
 int bvh_build(const float (*pos)[3][3], uint32_t n, std::vector<BvhNode> &nodes,
@@ -298,14 +281,6 @@ int rvcp_launch_assemble(const uint32_t *gathered, uint32_t slot_rows, uint32_t 
 int rvcp_launch_fill(uint32_t *out_rgba, float *out_lin, uint32_t n_pixels, uint32_t rgba,
                      void *stream);
 int rvcp_games101_occupancy(int variant, int *blocks_per_cu);
-int rvcp_launch_bvh_wavefront(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
-                              const void *faces, const void *verts, const rvcp::MatRecord *mats,
-                              const rvcp::LightRecord *lights, const float *gamma_t,
-                              uint32_t *out_rgba, float *out_lin, unsigned long long *counters,
-                              rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
-                              const rvcp::Bvh4Node *bvh_nodes, const rvcp::TriRecord *bvh_tris,
-                              void *stream, void *main_event, const rvcp::WfBuffers *wb);
-int rvcp_wf_trace_occupancy(int *blocks_per_cu);
 void rvcp_static_split(uint32_t n, uint32_t grid_waves, uint32_t n_simds, uint32_t *waves,
                        uint32_t *chunk);
 }

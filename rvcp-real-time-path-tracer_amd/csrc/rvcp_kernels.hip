@@ -146,11 +146,7 @@ __device__ __forceinline__ bool quot_box(f3 v) {
     const uint32_t lo = min(min(bx - 1u, by - 1u), bz - 1u);
     return (hi <= (0x58800000u << 1)) & (lo >= (0x26800000u << 1) - 1u);   // 2^50, 2^-50
 }
-#ifndef RVCP_DIV_SHARED
-#define RVCP_DIV_SHARED 1
-#endif
 __device__ __forceinline__ f3 divs_y(f3 v, float s, float y) {
-    if (!RVCP_DIV_SHARED) return divs(v, s);
     f3 o = mk(quot_refine(v.x, s, y), quot_refine(v.y, s, y), quot_refine(v.z, s, y));
     const bool ok = (s >= 0x1p-50f) & (s <= 0x1p50f) & quot_box(v);
     if (__builtin_expect(!ok, 0)) o = divs(v, s);
@@ -328,25 +324,8 @@ __device__ __forceinline__ bool slab(const float *b, f3 o, f3 inv, float tmin, f
 // leaf costs one memory round trip instead of one per triangle.  The leaf-ordered triangles
 // are packed as 10 floats per slot (v0, e1, e2, face id bits; leaves start at even slots, so
 // 16-B aligned, rvcp_host.cpp): ceil(2.5 cnt) 16-B loads.
-#ifndef RVCP_BVH_SPEC
-#define RVCP_BVH_SPEC 1            // speculative while-while traversal (bvh_nearest)
-#endif
-// RVCP_BVH_POOL: the wave's A and B rays pooled over its lanes (bvh_pool): C5 BVH 138 -> 103
-// ms per frame; with two-triangle leaf loads and the traversal inlined (112 VGPRs, no
-// spills) 97.5 ms (profiles/r03zj_bvh_pool_ab.log, r03zk_bvh_pool_ab.log).
-#ifndef RVCP_BVH_POOL
-#define RVCP_BVH_POOL 1
-#endif
-#ifndef RVCP_BVH_POOL_INLINE
-#define RVCP_BVH_POOL_INLINE 1
-#endif
-#ifndef RVCP_BVH_SPEC_MIN
-#define RVCP_BVH_SPEC_MIN 64       // ... whose node phase ends once this many lanes hold a leaf
-#endif
-#ifndef RVCP_BVH_LEAF_CHUNK
-#define RVCP_BVH_LEAF_CHUNK 4      // triangles loaded together (one memory round trip; 2: 2 % slower)
-#endif
-template <uint32_t kCh = RVCP_BVH_LEAF_CHUNK>
+constexpr uint32_t kBvhLeafChunk = 4;   // triangles loaded together (one round trip; 2: 2 % slower)
+template <uint32_t kCh = kBvhLeafChunk>
 __device__ __forceinline__ void bvh_leaf(const TriRecord *__restrict__ btri, int32_t ref, f3 o, f3 d,
                                          float tmin, float &bt, int &best, uint32_t slots = 0) {
     const uint32_t code = ~(uint32_t)ref;
@@ -428,7 +407,6 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
     int32_t ref = root;
     const Bvh4QNode *__restrict__ qn = reinterpret_cast<const Bvh4QNode *>(nodes + n4);
     const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
-#if RVCP_BVH_SPEC
     // Speculative while-while: a lane that reaches a leaf parks it and keeps stepping through
     // nodes until every lane holds a parked leaf (or cannot step), then the wave tests the
     // parked leaves together -- node steps and leaf tests each run with most lanes active
@@ -446,15 +424,7 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
                 else { sp -= 1; ref = LDS ? stk[sp * kBlock] : priv[sp]; }
             }
             const bool step = alive && ref >= 0;
-#if RVCP_BVH_SPEC_MIN >= 64
             if (!__any(step) || __all(parked || !alive)) break;
-#else
-            // (a leaf phase must have a parked leaf to test, or finished lanes alone could
-            // satisfy the count and the loop would never step again)
-            if (!__any(step) ||
-                (__any(parked) && __builtin_popcountll(__ballot(parked || !alive)) >= RVCP_BVH_SPEC_MIN))
-                break;
-#endif
             if (step) {
                 const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
                 const float4 w0 = q[0], w1 = q[1], w2 = q[2];
@@ -498,50 +468,6 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
             parked = false;
         }
         if (!__any(alive)) break;
-    }
-    return;
-#endif
-    for (;;) {
-        if (ref >= 0) {
-            const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
-            const float4 w0 = q[0], w1 = q[1], w2 = q[2];
-            const int4 r = reinterpret_cast<const int4 *>(qn + ref)[3];
-            const float ax = w0.w * inv.x, ay = w1.x * inv.y, az = w1.y * inv.z;
-            const float bx = (w0.x - o.x) * inv.x, by = (w0.y - o.y) * inv.y, bz = (w0.z - o.z) * inv.z;
-            const uint32_t lx = __float_as_uint(w1.z), ly = __float_as_uint(w1.w), lz = __float_as_uint(w2.x);
-            const uint32_t hx = __float_as_uint(w2.y), hy = __float_as_uint(w2.z), hz = __float_as_uint(w2.w);
-            const uint32_t nx = px ? lx : hx, fx = px ? hx : lx;
-            const uint32_t ny = py ? ly : hy, fy = py ? hy : ly;
-            const uint32_t nz = pz ? lz : hz, fz = pz ? hz : lz;
-            float kk[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float tn = __builtin_fmaxf(
-                    __builtin_fmaxf(__builtin_fmaf(ubyte_f(nx, c), ax, bx), __builtin_fmaf(ubyte_f(ny, c), ay, by)),
-                    __builtin_fmaxf(__builtin_fmaf(ubyte_f(nz, c), az, bz), tmin));
-                const float tf = __builtin_fminf(
-                    __builtin_fminf(__builtin_fmaf(ubyte_f(fx, c), ax, bx), __builtin_fmaf(ubyte_f(fy, c), ay, by)),
-                    __builtin_fminf(__builtin_fmaf(ubyte_f(fz, c), az, bz), bt));
-                kk[c] = tn <= tf ? tn : __builtin_inff();
-            }
-            float k0 = kk[0], k1 = kk[1], k2 = kk[2], k3 = kk[3];
-            int32_t c0 = r.x, c1 = r.y, c2 = r.z, c3 = r.w;
-            bvh4_cas(k0, c0, k1, c1);
-            bvh4_cas(k2, c2, k3, c3);
-            bvh4_cas(k0, c0, k2, c2);
-            bvh4_cas(k1, c1, k3, c3);
-            bvh4_cas(k1, c1, k2, c2);
-            const float inf = __builtin_inff();
-            if (k3 < inf) { if (LDS) stk[sp * kBlock] = c3; else priv[sp] = c3; sp += 1; }
-            if (k2 < inf) { if (LDS) stk[sp * kBlock] = c2; else priv[sp] = c2; sp += 1; }
-            if (k1 < inf) { if (LDS) stk[sp * kBlock] = c1; else priv[sp] = c1; sp += 1; }
-            if (k0 < inf) { ref = c0; continue; }
-        } else {
-            bvh_leaf(btri, ref, o, d, tmin, bt, best, slots);
-        }
-        if (sp == 0) break;
-        sp -= 1;
-        ref = LDS ? stk[sp * kBlock] : priv[sp];
     }
 }
 
@@ -588,22 +514,17 @@ __device__ __forceinline__ void bvh4_step(const Bvh4QNode *__restrict__ qn, lds_
     else { sp -= 1; ref = stk[sp * kBlock]; }
 }
 
-// Wave-pooled traversal (RVCP_BVH_POOL): the wave's shadow rays (lanes sA, in lane order) and
+// Wave-pooled traversal (bvh_pool): the wave's shadow rays (lanes sA, in lane order) and
 // path rays (sB) form one list of up to 128 rays; every lane takes the next untaken ray as soon
 // as its current one is finished, with the speculative while-while steps of bvh_nearest, so a
 // wave's 64 lanes share its rays instead of each waiting for its own longest traversal.  A
 // ray's (o, d) is read from its owner lane's registers (ds_bpermute via the wave's LDS table of
 // owners, tab[128]), its (t, face) is left in res[128] and read back by the owner.  Same
 // traversal per ray, so the same nearest hits.
-#ifndef RVCP_BVH_POOL_CHUNK
-#define RVCP_BVH_POOL_CHUNK 2      // leaf triangles loaded together in bvh_pool
-#endif
-#if RVCP_BVH_POOL_INLINE
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-void bvh_pool(const Bvh4Node *__restrict__ nodes,
+// (inlined into the path kernel with two-triangle leaf loads: 112 VGPRs without spills, C5
+// BVH 138 -> 97.5 ms per frame, profiles/r03zj_bvh_pool_ab.log, r03zk_bvh_pool_ab.log)
+constexpr uint32_t kBvhPoolChunk = 2;      // leaf triangles loaded together in bvh_pool
+__device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
                                       const TriRecord *__restrict__ btri, int32_t root,
                                       lds_i32 *stk, uint8_t *tab, float2 *res, uint32_t lane,
                                       bool sA, bool sB, f3 a_o, f3 a_d, f3 b_o, f3 b_d,
@@ -670,7 +591,7 @@ void bvh_pool(const Bvh4Node *__restrict__ nodes,
             if (step) bvh4_step(qn, stk, o, inv, px, py, pz, tmin, bt, ref, sp, alive);
         }
         if (parked) {
-            bvh_leaf<RVCP_BVH_POOL_CHUNK>(btri, lref, o, d, tmin, bt, best, slots);
+            bvh_leaf<kBvhPoolChunk>(btri, lref, o, d, tmin, bt, best, slots);
             parked = false;
         }
         if (has && !alive) {            // this ray is done: leave its result for the owner
@@ -1376,10 +1297,7 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
 // never touch the RNG, :424-428), and appends every other pixel with its primary hit record to
 // a compact list for the path kernel (one atomic per wave).
 // ======================================================================================
-#ifndef RVCP_PRIMARY_BLOCK
-#define RVCP_PRIMARY_BLOCK 256
-#endif
-constexpr uint32_t kPrimaryBlock = RVCP_PRIMARY_BLOCK;   // one list append (global atomic) per block
+constexpr uint32_t kPrimaryBlock = 256;   // one list append (global atomic) per block
 
 template <bool BVH>
 __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
@@ -1471,34 +1389,15 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 // faster on C5 than the 3 waves its natural 146-155 VGPRs give.
 // The BVH path kernel traces one ray per lane per iteration (the variant-5 form): C5 297 ->
 // 283 ms over the dual form, whose second traversal leaves the lanes without a path ray idle.
-#ifndef RVCP_BVH_SINGLE
-#define RVCP_BVH_SINGLE true
-#endif
-#ifndef RVCP_SPLIT_PRETEST
-#define RVCP_SPLIT_PRETEST 1
-#endif
-#ifndef RVCP_TILED_MIN_WAVES
-#define RVCP_TILED_MIN_WAVES 4
-#endif
-// RVCP_TILED_PAIR: the tiled scans issue the first pretest halves of two triangles together
-// (ILP for the latency-bound per-triangle chain; C5 -5 %).  RVCP_TILED_STEP1:
-// triangles per step of the one-slot schedule 5 (3 and 4 measured equal to 2).
-#ifndef RVCP_TILED_PAIR
-#define RVCP_TILED_PAIR 1
-#endif
-#ifndef RVCP_TILED_STEP1
-#define RVCP_TILED_STEP1 2
-#endif
+constexpr int kTiledMinWaves = 4;
+// The tiled scans issue the first pretest halves of two triangles together (ILP for the
+// latency-bound per-triangle chain; C5 -5 %); the one-slot schedule 5 too (3
+// and 4 triangles per step measured equal to 2).
 // The variant-3 path kernel runs 5 waves per SIMD: 95 VGPRs without spills once the scan loop
 // is not unrolled and the pixel's surface record is re-read per sample instead of held in
 // registers (C3 5.93 -> 5.73 ms, C4 44.2 -> 41.3 ms, C2 unchanged, over 105 VGPRs / 4 waves;
 // tools/ab.sh).  Forcing 6 waves spills 26 VGPRs and is slower.
-#ifndef RVCP_SCAN_UNROLL
-#define RVCP_SCAN_UNROLL 1
-#endif
-#ifndef RVCP_PATH_MIN_WAVES
-#define RVCP_PATH_MIN_WAVES 5
-#endif
+constexpr int kPathMinWaves = 5;
 // LDS_STATE: the light sample's pending state (a_p, nee_C, nee_dist: written at the surface
 // event, read when the shadow ray resolves) and the pixel's running sum `acc` live in this
 // lane's column of an LDS block (SoA, stride = the block size) instead of 10 VGPRs across the
@@ -1811,12 +1710,11 @@ __device__ __forceinline__ void path_body(
                     // Two-stage exact test: stage 2 (1/den, t, b1, b2, the
                     // compares) only when some lane may accept.  (A software-pipelined read of
                     // the next triangle costs 12 VGPRs and was slower at 4 waves/SIMD.)
-#if RVCP_TILED_PAIR
                     // Two triangles per step: the first pretest halves of both (slots A and B)
                     // are four independent chains issued together; their results stay live
                     // and the gates then run per triangle, in index order.
-                    // (SINGLE scans one slot: RVCP_TILED_STEP1 triangles per step, same form)
-                    constexpr uint32_t kStep = SINGLE ? RVCP_TILED_STEP1 : 2u;
+                    // (SINGLE scans one slot, two triangles per step too)
+                    constexpr uint32_t kStep = 2u;
                     uint32_t i = 0;
                     for (; i + kStep <= n; i += kStep) {
                         TriRecord Tp[kStep];
@@ -1853,11 +1751,7 @@ __device__ __forceinline__ void path_body(
                         }
                     }
                     for (; i < n; ++i) {          // the last triangles of a tile
-#else
-                    for (uint32_t i = 0; i < n; ++i) {
-#endif
                         const TriRecord T = tile[i];
-#if RVCP_SPLIT_PRETEST
                         // the gates are lane masks ANDed in scalar registers (ballot of one
                         // compare each): __any(sA && p) materialised the predicate in a VGPR
                         // and compared it again, 2 VALU per gate (C5 schedule 4: -7 %)
@@ -1881,20 +1775,6 @@ __device__ __forceinline__ void path_body(
                                 }
                             }
                         }
-#else
-                        const TriPart PA = tri_stage1(T, so0, sd0);
-                        if (__any(((m0 >> lane) & 1ull) && tri_maybe(PA))) {
-                            float tA;
-                            if (tri_stage2(T, PA, A.t_min, btA, tA)) { btA = tA; bestA = (int)(base + i); }
-                        }
-                        if (!SINGLE) {
-                            const TriPart PB = tri_stage1(T, so1, sd1);
-                            if (__any(((m1 >> lane) & 1ull) && tri_maybe(PB))) {
-                                float tB;
-                                if (tri_stage2(T, PB, A.t_min, btB, tB)) { btB = tB; bestB = (int)(base + i); }
-                            }
-                        }
-#endif
                     }
                 }
                 __syncthreads();
@@ -1942,16 +1822,14 @@ __device__ __forceinline__ void path_body(
             }
         } else if (BVH) {
             // ---- opt-in BVH: each lane traverses for its own rays, or the wave's rays are
-            // pooled over its lanes (RVCP_BVH_POOL) ----
+            // pooled over its lanes (bvh_pool) ----
             lds_i32 *stk = (lds_i32 *)bvh_stack;
-#if RVCP_BVH_POOL
             if (!SINGLE) {
                 float4 *pl = pool + wv * 72;            // res: 64 float4 (128 float2), tab: 8 float4
                 bvh_pool(bvh_nodes, bvh_tris, A.bvh_root, stk, reinterpret_cast<uint8_t *>(pl + 64),
                          reinterpret_cast<float2 *>(pl), lane, sA, sB, s_ao, s_ad, b_o, b_d, A.t_min,
                          A.t_max, btA, bestA, btB, bestB, A.bvh_n4, A.bvh_slots);
             } else
-#endif
             {
             if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA, A.bvh_n4, A.bvh_slots);
             if (sB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB, A.bvh_n4, A.bvh_slots);
@@ -2037,7 +1915,7 @@ __device__ __forceinline__ void path_body(
             } else
 #endif
             {
-#pragma unroll RVCP_SCAN_UNROLL
+#pragma unroll 1
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
                 float t;
@@ -2070,7 +1948,7 @@ __device__ __forceinline__ void path_body(
             } else
 #endif
             {
-#pragma unroll RVCP_SCAN_UNROLL
+#pragma unroll 1
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 const TriRecord T = tri[i];
                 float tA, tB;
@@ -2149,11 +2027,8 @@ __global__ __launch_bounds__(kBlock, MIN_WAVES) void games101_path_kernel(
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];   // tail: ray rank -> owner lane
     __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];  // compact scan: rays, then hits
-#ifndef RVCP_STATE_LDS
-#define RVCP_STATE_LDS 1
-#endif
-    __shared__ float state_lds[RVCP_STATE_LDS ? kStateCols * kBlock : 1];   // LDS_STATE columns
-    path_body<false, false, false, RVCP_STATE_LDS != 0>(
+    __shared__ float state_lds[kStateCols * kBlock];   // LDS_STATE columns
+    path_body<false, false, false, true>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
 }
@@ -2172,19 +2047,13 @@ __global__ __launch_bounds__(kBlock, 4) void games101_bvh_path_kernel(
 {
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ int32_t bvh_stack[kBvhStack * kBlock];     // traversal stacks, column per thread
-#if RVCP_BVH_POOL
     __shared__ float4 bvh_pool_lds[(kBlock / kWave) * 72];  // per wave: 128 results + 128-B owner table
     path_body<false, true, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
                            shade, tail_tab, nullptr, bvh_nodes, bvh_tris,
                            bvh_stack + threadIdx.x, nullptr, nullptr, bvh_pool_lds);
-#else
-    path_body<false, true, RVCP_BVH_SINGLE>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
-                           shade, tail_tab, nullptr, bvh_nodes, bvh_tris,
-                           bvh_stack + threadIdx.x);
-#endif
 }
 
-__global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_kernel(
+__global__ __launch_bounds__(kBlock, kTiledMinWaves) void games101_tiled_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
@@ -2199,7 +2068,7 @@ __global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_k
 
 // Schedule 10: schedule 4 with the workgroup ray pool (path_body POOL_W): the workgroup's rays
 // are scanned against each LDS tile in full 64-ray passes shared out over its 4 waves.
-__global__ __launch_bounds__(kTiledPoolWaves * kWave, RVCP_TILED_MIN_WAVES) void games101_tiled_pool_kernel(
+__global__ __launch_bounds__(kTiledPoolWaves * kWave, kTiledMinWaves) void games101_tiled_pool_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
@@ -2216,7 +2085,7 @@ __global__ __launch_bounds__(kTiledPoolWaves * kWave, RVCP_TILED_MIN_WAVES) void
 }
 
 // Variant 5: the LDS-tiled scan with one ray per lane per iteration (no empty ray slots).
-__global__ __launch_bounds__(kBlock, RVCP_TILED_MIN_WAVES) void games101_tiled_single_kernel(
+__global__ __launch_bounds__(kBlock, kTiledMinWaves) void games101_tiled_single_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
@@ -2257,400 +2126,6 @@ __global__ __launch_bounds__(kToneBlock) void tonemap_kernel(const float *__rest
     __syncthreads();
     for (uint32_t i = blockIdx.x * kToneBlock + threadIdx.x; i < n; i += gridDim.x * kToneBlock)
         out_rgba[i] = pack_rgba(mk(lin[3 * (size_t)i], lin[3 * (size_t)i + 1], lin[3 * (size_t)i + 2]), T);
-}
-
-// ======================================================================================
-// Opt-in BVH, wavefront form.  The BVH path kernel above traverses one ray
-// per lane with the lane's whole path state live around the traversal: 4 waves per SIMD, and a
-// wave waits for the longest of its 64 traversals (PMC: 0.21 of the lanes active per VALU
-// instruction).  Here the same SINGLE ray machine is cut at the traversal:
-//   wf_shade_kernel -- one lane per path slot: resolve the ray the slot traced in the previous
-//       generation, run the settle step (end samples, take pixels from the pre-pass's surface
-//       list, surface events), append the slot's next ray to the generation's ray list and
-//       store the state (structure of arrays in HBM, WF_* fields);
-//   wf_trace_kernel -- persistent, few registers: every lane traverses a ray of the list and
-//       takes the next one as soon as it finishes (per-wave grabs of kWfGrab rays), so lanes do
-//       not idle behind the wave's longest traversal; a short LDS stack (kWfShort entries, the
-//       rest of the kBvhStack bound in global memory) leaves room for 8 waves per SIMD.
-// Each slot performs exactly the operations of path_body<false, true, true> on its pixels, in
-// the same order, and the traversal is bvh_nearest's (same nearest-hit rule), so frames are
-// the BVH path kernel's.  The host runs generations in batches and stops when no slot has work
-// left (wf_counters.alive), reading that count one batch behind so the GPU stays fed.
-// ======================================================================================
-struct WfCounters {
-    uint32_t n_rays[2];     // rays appended by the shade kernel of generation g (index g & 1)
-    uint32_t fetch[2];      // the trace kernel's next ray of generation g
-    uint32_t alive[2];      // slots with work left after the shade kernel of generation g
-    uint32_t pix_next;      // next entry of the surface list
-    uint32_t pad;
-};
-enum : uint32_t { WF_HASA = 1u, WF_HASB = 2u, WF_DONE = 4u, WF_PIX = 8u, WF_TRACED = 16u };
-enum : int {
-    WF_PSLOT = 0, WF_K, WF_DEPTH, WF_SEED, WF_RIDX, WF_ACC = 5, WF_ATT = 8, WF_COL = 11,
-    WF_FLAGS = 14, WF_RAYJ = 15, WF_AP = 16, WF_NEEC = 19, WF_NEED = 22, WF_BO = 23, WF_BD = 26,
-    WF_FIELDS = 29
-};
-constexpr uint32_t kWfShort = 16;           // LDS stack entries per trace lane
-constexpr uint32_t kWfTraceBlock = 256;
-constexpr uint32_t kWfGrab = 64;            // rays per wave grab
-#ifndef RVCP_WF_LEAF_CHUNK
-#define RVCP_WF_LEAF_CHUNK 2                // leaf triangles loaded together in the trace kernel
-#endif
-
-static_assert(sizeof(WfCounters) == kWfCountersBytes, "WfCounters layout (rvcp_internal.h)");
-static_assert(WF_FIELDS == (int)kWfStateFields, "slot state fields (rvcp_internal.h)");
-static_assert(kWfTraceBlock == kWfTraceThreads, "trace block (rvcp_internal.h)");
-static_assert(kBvhStack - (int)kWfShort == (int)kWfStackGlobal, "trace stack split (rvcp_internal.h)");
-
-__device__ __forceinline__ uint32_t wave_append(uint64_t M, uint32_t lane, uint32_t *ctr) {
-    // one atomic per wave: returns the base index of the wave's popc(M) appended entries
-    const int first = __builtin_ctzll(M);
-    uint32_t base = 0;
-    if ((int)lane == first) base = atomicAdd(ctr, (uint32_t)__builtin_popcountll(M));
-    return (uint32_t)__shfl((int)base, first);
-}
-
-__global__ __launch_bounds__(kBlock) void wf_shade_kernel(
-    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
-    const LightRecord *__restrict__ lights, float *__restrict__ lin,
-    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
-    const FaceShade *__restrict__ shade, float *__restrict__ st, uint32_t N, uint32_t gen,
-    WfCounters *__restrict__ wc, float4 *__restrict__ rays, const float2 *__restrict__ res)
-{
-    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
-    const uint32_t par = gen & 1u;
-    if (blockIdx.x == 0 && threadIdx.x == 0) wc->fetch[par] = 0u;
-    if (gen > 0 && *(volatile uint32_t *)&wc->alive[par ^ 1u] == 0u) return;   // frame finished
-    const uint32_t lane = lane_id();
-    const uint32_t wv = threadIdx.x / kWave;
-    const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
-    const bool live = slot < N;
-    const uint32_t n_surf = (uint32_t)(*(volatile unsigned long long *)&counters[3]);
-    const float sppf = (float)A.spp;
-    const float inv_spp = rcp_ieee(sppf);
-    float *const S = st + slot;                       // field f at S[f * N]
-    auto ldu = [&](int f) { return __float_as_uint(S[(size_t)f * N]); };
-    auto ld3f = [&](int f) { return mk(S[(size_t)f * N], S[(size_t)(f + 1) * N], S[(size_t)(f + 2) * N]); };
-    auto st3f = [&](int f, f3 v) { S[(size_t)f * N] = v.x; S[(size_t)(f + 1) * N] = v.y; S[(size_t)(f + 2) * N] = v.z; };
-
-    uint32_t flags = live ? ldu(WF_FLAGS) : WF_DONE;
-    bool done = (flags & WF_DONE) != 0u, have_pix = (flags & WF_PIX) != 0u;
-    bool hasA = (flags & WF_HASA) != 0u, hasB = (flags & WF_HASB) != 0u;
-    uint32_t pslot = 0, k = 0, depth = 0;
-    float seed = 0.0f, ridx = 0.0f, nee_dist = 0.0f;
-    f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
-    f3 a_o = mk(0, 0, 0), a_d = mk(0, 0, 1), a_p = mk(0, 0, 0), nee_C = mk(0, 0, 0);
-    f3 b_o = mk(0, 0, 0), b_d = mk(0, 0, 1);
-    if (have_pix) {
-        pslot = ldu(WF_PSLOT);
-        k = ldu(WF_K);
-        depth = ldu(WF_DEPTH);
-        seed = S[(size_t)WF_SEED * N];
-        ridx = S[(size_t)WF_RIDX * N];
-        acc = ld3f(WF_ACC);
-        att = ld3f(WF_ATT);
-        col = ld3f(WF_COL);
-        if (hasA) {
-            a_p = ld3f(WF_AP);
-            nee_C = ld3f(WF_NEEC);
-            nee_dist = S[(size_t)WF_NEED * N];
-        }
-        if (hasB) {
-            b_o = ld3f(WF_BO);
-            b_d = ld3f(WF_BD);
-        }
-    }
-    bool ended = false, surf_ev = false;
-    f3 S_pos = mk(0, 0, 0), S_nrm = mk(0, 0, 0), S_alb = mk(0, 0, 0);
-
-    // ---- the ray traced in the previous generation: resolve A (light sample) or B (bounce) ----
-    // the ray lists alternate by generation parity (this kernel appends to list `par` while
-    // it reads its slots' previous rays from list `par ^ 1`)
-    const float4 *__restrict__ prev_rays = rays + 2 * (size_t)N * (par ^ 1u);
-    float4 *__restrict__ next_rays = rays + 2 * (size_t)N * par;
-    if (flags & WF_TRACED) {
-        const uint32_t j = ldu(WF_RAYJ);
-        const float2 r = res[j];
-        const float bt = r.x;
-        const int best = __float_as_int(r.y);
-        if (hasA) {                                         // :447-459
-            const float4 ro = prev_rays[2 * j], rd = prev_rays[2 * j + 1];
-            a_o = mk(ro.x, ro.y, ro.z);
-            a_d = mk(rd.x, rd.y, rd.z);
-            const f3 hp = best >= 0 ? add(a_o, muls(a_d, bt))
-                                    : mk(__builtin_inff(), __builtin_inff(), __builtin_inff());
-            const float dist_blocked = len(sub(hp, a_p));
-            if (__builtin_fabsf(nee_dist - dist_blocked) < A.eps) col = add(col, nee_C);
-        }
-        const bool defer_B = hasA && hasB;                  // B was not traced
-        if (hasB && !defer_B) {                             // :421-429
-            if (best < 0) {
-                col = add(col, mk(0.1f, 0.1f, 0.1f));
-                ended = true;
-            } else {
-                f3 hpos, hn;
-                FaceShade fs;
-                hit_shade(tri, shade, best, b_o, b_d, bt, hpos, hn, fs);
-                if (fs.ty == kLight) {
-                    ended = true;
-                } else {
-                    S_pos = hpos; S_nrm = hn; S_alb = ld3(fs.alb_pi);
-                    surf_ev = true;
-                }
-            }
-        } else if (hasA && !hasB) {
-            ended = true;
-        }
-        hasA = false;
-        if (!defer_B) hasB = false;
-    }
-
-    // ---- settle: end samples, take pixels, emit surface events (path_body's) ----
-    for (;;) {
-        if (ended) {                                        // color += L / SPP (:495)
-            ended = false;
-            acc = add(acc, divs_y(col, sppf, inv_spp));
-            k += 1;
-            if (k >= A.spp) {
-                store_acc(surf[pslot].pix, acc, lin);
-                have_pix = false;
-            } else {
-                depth = 0;
-                att = mk(1, 1, 1);
-                col = mk(0, 0, 0);
-                const SurfRecord r = surf[pslot];
-                S_pos = ld3(r.pos); S_nrm = ld3(r.nrm); S_alb = ld3(r.alb_pi);
-                surf_ev = true;
-            }
-        }
-        {   // new pixels from the surface list
-            const bool need = live && !have_pix && !done;
-            const uint64_t M = __ballot(need);
-            if (M) {
-                const uint32_t base = wave_append(M, lane, &wc->pix_next);
-                if (need) {
-                    const uint32_t idx = base + rank_in(M);
-                    if (idx < n_surf) {
-                        const SurfRecord r = surf[idx];
-                        pslot = idx;
-                        seed = r.seed;
-                        ridx = 0.0f;
-                        k = 0;
-                        acc = mk(0, 0, 0);
-                        depth = 0;
-                        att = mk(1, 1, 1);
-                        col = mk(0, 0, 0);
-                        S_pos = ld3(r.pos); S_nrm = ld3(r.nrm); S_alb = ld3(r.alb_pi);
-                        have_pix = true;
-                        surf_ev = true;
-                    } else {
-                        done = true;
-                    }
-                }
-            }
-        }
-        bool need_dir = false;
-        if (surf_ev) {                                      // :431-462
-            surf_ev = false;
-            f3 ws;
-            if (nee_sample(A, lights, S_alb, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist, ws)) {
-                a_o = add(S_pos, muls(ws, A.eps));
-                a_d = ws;
-                a_p = S_pos;
-                hasA = true;
-            }
-            need_dir = !(rnd(seed, ridx) > A.rr);           // Russian roulette :462
-            if (!need_dir && !hasA) ended = true;
-        }
-        f3 p = mk(0, 0, 0);
-        coop_unit_sphere(need_dir, seed, ridx, p, lane, tail_tab[wv]);
-        if (need_dir) {                                     // :464-478
-            f3 wi;
-            brdf_finish(A, S_alb, S_nrm, p, att, wi);
-            depth += 1;
-            if (!(depth >= A.max_bounces || att_stop(A, att))) {
-                b_o = add(S_pos, muls(wi, A.eps));
-                b_d = wi;
-                hasB = true;
-            }
-            if (!hasA && !hasB) ended = true;
-        }
-        if (!__any(ended)) break;
-    }
-
-    // ---- this generation's ray: the light sample while pending, else the bounce ----
-    const bool sA = hasA || hasB;
-    const uint64_t M = __ballot(sA);
-    uint32_t j = 0;
-    if (M) {
-        const uint32_t base = wave_append(M, lane, &wc->n_rays[par]);
-        if (sA) {
-            j = base + rank_in(M);
-            const f3 o = hasA ? a_o : b_o, d = hasA ? a_d : b_d;
-            next_rays[2 * j] = make_float4(o.x, o.y, o.z, 0.0f);
-            next_rays[2 * j + 1] = make_float4(d.x, d.y, d.z, 0.0f);
-        }
-        if (lane == 0) {
-            atomicAdd(&counters[0], (unsigned long long)__builtin_popcountll(M));
-            atomicAdd(&counters[2], 1ull);
-        }
-    }
-    const uint64_t L = __ballot(live && !done);
-    if (L) (void)wave_append(L, lane, &wc->alive[par]);
-    if (!live) return;
-    S[(size_t)WF_FLAGS * N] = __uint_as_float((hasA ? WF_HASA : 0u) | (hasB ? WF_HASB : 0u) |
-                                              (done ? WF_DONE : 0u) | (have_pix ? WF_PIX : 0u) |
-                                              (sA ? WF_TRACED : 0u));
-    if (!have_pix) return;
-    S[(size_t)WF_PSLOT * N] = __uint_as_float(pslot);
-    S[(size_t)WF_K * N] = __uint_as_float(k);
-    S[(size_t)WF_DEPTH * N] = __uint_as_float(depth);
-    S[(size_t)WF_SEED * N] = seed;
-    S[(size_t)WF_RIDX * N] = ridx;
-    S[(size_t)WF_RAYJ * N] = __uint_as_float(j);
-    st3f(WF_ACC, acc);
-    st3f(WF_ATT, att);
-    st3f(WF_COL, col);
-    if (hasA) {
-        st3f(WF_AP, a_p);
-        st3f(WF_NEEC, nee_C);
-        S[(size_t)WF_NEED * N] = nee_dist;
-    }
-    if (hasB) {
-        st3f(WF_BO, b_o);
-        st3f(WF_BD, b_d);
-    }
-}
-
-__global__ __launch_bounds__(kWfTraceBlock) void wf_trace_kernel(
-    const Bvh4Node *__restrict__ nodes, const TriRecord *__restrict__ btri, int32_t root,
-    uint32_t n4, uint32_t slots, const float4 *__restrict__ rays, float2 *__restrict__ res,
-    uint32_t gen, WfCounters *__restrict__ wc, float tmin, float tmax, int32_t *__restrict__ gstk)
-{
-    __shared__ int32_t stk[kWfShort * kWfTraceBlock];
-    const uint32_t par = gen & 1u;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {     // the next generation's lists start empty
-        wc->n_rays[par ^ 1u] = 0u;
-        wc->alive[par ^ 1u] = 0u;
-    }
-    const uint32_t n = *(volatile uint32_t *)&wc->n_rays[par];
-    if (n == 0u) return;
-    const uint32_t lane = lane_id();
-    lds_i32 *const ls = (lds_i32 *)stk + threadIdx.x;            // ls[i * kWfTraceBlock]
-    int32_t *const gs = gstk + ((size_t)blockIdx.x * kWfTraceBlock + threadIdx.x) *
-                                   (uint32_t)(kBvhStack - (int)kWfShort);
-    const Bvh4QNode *__restrict__ qn = reinterpret_cast<const Bvh4QNode *>(nodes + n4);
-    uint32_t wnext = 0, wend = 0;      // this wave's grabbed range of the ray list (uniform)
-    bool wex = false;                  // the list is used up
-    bool has = false;
-    uint32_t j = 0;
-    f3 o = mk(0, 0, 0), d = mk(0, 0, 1), inv = mk(1, 1, 1);
-    bool px = true, py = true, pz = true;
-    int32_t ref = 0;
-    int sp = 0;
-    float bt = tmax;
-    int best = -1;
-    for (;;) {
-        const uint64_t M = __ballot(!has);
-        if (M && !wex) {
-            if (wnext >= wend) {
-                uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(&wc->fetch[par], kWfGrab);
-                b = (uint32_t)__shfl((int)b, 0);
-                if (b >= n) {
-                    wex = true;
-                } else {
-                    wnext = b;
-                    wend = b + kWfGrab < n ? b + kWfGrab : n;
-                }
-            }
-            const uint32_t avail = wex ? 0u : wend - wnext;
-            if (!has) {
-                const uint32_t r = rank_in(M);
-                if (r < avail) {
-                    j = wnext + r;
-                    const float4 a = rays[2 * j], b = rays[2 * j + 1];
-                    o = mk(a.x, a.y, a.z);
-                    d = mk(b.x, b.y, b.z);
-                    inv = slab_inv(d);
-                    px = inv.x >= 0.0f; py = inv.y >= 0.0f; pz = inv.z >= 0.0f;
-                    ref = root;
-                    sp = 0;
-                    bt = tmax;
-                    best = -1;
-                    has = true;
-                }
-            }
-            const uint32_t took = (uint32_t)__builtin_popcountll(M);
-            wnext += took < avail ? took : avail;
-        }
-        if (!__any(has)) {
-            if (wex) break;
-            continue;
-        }
-        if (has) {
-            bool fin = false;
-            if (ref >= 0) {
-                const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
-                const float4 w0 = q[0], w1 = q[1], w2 = q[2];
-                const int4 r = reinterpret_cast<const int4 *>(qn + ref)[3];
-                const float ax = w0.w * inv.x, ay = w1.x * inv.y, az = w1.y * inv.z;
-                const float bx = (w0.x - o.x) * inv.x, by = (w0.y - o.y) * inv.y, bz = (w0.z - o.z) * inv.z;
-                const uint32_t lx = __float_as_uint(w1.z), ly = __float_as_uint(w1.w), lz = __float_as_uint(w2.x);
-                const uint32_t hx = __float_as_uint(w2.y), hy = __float_as_uint(w2.z), hz = __float_as_uint(w2.w);
-                const uint32_t nx = px ? lx : hx, fx = px ? hx : lx;
-                const uint32_t ny = py ? ly : hy, fy = py ? hy : ly;
-                const uint32_t nz = pz ? lz : hz, fz = pz ? hz : lz;
-                float kk[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float tn = __builtin_fmaxf(
-                        __builtin_fmaxf(__builtin_fmaf(ubyte_f(nx, c), ax, bx), __builtin_fmaf(ubyte_f(ny, c), ay, by)),
-                        __builtin_fmaxf(__builtin_fmaf(ubyte_f(nz, c), az, bz), tmin));
-                    const float tf = __builtin_fminf(
-                        __builtin_fminf(__builtin_fmaf(ubyte_f(fx, c), ax, bx), __builtin_fmaf(ubyte_f(fy, c), ay, by)),
-                        __builtin_fminf(__builtin_fmaf(ubyte_f(fz, c), az, bz), bt));
-                    kk[c] = tn <= tf ? tn : __builtin_inff();
-                }
-                float k0 = kk[0], k1 = kk[1], k2 = kk[2], k3 = kk[3];
-                int32_t c0 = r.x, c1 = r.y, c2 = r.z, c3 = r.w;
-                bvh4_cas(k0, c0, k1, c1);
-                bvh4_cas(k2, c2, k3, c3);
-                bvh4_cas(k0, c0, k2, c2);
-                bvh4_cas(k1, c1, k3, c3);
-                bvh4_cas(k1, c1, k2, c2);
-                const float inf = __builtin_inff();
-                auto push = [&](int32_t c) {
-                    if (sp < (int)kWfShort) ls[sp * kWfTraceBlock] = c;
-                    else gs[sp - (int)kWfShort] = c;
-                    sp += 1;
-                };
-                if (k3 < inf) push(c3);
-                if (k2 < inf) push(c2);
-                if (k1 < inf) push(c1);
-                if (k0 < inf) {
-                    ref = c0;
-                } else if (sp == 0) {
-                    fin = true;
-                } else {
-                    sp -= 1;
-                    ref = sp < (int)kWfShort ? ls[sp * kWfTraceBlock] : gs[sp - (int)kWfShort];
-                }
-            } else {
-                bvh_leaf<RVCP_WF_LEAF_CHUNK>(btri, ref, o, d, tmin, bt, best, slots);
-                if (sp == 0) {
-                    fin = true;
-                } else {
-                    sp -= 1;
-                    ref = sp < (int)kWfShort ? ls[sp * kWfTraceBlock] : gs[sp - (int)kWfShort];
-                }
-            }
-            if (fin) {
-                res[j] = make_float2(bt, __int_as_float(best));
-                has = false;
-            }
-        }
-    }
 }
 
 __global__ void fill_kernel(uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
@@ -2703,9 +2178,6 @@ __device__ __forceinline__ float fresnel_schlick(float cosine, float ratio) {
 // NaN), so with t_min >= 2^-29 and t_max < 2^29 both are rejected, and the root order of the
 // swap differs at most between two rejected roots: the decision and the accepted t are the
 // IEEE ones.  The caller checks the ranges per wave.
-#ifndef RVCP_SPHERE_SKIP
-#define RVCP_SPHERE_SKIP 1
-#endif
 __device__ __forceinline__ float quot_markstein(float x, float s, float y) {
     const float q = x * y;
     return __builtin_fmaf(__builtin_fmaf(-s, q, x), y, q);
@@ -2718,12 +2190,10 @@ __device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d
     const float b = 2.0f * dot(d, co);
     const float c = dot(co, co) - S.radius * S.radius;
     const float delta = b * b - 4.0f * a * c;
-#if RVCP_SPHERE_SKIP
     // no lane's line meets the sphere (delta < 0 or NaN everywhere): every lane rejects it
     // below (!(delta < 0) fails, or NaN roots fail the compares), so the wave skips the
     // square root, the roots and the compares
     if (!__any(delta >= 0.0f)) { t_out = bt; return false; }
-#endif
     const float sq = __builtin_sqrtf(delta);
     float t0 = FAST ? quot_markstein(-b + sq, two_a, y) : (-b + sq) / two_a;
     float t1 = FAST ? quot_markstein(-b - sq, two_a, y) : (-b - sq) / two_a;
@@ -2736,12 +2206,10 @@ __device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d
 
 constexpr int L_IDLE = 0, L_TRACE = 1, L_SCATTER = 2, L_END = 3;
 
-// RVCP_LEGACY_DEFER: the most lanes left ending a sample that sit out one trace (below).  16
+// kLegacyDefer: the most lanes left ending a sample that sit out one trace (below).  16
 // measured best: sphere room 0.367 -> 0.345 ms, mode 2 on the C3 frame 2.237 -> 2.156 ms per
 // frame (profiles/r03v_m2_defer_sweep.log; 8, 24, 32, 40 and 64 less good).
-#ifndef RVCP_LEGACY_DEFER
-#define RVCP_LEGACY_DEFER 16
-#endif
+constexpr int kLegacyDefer = 16;
 
 }  // namespace
 
@@ -2876,13 +2344,11 @@ __device__ __forceinline__ void legacy_body(
                 }
             }
             if (!__any(st == L_END)) break;
-#if RVCP_LEGACY_DEFER
             // Lanes whose sample ended in this scatter (bounce limit) sit out one trace when
             // few of them did and other lanes have rays: their next sample's scatter then runs
             // inside the next settle with the whole wave's instead of in a nearly empty pass
             // now.  Timing only: each lane's own sequence of operations is unchanged.
-            if (__any(st == L_TRACE) && __popcll(__ballot(st == L_END)) <= RVCP_LEGACY_DEFER) break;
-#endif
+            if (__any(st == L_TRACE) && __popcll(__ballot(st == L_END)) <= kLegacyDefer) break;
         }
         if (!__any(st == L_TRACE)) break;
         iters += 1;
@@ -2892,10 +2358,7 @@ __device__ __forceinline__ void legacy_body(
         float bt = rtmax;
         const float a = dot(rd, rd), two_a = 2.0f * a;
         // the sphere roots by Markstein quotients when every tracing lane is in range (above)
-#ifndef RVCP_SPHERE_MARKSTEIN
-#define RVCP_SPHERE_MARKSTEIN 1
-#endif
-        const bool fast = RVCP_SPHERE_MARKSTEIN && A.t_max < 0x1p29f &&
+        const bool fast = A.t_max < 0x1p29f &&
                           __all(st != L_TRACE || ((two_a >= 0x1p-30f) & (two_a <= 0x1p30f) &
                                                   (rtmin >= 0x1p-29f)));
 #ifdef RVCP_SPEC_SCAN
@@ -3025,7 +2488,7 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
 // Scene-specialised path kernels (rvcp_jit.cpp compiles this file with hipRTC, RVCP_JIT and
 // RVCP_SPEC_SCAN set): schedules 3 and 6 with the scan unrolled over the uploaded scene
 // (DESIGN.md §4.7).  extern "C" so that the host finds them by name in the module.
-extern "C" __global__ __launch_bounds__(kBlock, RVCP_PATH_MIN_WAVES) void rvcp_spec_path_kernel5(
+extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_path_kernel5(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
     uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
@@ -3121,7 +2584,7 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_f
                            out_lin, counters, surf, shade);
     else
         hipLaunchKernelGGL(args->variant == 6 ? rvcp::games101_path_kernel<6>
-                                              : rvcp::games101_path_kernel<RVCP_PATH_MIN_WAVES>,
+                                              : rvcp::games101_path_kernel<rvcp::kPathMinWaves>,
                            dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, mats, lights, gamma_t, out_rgba,
                            out_lin, counters, surf, shade);
@@ -3134,75 +2597,6 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_f
     hipLaunchKernelGGL(rvcp::tonemap_kernel, dim3(tb), dim3(rvcp::kToneBlock), 0, (hipStream_t)stream,
                        out_lin, n_tone, gamma_t, out_rgba);
     return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-// Opt-in BVH, wavefront form: pre-pass, then shade / trace generations until no slot has work
-// left, then the tone map.  Blocks the calling thread until the frame's last generation is
-// queued (the loop reads the live-slot count of a batch while the next batch runs).
-extern "C" int rvcp_launch_bvh_wavefront(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
-                                         const void *faces, const void *verts,
-                                         const rvcp::MatRecord *mats,
-                                         const rvcp::LightRecord *lights, const float *gamma_t,
-                                         uint32_t *out_rgba, float *out_lin,
-                                         unsigned long long *counters, rvcp::SurfRecord *surf,
-                                         const rvcp::FaceShade *shade,
-                                         const rvcp::Bvh4Node *bvh_nodes,
-                                         const rvcp::TriRecord *bvh_tris, void *stream,
-                                         void *main_event, const rvcp::WfBuffers *wb)
-{
-    hipStream_t s = (hipStream_t)stream;
-    const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
-    hipLaunchKernelGGL(rvcp::games101_primary_kernel<true>, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
-                       s, *args, tri, (const rvcp_face_t *)faces, (const rvcp_vertex_t *)verts, mats,
-                       gamma_t, out_rgba, out_lin, counters, surf, shade, bvh_nodes, bvh_tris);
-    if (main_event && hipEventRecord((hipEvent_t)main_event, s) != hipSuccess) return -2;
-    const uint32_t N = wb->n_slots;
-    rvcp::WfCounters *wc = (rvcp::WfCounters *)wb->counters;
-    if (hipMemsetAsync(wc, 0, sizeof(rvcp::WfCounters), s) != hipSuccess) return -2;
-    if (hipMemsetAsync(wb->st + (size_t)rvcp::WF_FLAGS * N, 0, (size_t)N * 4, s) != hipSuccess) return -2;
-    const uint32_t shade_blocks = (N + rvcp::kBlock - 1) / rvcp::kBlock;
-    float4 *rays = (float4 *)wb->rays;
-    float2 *res = (float2 *)wb->res;
-    // generations: a slot spends at most 2 per bounce plus a few per sample, and takes pixels
-    // until the list is empty; the cap only stops a runaway loop
-    const uint64_t per_pixel = (uint64_t)args->spp * (2ull * args->max_bounces + 4ull) + 8ull;
-    const uint64_t cap = per_pixel * ((args->n_pixels + N - 1) / N + 1) + 64ull;
-    constexpr uint32_t kBatch = 8;
-    for (uint32_t g0 = 0, it = 0;; g0 += kBatch, ++it) {
-        for (uint32_t g = g0; g < g0 + kBatch; ++g) {
-            hipLaunchKernelGGL(rvcp::wf_shade_kernel, dim3(shade_blocks), dim3(rvcp::kBlock), 0, s,
-                               *args, tri, mats, lights, out_lin, counters, surf, shade, wb->st, N, g,
-                               wc, rays, (const float2 *)res);
-            hipLaunchKernelGGL(rvcp::wf_trace_kernel, dim3(wb->trace_blocks), dim3(rvcp::kWfTraceBlock), 0, s,
-                               bvh_nodes, bvh_tris, args->bvh_root, args->bvh_n4, args->bvh_slots,
-                               (const float4 *)(rays + 2 * (size_t)N * (g & 1u)), res, g, wc,
-                               args->t_min, args->t_max, wb->gstk);
-        }
-        if (hipGetLastError() != hipSuccess) return -2;
-        const uint32_t last = (g0 + kBatch - 1) & 1u;
-        if (hipMemcpyAsync(&wb->pinned[it & 1u], &wc->alive[last], 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipEventRecord((hipEvent_t)wb->ev[it & 1u], s) != hipSuccess)
-            return -2;
-        if (it > 0) {
-            if (hipEventSynchronize((hipEvent_t)wb->ev[(it - 1) & 1u]) != hipSuccess) return -2;
-            if (wb->pinned[(it - 1) & 1u] == 0u) break;
-        }
-        if (g0 > cap) return -3;
-    }
-    uint32_t tb = (args->n_pixels + rvcp::kToneBlock - 1) / rvcp::kToneBlock;
-    if (tb > 8192u) tb = 8192u;
-    hipLaunchKernelGGL(rvcp::tonemap_kernel, dim3(tb), dim3(rvcp::kToneBlock), 0, s,
-                       out_lin, args->n_pixels, gamma_t, out_rgba);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-extern "C" int rvcp_wf_trace_occupancy(int *blocks_per_cu)
-{
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::wf_trace_kernel, rvcp::kWfTraceBlock, 0) != hipSuccess)
-        return -2;
-    *blocks_per_cu = b;
-    return 0;
 }
 
 extern "C" void rvcp_static_split(uint32_t n, uint32_t grid_waves, uint32_t n_simds,
@@ -3244,7 +2638,7 @@ extern "C" int rvcp_games101_occupancy(int variant, int *blocks_per_cu)
         : variant == 6
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel<6>, rvcp::kBlock, 0)
         : variant == 3
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel<RVCP_PATH_MIN_WAVES>, rvcp::kBlock, 0)
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_path_kernel<rvcp::kPathMinWaves>, rvcp::kBlock, 0)
         : variant == 2
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_dual_kernel, rvcp::kBlock, 0)
         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rvcp::games101_kernel, rvcp::kBlock, 0);

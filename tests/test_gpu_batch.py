@@ -123,13 +123,6 @@ def test_batch_refused_where_unsupported(cornell):
             # a batch of one is rvcp_render_shard_async
             rt.render_frames_async(push[:1], 32, 32, 0, 1, out.data_ptr())
             rt.sync_stats()
-    # the BVH wavefront form (schedule 9) has one slot state per pixel of one frame
-    sc = rvcp_amd.scene.with_random_triangles(cornell, 100)
-    with rvcp_amd.RayTracer(spp=2, accel=rvcp_amd.abi.ACCEL_BVH, kernel_variant=9) as rt:
-        rt.upload_scene(sc)
-        with pytest.raises(rvcp_amd.abi.RvcpError) as e:
-            rt.render_frames_async(push, 32, 32, 0, 1, out.data_ptr())
-        assert e.value.code == rvcp_amd.abi.RVCP_E_UNSUPPORTED
 
 
 def test_batch_with_rccl_gathers(cornell):

@@ -107,17 +107,3 @@ def test_bvh_full_c3_identical(cornell):
     a = _render(cornell, 1024, 1024, 123.0, spp=30)
     b = _render(cornell, 1024, 1024, 123.0, spp=30, accel=rvcp_amd.abi.ACCEL_BVH)
     assert np.array_equal(a[0], b[0])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("W,H,spp", [(96, 80, 4), (1024, 768, 2)])
-def test_bvh_wavefront_schedule_identical(cornell, W, H, spp):
-    """Schedule 9 (the BVH path in wavefront form: shade / trace kernel generations, slot
-    state in HBM) renders the persistent BVH kernel's frame bit for bit -- 1024x768 has more
-    surface pixels than the 2^19 path slots, so slots take several pixels."""
-    a = _render(cornell, W, H, 9.0, spp=spp, accel=rvcp_amd.abi.ACCEL_BVH)
-    b = _render(cornell, W, H, 9.0, spp=spp, accel=rvcp_amd.abi.ACCEL_BVH, kernel_variant=9)
-    assert int(b[2]["kernel_variant"]) == 9 and int(a[2]["kernel_variant"]) == 7
-    assert np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32))
-    assert np.array_equal(a[0], b[0])
-    assert int(a[2]["traversals_executed"]) == int(b[2]["traversals_executed"])

@@ -83,7 +83,8 @@ def test_rotated_c3_rows_specialised_equals_generic_and_oracle(rotated):
     for spec in (rvcp_amd.abi.SPECIALIZE_AUTO, rvcp_amd.abi.SPECIALIZE_OFF):
         with rvcp_amd.RayTracer(spp=30, specialize=spec) as rt:
             rt.upload_scene(rotated)
-            frames.append(rt.render(W, H, 123.0)[0])
+            rgba, _ = rt.render(W, H, 123.0, want_linear=True)
+            frames.append(rgba)
     assert np.array_equal(frames[0], frames[1])
     cfg = rvcp_amd.abi.make_config(spp=30)
     for y in (0, 9, 130, 515, 766, 1023):

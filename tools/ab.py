@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Same-box A/B driver: every measurement of a variant against another runs through this.
+
+A case is `label=ENV=v,ENV2=w::runner args`: the environment it runs with (RVCP_LIB to pick a
+library build -- tools/build_variant.sh builds variants, the debug build holds the
+experiment knobs; RVCP_JIT_FLAGS for hipRTC -D options of the specialised module), and the
+arguments of the runner.  Cases run interleaved, pass after pass, each under its own time
+limit; one line per (pass, case), then the median per case.
+
+Runners:
+  bench     python bench.py --no-cpu-baseline --launch-pass 0 --steps 40 --warmup 5 ARGS
+            (ms_per_step, the driver's figure: frames in flight and batches as the bench
+            picks them unless ARGS fix them)
+  frames    python tools/frames.py --frames 20 ARGS  (one frame at a time, path-kernel ms:
+            median of the frames after the first 3)
+  share     python tools/rank_share.py ARGS  (rank 0's share of the N-GPU C4 frame alone)
+
+  python tools/ab.py --runner bench --passes 2 \\
+      "base=::--workload c3" "v2=RVCP_LIB=tools/build/var_v2/librvcp.so::--workload c3"
+  python tools/ab.py --runner frames "s3=::--variant 3" "s10=::--variant 10 --tris 2000"
+"""
+import argparse
+import json
+import os
+import shlex
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RUNNERS = {
+    "bench": [sys.executable, "bench.py", "--no-cpu-baseline", "--launch-pass", "0",
+              "--steps", "40", "--warmup", "5"],
+    "frames": [sys.executable, "tools/frames.py", "--frames", "20"],
+    "share": [sys.executable, "-u", "tools/rank_share.py"],
+}
+
+
+def parse_case(text):
+    label, _, rest = text.partition("=")
+    envs, _, args = rest.partition("::")
+    env = {}
+    for kv in filter(None, envs.split(",")):
+        k, _, v = kv.partition("=")
+        env[k] = v
+    return label, env, shlex.split(args)
+
+
+def measure(runner, out):
+    """The case's figure from the runner's stdout (ms)."""
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if runner == "bench":
+        return json.loads(lines[-1])["ms_per_step"]
+    if runner == "frames":
+        ms = sorted(json.loads(l)["kernel_ms"] for l in lines[3:] or lines)
+        return ms[len(ms) // 2]
+    vals = [json.loads(l).get("ms_per_frame") for l in lines]
+    return [v for v in vals if v is not None][-1]
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--runner", choices=sorted(RUNNERS), default="bench")
+    ap.add_argument("--passes", type=int, default=2)
+    ap.add_argument("--timeout", type=int, default=200)
+    ap.add_argument("cases", nargs="+")
+    a = ap.parse_args()
+    cases = [parse_case(c) for c in a.cases]
+    got = {label: [] for label, _, _ in cases}
+    for p in range(1, a.passes + 1):
+        for label, env, args in cases:
+            cmd = ["timeout", "-k", "10", str(a.timeout)] + RUNNERS[a.runner] + args
+            r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, **env), capture_output=True,
+                               text=True)
+            if r.returncode != 0:
+                print(f"pass {p} {label:>24}  FAILED rc={r.returncode}: {r.stderr[-400:]}", flush=True)
+                if r.returncode >= 124:      # time limit / signal: stop here
+                    sys.exit(r.returncode)
+                continue
+            v = measure(a.runner, r.stdout)
+            got[label].append(v)
+            print(f"pass {p} {label:>24}  {v:.4f} ms", flush=True)
+    for label, vals in got.items():
+        if vals:
+            print(f"median {label:>24}  {statistics.median(vals):.4f} ms  (n={len(vals)}, "
+                  f"min {min(vals):.4f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()

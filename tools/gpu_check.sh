@@ -80,6 +80,8 @@ for s in $STEPS; do
         rehearse8c4b) run rehearse8c4b 500 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29539 bench.py --gpus 8 --workload c4 --steps 20 --warmup 4 ;;
         rehearse2) run rehearse2 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
         frames) run frames 300 python tools/frames.py --frames 20 ;;
+        # schedules 4 / 10 on meshes (tools/ab.py, one frame at a time)
+        c5pool) run c5pool 900 python tools/ab.py --runner frames "s4=::--variant 4 --tris 2000 --size 1024 --spp 8 --frames 6" "s10=::--variant 10 --tris 2000 --size 1024 --spp 8 --frames 6" ;;
         pipeline) run pytest_pipeline 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_bench.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         benchrot) run bench_c3rot 300 python bench.py --workload c3rot --steps 30 --warmup 5 --no-cpu-baseline ;;
         benchgen) run bench_c3gen 300 python bench.py --workload c3gen --steps 30 --warmup 5 --no-cpu-baseline ;;
@@ -88,8 +90,6 @@ for s in $STEPS; do
         # the driver's N>1 form without a launcher (bench.self_launch), one-GPU rehearsal
         selfl2) run selfl2 300 env RVCP_BENCH_REHEARSAL=1 python bench.py --gpus 2 --steps 10 --warmup 2 ;;
         selfl8) run selfl8 500 env RVCP_BENCH_REHEARSAL=1 python bench.py --gpus 8 --steps 10 --warmup 2 ;;
-        poolab) run poolab 600 bash tools/sched_ab.sh "3 9" "--frames 20" "--size 384 --spp 10 --frames 40" "--size 2048 --spp 64 --frames 6" "--size 128 --spp 30 --frames 40" ;;
-        c5pool) run c5pool 900 bash tools/sched_ab.sh "${VARS:-4 10}" "--tris 100000 --size 512 --spp 4 --frames 5" "--tris 2000 --size 1024 --spp 8 --frames 6" "--tris 300 --size 1024 --spp 8 --frames 8" ;;
         c5tests) run c5tests 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "c5 or multi_tile or odd_remainder or variants or bitexact_cornell" ;;
         pooltests) run pooltests 600 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         *) echo "unknown step $s"; exit 2 ;;
