@@ -682,6 +682,13 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     A.n_lights = ctx->n_lights;
     A.light_total = ctx->light_total;
     A.light_pdf = ctx->light_pdf;
+    {   // :465-471: denom = max(0.1, pdf) * rr, pdf = 0.5 / 3.1415926 (cos > 0) or 0; IEEE 1/denom
+        const float pdf1 = 0.5f / 3.1415926f;
+        A.brdf_den[1] = std::fmax(0.1f, pdf1) * A.rr;
+        A.brdf_den[0] = std::fmax(0.1f, 0.0f) * A.rr;
+        A.brdf_rcp[1] = 1.0f / A.brdf_den[1];
+        A.brdf_rcp[0] = 1.0f / A.brdf_den[0];
+    }
     A.want_linear = d_linear_rgb ? 1u : 0u;
     // automatic schedule: 10 / 5 (LDS tiles; the workgroup's rays pooled into full passes on
     // large frames, one ray per lane on small ones) for large meshes, 10 also for mid-size

@@ -195,6 +195,10 @@ struct FrameArgs {
     float att_stop, t_min, t_max, rr, eps;
     uint32_t n_faces, n_lights;
     float light_total, light_pdf;
+    // the BRDF update's divisor max(0.1, pdf) * rr (:465-471) for pdf = 1/(2 pi) (cos > 0) and
+    // pdf = 0, and their IEEE reciprocals: frame constants, so the update divides by a known
+    // reciprocal (divs_y) instead of computing rcp_ieee per event
+    float brdf_den[2], brdf_rcp[2];
     uint32_t static_chunks;  // pixels handed out statically (one chunk per wave)
     uint32_t static_chunk;   // pixels of each wave's static chunk (<= kChunk)
     uint32_t n_simds;        // SIMDs of the device (CUs x 4), for static_split

@@ -263,8 +263,14 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     else if (!b2.empty()) add("(" + b2 + " <= 1.0f)");
     add("(" + t + " >= tmin)");
     decl += g.out;
-    accept += "        if (" + cond + " & (" + t + " <= bt" + R + ")) { bt" + R + " = " + t + "; best" + R +
-              " = " + std::to_string(index) + "; }\n";
+    // the dual scan's shadow ray (slot A) needs the nearest t and whether there was a hit, not
+    // the face: only its t is kept (btA != t_max after the scan means a hit;
+    // the caller resolves btA == t_max, a miss or a hit at exactly t_max, with the generic scan)
+    if (R == "A")
+        accept += "        if (" + cond + " & (" + t + " <= btA)) btA = " + t + ";\n";
+    else
+        accept += "        if (" + cond + " & (" + t + " <= bt" + R + ")) { bt" + R + " = " + t + "; best" +
+                  R + " = " + std::to_string(index) + "; }\n";
     return true;
 }
 
@@ -299,8 +305,12 @@ void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *c
             continue;
         }
         out += decl + "    {\n" + accept + "    }\n";
-        for (int r = 0; r < n_rays; r++)
-            if (used[r]) out += "    RVCP_SPEC_COMMIT(bt" + std::string(rays[r]) + ", best" + std::string(rays[r]) + ");\n";
+        for (int r = 0; r < n_rays; r++) {
+            if (!used[r]) continue;
+            const std::string R(rays[r]);
+            out += R == "A" ? "    RVCP_SPEC_COMMIT1(btA);\n"
+                            : "    RVCP_SPEC_COMMIT(bt" + R + ", best" + R + ");\n";
+        }
     }
 }
 
@@ -332,7 +342,7 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n)
     emit_scan(out, tri, n, one, 1, RVCP_SPEC_GROUP1);
     out += "}\n";
     out += "__device__ __forceinline__ void spec_scan2(f3 oA, f3 dA, f3 oB, f3 dB, float tmin, "
-           "float &btA, int &bestA, float &btB, int &bestB) {\n";
+           "float &btA, float &btB, int &bestB) {\n";
     emit_scan(out, tri, n, two, 2, RVCP_SPEC_GROUP2);
     out += "}\n";
     return out;
@@ -418,10 +428,10 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
         err = api.why;
         return -1;
     }
-    const char *hdr_src[] = {kJitSrcInternal, kJitSrcAbi, scan.c_str()};
-    const char *hdr_name[] = {"rvcp_internal.h", "../../include/rvcp.h", "rvcp_spec_scan.inc"};
+    const char *hdr_src[] = {kJitSrcInternal, kJitSrcAbi, kJitSrcSqrt, scan.c_str()};
+    const char *hdr_name[] = {"rvcp_internal.h", "../../include/rvcp.h", "rvcp_sqrt.h", "rvcp_spec_scan.inc"};
     rtc_program prog = nullptr;
-    if (api.create(&prog, kJitSrcKernels, "rvcp_kernels.hip", 3, hdr_src, hdr_name) != 0) {
+    if (api.create(&prog, kJitSrcKernels, "rvcp_kernels.hip", 4, hdr_src, hdr_name) != 0) {
         err = "hiprtcCreateProgram failed";
         return -1;
     }

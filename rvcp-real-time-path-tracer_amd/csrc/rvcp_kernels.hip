@@ -30,6 +30,7 @@
 
 #include "rvcp_internal.h"
 #include "../../include/rvcp.h"
+#include "rvcp_sqrt.h"
 
 namespace rvcp {
 namespace {
@@ -55,10 +56,16 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
               __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
 }
-__device__ __forceinline__ float len(f3 a) { return __builtin_sqrtf(dot(a, a)); }
+// The IEEE square root: rvcp_sqrt.h's 5-instruction form (checked on all 2^32 inputs) or the
+// compiler's correctly-rounded sequence (A/B)
+#ifndef RVCP_FAST_SQRT
+#define RVCP_FAST_SQRT 0
+#endif
+__device__ __forceinline__ float sqrt_c(float x) { return RVCP_FAST_SQRT ? sqrt_ieee(x) : __builtin_sqrtf(x); }
+__device__ __forceinline__ float len(f3 a) { return sqrt_c(dot(a, a)); }
 // 1 / sqrt by rcp_ieee below (the IEEE quotient, fast path verified over all inputs)
 __device__ __forceinline__ float rcp_ieee(float den);
-__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, rcp_ieee(__builtin_sqrtf(dot(a, a)))); }
+__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, rcp_ieee(sqrt_c(dot(a, a)))); }
 __device__ __forceinline__ float fractf(float x) { return x - __builtin_floorf(x); }
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 
@@ -249,11 +256,29 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
 // interleaves all unrolled tests and spills hundreds of registers
 #define RVCP_SPEC_COMMIT(t, i) do { asm volatile("" : "+v"(t), "+v"(i)); \
                                     __builtin_amdgcn_sched_barrier(0); } while (0)
+// the dual scan's shadow ray: its t only (spec_scan2 keeps no face index for slot A)
+#define RVCP_SPEC_COMMIT1(t) do { asm volatile("" : "+v"(t)); \
+                                  __builtin_amdgcn_sched_barrier(0); } while (0)
 // The reciprocal of the specialised tests: rcp_scan, with its rare IEEE branch inline.  (A
 // branch-free variant that only flags non-normal reciprocals and re-runs the wave's scan with
 // the generic loop when a live ray was flagged is bit-exact too but measured 1.9x slower --
 // DESIGN.md §4.7.)
+#ifdef RVCP_SPEC_RCP_UNIFORM
+// A/B: the rare IEEE branch behind a wave-uniform test (a ballot and a scalar branch) instead
+// of a divergent one (exec save / restore around every test)
+__device__ __forceinline__ float rcp_scan_u(float den) {
+    const float r = __builtin_amdgcn_rcpf(den);
+    float f = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    const bool bad = !__builtin_amdgcn_classf(f, (1 << 8) | (1 << 3));
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0ull, 0)) {
+        if (bad && __builtin_amdgcn_classf(den, 0x39c)) f = 1.0f / den;
+    }
+    return f;
+}
+#define RVCP_SPEC_RCP(den) rcp_scan_u(den)
+#else
 #define RVCP_SPEC_RCP(den) rcp_scan(den)
+#endif
 #include RVCP_SPEC_SCAN
 // The specialised scan drops products with exact-zero triangle components.  That is exact
 // when no intermediate of the generic test overflows (inf * 0 = NaN rejects there, while the
@@ -747,7 +772,7 @@ __device__ __forceinline__ bool nee_sample(const FrameArgs &A, const LightRecord
     }
     if (li >= A.n_lights) return false;
     const LightRecord &L = lights[li];
-    const float x = __builtin_sqrtf(rnd(seed, ridx));                              // :319
+    const float x = sqrt_c(rnd(seed, ridx));                                       // :319
     const float y = rnd(seed, ridx);                                               // :320
     const f3 Xp = add(add(muls(ld3(L.v0), 1.0f - x), muls(ld3(L.v1), x * (1.0f - y))),
                       muls(ld3(L.v2), x * y));                                     // :324
@@ -787,15 +812,18 @@ __device__ __forceinline__ bool brdf_continue(const FrameArgs &A, const MatRecor
 
 // Continuation, after the direction: the attenuation update of :465-471 for direction wi
 // (wi = normalize(h), h the hemisphere-flipped unit-ball sample, :207-214).
+// dot(wi, S_nrm) is dot(S_nrm, wi) bit for bit (each product commutes), so the pdf test is the
+// cosine test and the divisor is one of two frame constants (FrameArgs::brdf_den, whose IEEE
+// reciprocals the host computed: divs_y with them is divs_pos).
 __device__ __forceinline__ void brdf_finish(const FrameArgs &A, f3 alb_pi, f3 S_nrm, f3 p,
                                             f3 &att, f3 &wi) {
     const f3 h = dot(p, S_nrm) > 0.0f ? p : neg(p);
     wi = normalize(h);
     const float cosw = dot(S_nrm, wi);
-    const f3 f = cosw > 0.0f ? alb_pi : mk(0, 0, 0);
-    const float pdf = dot(wi, S_nrm) > 0.0f ? 0.5f / 3.1415926f : 0.0f;
-    const float denom = __builtin_fmaxf(0.1f, pdf) * A.rr;
-    att = mulv(att, divs_pos(muls(f, cosw), denom));
+    const bool pos = cosw > 0.0f;
+    const f3 f = pos ? alb_pi : mk(0, 0, 0);
+    att = mulv(att, divs_y(muls(f, cosw), pos ? A.brdf_den[1] : A.brdf_den[0],
+                           pos ? A.brdf_rcp[1] : A.brdf_rcp[0]));
 }
 
 // random_in_unit_sphere (:195-201) for every lane with `need`, cooperatively: each round the
@@ -1944,7 +1972,20 @@ __device__ __forceinline__ void path_body(
             // ---- scan: both rays against every triangle (wave-uniform face index) ----
 #ifdef RVCP_SPEC_SCAN
             if (!__any((hasA && !ray_in_range(a_o, a_d)) || (hasB && !ray_in_range(b_o, b_d)))) {
-                spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
+                // the shadow ray's nearest face is not needed, only whether it hit (resolve
+                // A): a nearest t other than t_max is a hit; t_max itself (a miss, or a hit at
+                // exactly t_max -- neither occurs in a closed room) is settled by the generic
+                // scan of the wave's shadow rays, which finds the same nearest hit
+                spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, btB, bestB);
+                bestA = btA != A.t_max ? 0 : -1;
+                if (__builtin_expect(__any(hasA && btA == A.t_max), 0)) {
+                    btA = A.t_max;
+                    bestA = -1;
+                    for (uint32_t i = 0; i < A.n_faces; ++i) {
+                        float tA;
+                        if (tri_accept(tri[i], a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
+                    }
+                }
             } else
 #endif
             {
@@ -2156,7 +2197,7 @@ __device__ __forceinline__ f3 refract_glsl(f3 I, f3 N, float eta) {
     const float d = dot(N, I);
     const float k = 1.0f - eta * eta * (1.0f - d * d);
     if (k < 0.0f) return mk(0, 0, 0);
-    return sub(muls(I, eta), muls(N, eta * d + __builtin_sqrtf(k)));
+    return sub(muls(I, eta), muls(N, eta * d + sqrt_c(k)));
 }
 
 // fresnel_schlick, :544-551; pow(x, 5.0) := ((x*x)*(x*x))*x
@@ -2194,7 +2235,7 @@ __device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d
     // below (!(delta < 0) fails, or NaN roots fail the compares), so the wave skips the
     // square root, the roots and the compares
     if (!__any(delta >= 0.0f)) { t_out = bt; return false; }
-    const float sq = __builtin_sqrtf(delta);
+    const float sq = sqrt_c(delta);
     float t0 = FAST ? quot_markstein(-b + sq, two_a, y) : (-b + sq) / two_a;
     float t1 = FAST ? quot_markstein(-b - sq, two_a, y) : (-b - sq) / two_a;
     if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
@@ -2315,7 +2356,7 @@ __device__ __forceinline__ void legacy_body(
                 if (sc && ty == 2u) {                                       // :553-581
                     const float ratio = H_out ? (1.0f / ior) : ior;
                     const float cos_t = dot(neg(H_dir), H_nrm);
-                    const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+                    const float sin_t = sqrt_c(1.0f - cos_t * cos_t);
                     bool refracted = ratio * sin_t <= 1.0f;
                     if (refracted) refracted = rnd(seed, ridx) >= fresnel_schlick(cos_t, ratio);
                     dir = refracted ? refract_glsl(H_dir, H_nrm, ratio) : reflect_glsl(H_dir, H_nrm);

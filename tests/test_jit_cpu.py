@@ -32,6 +32,7 @@ struct f3 { float x, y, z; };
 static inline float RVCP_F32(uint32_t b) { float f; std::memcpy(&f, &b, 4); return f; }
 #define RVCP_SPEC_RCP(d) (1.0f / (d))
 #define RVCP_SPEC_COMMIT(t, i) ((void)0)
+#define RVCP_SPEC_COMMIT1(t) ((void)0)
 """
 DRIVER = r"""
 extern "C" void scan_all(const float *rays, int n, float tmin, float tmax, float *bt_out,
@@ -40,10 +41,18 @@ extern "C" void scan_all(const float *rays, int n, float tmin, float tmax, float
         const float *q = rays + 6 * r;
         f3 o{q[0], q[1], q[2]}, d{q[3], q[4], q[5]};
         float bt = tmax; int best = -1;
-        if (dual) {           // the two-ray form, with a second (different) ray in slot B
+        if (dual) {
+            // the two-ray form: the ray in slot B (nearest t and face), a different ray in
+            // slot A; then the ray in slot A (its t and hit flag), the other ray in slot B
             f3 o2{q[0] + 1.0f, q[1], q[2]}, d2{q[4], q[5], q[3]};
-            float bt2 = tmax; int best2 = -1;
-            spec_scan2(o, d, o2, d2, tmin, bt, best, bt2, best2);
+            // (slot A keeps only its t: t_max after the scan is a miss or a hit at exactly
+            // t_max, which the kernel settles with the generic scan)
+            float bt2 = tmax;
+            spec_scan2(o2, d2, o, d, tmin, bt2, bt, best);
+            float btA = tmax, bt3 = tmax; int best3 = -1;
+            spec_scan2(o, d, o2, d2, tmin, btA, bt3, best3);
+            if (btA != bt || (btA != tmax && best < 0) || bt3 != bt2 || (bt2 != tmax && best3 < 0))
+                best = -2;        // the slots disagree: reported as a mismatch
         } else {
             spec_scan1(o, d, tmin, bt, best);
         }
@@ -169,7 +178,9 @@ def test_generated_scan_cornell_bitexact(tmp_path):
     pos = _cornell_positions()
     rec = _tri_records(pos)
     src = _scan_source(rec)
-    assert src.count("spec_scan1") == 1 and src.count("RVCP_SPEC_COMMIT") == 3 * len(pos)
+    # one commit per test: the single-ray scan's and slot B's with the face, slot A's t only
+    assert src.count("spec_scan1") == 1 and src.count("RVCP_SPEC_COMMIT(") == 2 * len(pos)
+    assert src.count("RVCP_SPEC_COMMIT1(") == len(pos)
     # zero components are dropped: 2544 arithmetic temporaries against 3552 for 32 triangles
     # with no zero component (-28 %)
     dense = _scan_source(_tri_records(np.random.default_rng(0).uniform(-5, 5, pos.shape)))
