@@ -113,10 +113,26 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// _rand's fract (:156-158) with one instruction: v_fract_f32 is x - floor(x) except where that
+// rounds to 1.0 (it returns 1 - 2^-24 there), i.e. for a negative x within 2^-25 of zero.  For
+// x = sin(y) * 43758.5453 no float rand() argument y in [1, 2^24 + 16] gives such an x (the
+// closest negative x is -2^-11.6): checked over all of them with the oracle's sin on the CPU and
+// with this kernel's on the GPU (tools/sqrt_check.hip).
+#ifndef RVCP_FAST_FRACT
+#define RVCP_FAST_FRACT 0
+#endif
+__device__ __forceinline__ float rand_of(float y) {
+    const float x = pt_sinf_rand(y) * 43758.5453f;
+    return RVCP_FAST_FRACT ? __builtin_amdgcn_fractf(x) : fractf(x);
+}
+// rand3's unit-cube coordinate 2 r - 1 (:197): 2 r is exact, so the fused form rounds the same
+// value once, as the written two-step form does
+__device__ __forceinline__ float cube_coord(float r) { return __builtin_fmaf(2.0f, r, -1.0f); }
+
 // rand(), :159-162: index += 1; fract(sin(seed + index) * 43758.5453)
 __device__ __forceinline__ float rnd(float seed, float &idx) {
     idx = idx + 1.0f;
-    return fractf(pt_sinf_rand(seed + idx) * 43758.5453f);
+    return rand_of(seed + idx);
 }
 
 // 1 / den, IEEE round-to-nearest (the shader's `1.0 / dot(s1, e1)`, :254).
@@ -798,7 +814,7 @@ __device__ __forceinline__ bool brdf_continue(const FrameArgs &A, const MatRecor
         const float rx = rnd(seed, ridx);
         const float ry = rnd(seed, ridx);
         const float rz = rnd(seed, ridx);
-        p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
+        p = mk(cube_coord(rx), cube_coord(ry), cube_coord(rz));
     } while (dot(p, p) >= 1.0f);
     const f3 h = dot(p, S_nrm) > 0.0f ? p : neg(p);                                // :207-210
     wi = normalize(h);                                                             // :212-214
@@ -843,10 +859,10 @@ __device__ __forceinline__ void coop_unit_sphere(bool need, float seed, float &r
         if (n > kWave / 2) {
             // K = 1: every lane still rejecting tests its own next candidate -- the same
             // candidate the compacted form below would hand it, without the LDS round trips
-            const float rx = fractf(pt_sinf_rand(seed + (ridx + 1.0f)) * 43758.5453f);
-            const float ry = fractf(pt_sinf_rand(seed + (ridx + 2.0f)) * 43758.5453f);
-            const float rz = fractf(pt_sinf_rand(seed + (ridx + 3.0f)) * 43758.5453f);
-            const f3 p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
+            const float rx = rand_of(seed + (ridx + 1.0f));
+            const float ry = rand_of(seed + (ridx + 2.0f));
+            const float rz = rand_of(seed + (ridx + 3.0f));
+            const f3 p = mk(cube_coord(rx), cube_coord(ry), cube_coord(rz));
             if (need) {
                 ridx = ridx + 3.0f;
                 if (!(dot(p, p) >= 1.0f)) {
@@ -870,10 +886,10 @@ __device__ __forceinline__ void coop_unit_sphere(bool need, float seed, float &r
         const int owner = worker ? (int)tab[j] : (int)lane;
         const float s_seed = __shfl(seed, owner);
         const float base = __shfl(ridx, owner) + (float)(3u * c);
-        const float rx = fractf(pt_sinf_rand(s_seed + (base + 1.0f)) * 43758.5453f);
-        const float ry = fractf(pt_sinf_rand(s_seed + (base + 2.0f)) * 43758.5453f);
-        const float rz = fractf(pt_sinf_rand(s_seed + (base + 3.0f)) * 43758.5453f);
-        const f3 p = mk(2.0f * rx - 1.0f, 2.0f * ry - 1.0f, 2.0f * rz - 1.0f);
+        const float rx = rand_of(s_seed + (base + 1.0f));
+        const float ry = rand_of(s_seed + (base + 2.0f));
+        const float rz = rand_of(s_seed + (base + 3.0f));
+        const f3 p = mk(cube_coord(rx), cube_coord(ry), cube_coord(rz));
         const uint64_t AM = __ballot(worker && !(dot(p, p) >= 1.0f));
         const uint64_t segmask = K >= 64u ? ~0ull : ((1ull << K) - 1ull);
         const uint64_t seg = need ? ((AM >> (r << lgK)) & segmask) : 0ull;

@@ -83,7 +83,7 @@ for s in $STEPS; do
         # schedules 4 / 10 on meshes (tools/ab.py, one frame at a time)
         c5pool) run c5pool 900 python tools/ab.py --runner frames "s4=::--variant 4 --tris 2000 --size 1024 --spp 8 --frames 6" "s10=::--variant 10 --tris 2000 --size 1024 --spp 8 --frames 6" ;;
         spec) run pytest_spec 900 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_pipeline.py tests/test_gpu_batch.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
-        abrcp) run ab_rcp 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3" "dbg=RVCP_LIB=$DBG::--workload c3" "unif=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_RCP_UNIFORM::--workload c3" "sqrt=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_SQRT=1::--workload c3" "both=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_SQRT=1 -DRVCP_SPEC_RCP_UNIFORM::--workload c3" ;;
+        abrcp) run ab_rcp 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3" "dbg=RVCP_LIB=$DBG::--workload c3" "unif=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_RCP_UNIFORM::--workload c3" "sqrt=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_SQRT=1::--workload c3" "fract=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_FRACT=1::--workload c3" "all=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_SQRT=1 -DRVCP_FAST_FRACT=1 -DRVCP_SPEC_RCP_UNIFORM::--workload c3" ;;
         sqrtchk) run sqrt_check 300 tools/build/sqrt_check ;;
         abc3) run ab_c3 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3" "new=::--workload c3" ;;
         pipeline) run pytest_pipeline 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_bench.py -m gpu -x -v --timeout 300 --timeout-method thread ;;

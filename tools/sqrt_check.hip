@@ -5,7 +5,11 @@
 //   y = v_rsq_f32(x); g = RN(x y); h = RN(0.5 y); r = fma(-g, g, x); s = fma(r, h, g)
 // used iff x lies in [2^-100, 2^100] (the guard the kernel applies; NaN, inf, zero, negative,
 // subnormal and extreme inputs take the IEEE sequence).  Reports the inputs on the fast path and
-// every mismatch.  Build: make -C tools build/sqrt_check
+// every mismatch.  Also: v_fract_f32 against x - floor(x) for every rand() value the RNG can
+// form, x = sin(y) * 43758.5453 over every float y in [1, 2^24 + 16] (rand's arguments; the
+// contract's software sin): the two differ only where x - floor(x) rounds to
+// 1.0 (a negative x within 2^-25 of zero), which this range never produces.
+// Build: make -C tools build/sqrt_check
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -28,6 +32,32 @@ __global__ void check(uint32_t hi, unsigned long long *bad, unsigned long long *
     }
 }
 
+// the kernel's rand() core with both fract forms
+__device__ __forceinline__ float sin_rand(float x) {
+    const float q = __builtin_rintf(x * 0x1.45f306p-2f);
+    float r = __builtin_fmaf(q, -0x1.921fb6p+1f, x);
+    r = __builtin_fmaf(q, 0x1.777a5cp-24f, r);
+    const float z = r * r;
+    const float p = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(0x1.5dbdfep-19f, z, -0x1.9f7p-13f),
+                                                  z, 0x1.110ed4p-7f), z, -0x1.55554cp-3f);
+    const float s = __builtin_fmaf(p, z * r, r);
+    return __uint_as_float(__float_as_uint(s) ^ ((uint32_t)(int)q << 31));
+}
+
+__global__ void check_fract(uint32_t base, uint32_t n, unsigned long long *bad, unsigned *first)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float y = __uint_as_float(base + i);
+    const float x = sin_rand(y) * 43758.5453f;
+    const float a = x - __builtin_floorf(x);
+    const float b = __builtin_amdgcn_fractf(x);
+    if (__float_as_uint(a) != __float_as_uint(b)) {
+        const unsigned long long k = atomicAdd(bad, 1ull);
+        if (k < 8) first[k] = base + i;
+    }
+}
+
 int main()
 {
     unsigned long long *bad, *used;
@@ -47,5 +77,15 @@ int main()
     printf("all 2^32 inputs: fast path taken for %llu, mismatches %llu", u, b);
     for (int i = 0; i < 8 && i < (int)b; i++) printf(" %08x", f[i]);
     printf("\n");
-    return b == 0 ? 0 : 1;
+    // fract: y over [1, 2^24 + 16] (0x3f800000 .. 0x4b800010)
+    const uint32_t lo = 0x3f800000u, n = 0x4b800010u - lo + 1u;
+    hipMemset(bad, 0, 8);
+    hipLaunchKernelGGL(check_fract, dim3((n + 255) / 256), dim3(256), 0, 0, lo, n, bad, first);
+    unsigned long long fb = 0;
+    hipMemcpy(&fb, bad, 8, hipMemcpyDeviceToHost);
+    hipMemcpy(f, first, 32, hipMemcpyDeviceToHost);
+    printf("rand fract: %u arguments, v_fract_f32 != x - floor(x) on %llu", n, fb);
+    for (int i = 0; i < 8 && i < (int)fb; i++) printf(" %08x", f[i]);
+    printf("\n");
+    return (b == 0 && fb == 0) ? 0 : 1;
 }
