@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark: Msamples/s of the path-tracing hot path (BASELINE.json metric), Cornell box.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|...]
 
-One step = one frame: every rank renders its 8-row stripes of the frame with the HIP kernel
+`--gpus N` (N > 1) without a launcher starts its N ranks itself (torch.distributed.run on
+127.0.0.1, see self_launch); under torch.distributed.run it is one rank.
+
+One step = one frame, each with its own time seed (123.0 + frame index, as the reference
+re-stamps `time` every frame): every rank renders its 8-row stripes of the frame with the HIP kernel
 (rvcp_render_shard_async), the stripes are gathered to rank 0 over RCCL
 (rvcp_gather_frame_async: ncclGather inside librvcp) and rank 0 assembles the frame on the
 device.  Two frames are in flight (--frames-in-flight, default 2): two contexts, each on its

@@ -77,6 +77,7 @@ struct rvcp_ctx {
     float *d_unorm = nullptr;
     unsigned long long *d_counters = nullptr;
     uint32_t n_faces = 0, n_lights = 0, n_mats = 0, n_verts = 0, n_spheres = 0;
+    bool lights_same = false;      // every light record samples the same face
     // scene-specialised path kernels (rvcp_jit.cpp), or null: generic kernels
     std::shared_ptr<JitKernels> jit;
     std::string jit_err;
@@ -604,6 +605,9 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     ctx->n_verts = n_vertices;
     ctx->n_mats = n_materials;
     ctx->n_lights = n_lum_face_ids;
+    ctx->lights_same = n_lum_face_ids >= 1;
+    for (uint32_t i = 1; i < n_lum_face_ids; i++)
+        if (tab.lights[i].face != tab.lights[0].face) ctx->lights_same = false;
     ctx->light_total = total;
     ctx->light_pdf = 1.0f / total;
     ctx->has_scene = true;
@@ -680,6 +684,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     A.eps = ctx->cfg.eps;
     A.n_faces = ctx->n_faces;
     A.n_lights = ctx->n_lights;
+    A.lights_same = ctx->lights_same ? 1u : 0u;
     A.light_total = ctx->light_total;
     A.light_pdf = ctx->light_pdf;
     {   // :465-471: denom = max(0.1, pdf) * rr, pdf = 0.5 / 3.1415926 (cos > 0) or 0; IEEE 1/denom

@@ -199,6 +199,9 @@ struct FrameArgs {
     // pdf = 0, and their IEEE reciprocals: frame constants, so the update divides by a known
     // reciprocal (divs_y) instead of computing rcp_ieee per event
     float brdf_den[2], brdf_rcp[2];
+    // every light record samples the same face (the std140 id quirk on the Cornell box maps
+    // both entries to face 0): nee_sample's pick cannot change the sample, so it reads record 0
+    uint32_t lights_same;
     uint32_t static_chunks;  // pixels handed out statically (one chunk per wave)
     uint32_t static_chunk;   // pixels of each wave's static chunk (<= kChunk)
     uint32_t n_simds;        // SIMDs of the device (CUs x 4), for static_split

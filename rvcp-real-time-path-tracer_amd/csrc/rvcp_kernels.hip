@@ -782,24 +782,36 @@ __device__ __forceinline__ bool nee_sample(const FrameArgs &A, const LightRecord
                                            f3 alb_pi, f3 S_pos, f3 S_nrm, f3 att,
                                            float seed, float &ridx, f3 &C, float &dist, f3 &ws) {
     const float pl = rnd(seed, ridx) * A.light_total;
-    uint32_t li = A.n_lights;
-    for (uint32_t i = 0; i < A.n_lights; ++i) {
-        if (pl <= lights[i].cum) { li = i; break; }
+    f3 Lv0, Lv1, Lv2, Ln, Lle;
+#ifndef RVCP_NEE_SAME_OFF
+    if (A.lights_same) {
+        // every record samples the same face, and pl <= the last cum always holds (pl =
+        // rand * total <= total, the same sum), so the pick is record 0: wave-uniform reads
+        const LightRecord &L = lights[0];
+        Lv0 = ld3(L.v0); Lv1 = ld3(L.v1); Lv2 = ld3(L.v2); Ln = ld3(L.n); Lle = ld3(L.le);
+    } else
+#endif
+    {
+        uint32_t li = A.n_lights;
+        for (uint32_t i = 0; i < A.n_lights; ++i) {
+            if (pl <= lights[i].cum) { li = i; break; }
+        }
+        if (li >= A.n_lights) return false;
+        const LightRecord &L = lights[li];
+        Lv0 = ld3(L.v0); Lv1 = ld3(L.v1); Lv2 = ld3(L.v2); Ln = ld3(L.n); Lle = ld3(L.le);
     }
-    if (li >= A.n_lights) return false;
-    const LightRecord &L = lights[li];
     const float x = sqrt_c(rnd(seed, ridx));                                       // :319
     const float y = rnd(seed, ridx);                                               // :320
-    const f3 Xp = add(add(muls(ld3(L.v0), 1.0f - x), muls(ld3(L.v1), x * (1.0f - y))),
-                      muls(ld3(L.v2), x * y));                                     // :324
+    const f3 Xp = add(add(muls(Lv0, 1.0f - x), muls(Lv1, x * (1.0f - y))),
+                      muls(Lv2, x * y));                                           // :324
     const f3 dv = sub(Xp, S_pos);
     dist = len(dv);                                                                // :438
     ws = divs_pos(dv, dist);                                                       // :439
     const float cosp = dot(S_nrm, ws);
     const f3 f = cosp > 0.0f ? alb_pi : mk(0, 0, 0);                               // :344-349
-    C = mulv(mulv(att, ld3(L.le)), f);                                             // :450-458
+    C = mulv(mulv(att, Lle), f);                                                   // :450-458
     C = muls(C, cosp);
-    C = muls(C, dot(ld3(L.n), neg(ws)));
+    C = muls(C, dot(Ln, neg(ws)));
     C = divs_pos(C, dist * dist * A.light_pdf);
     return true;
 }
@@ -2555,9 +2567,28 @@ extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_pa
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];
     __shared__ float state_lds[kStateCols * kBlock];
+#ifdef RVCP_SPEC_LDS_SCENE
+    // A/B: the scene's triangle and shading records (at most 64 faces in this module) copied
+    // into LDS once per workgroup, so the hit record's per-lane gathers are LDS reads
+    __shared__ TriRecord sh_tri[64];
+    __shared__ FaceShade sh_shade[64];
+    {
+        const float4 *src = reinterpret_cast<const float4 *>(tri);
+        float4 *dst = reinterpret_cast<float4 *>(sh_tri);
+        for (uint32_t e = threadIdx.x; e < 3u * A.n_faces; e += kBlock) dst[e] = src[e];
+        const float4 *src2 = reinterpret_cast<const float4 *>(shade);
+        float4 *dst2 = reinterpret_cast<float4 *>(sh_shade);
+        for (uint32_t e = threadIdx.x; e < 4u * A.n_faces; e += kBlock) dst2[e] = src2[e];
+        __syncthreads();
+    }
+    path_body<false, false, false, true>(
+        A, sh_tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, sh_shade, tail_tab,
+        nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+#else
     path_body<false, false, false, true>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+#endif
 }
 extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
