@@ -56,12 +56,10 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
               __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
 }
-// The IEEE square root: rvcp_sqrt.h's 5-instruction form (checked on all 2^32 inputs) or the
-// compiler's correctly-rounded sequence (A/B)
-#ifndef RVCP_FAST_SQRT
-#define RVCP_FAST_SQRT 0
-#endif
-__device__ __forceinline__ float sqrt_c(float x) { return RVCP_FAST_SQRT ? sqrt_ieee(x) : __builtin_sqrtf(x); }
+// The IEEE square root: rvcp_sqrt.h's 5-instruction form where its guard admits x (equal to the
+// correctly rounded root on every such input, tools/sqrt_check.hip), else the compiler's
+// correctly-rounded sequence
+__device__ __forceinline__ float sqrt_c(float x) { return sqrt_ieee(x); }
 __device__ __forceinline__ float len(f3 a) { return sqrt_c(dot(a, a)); }
 // 1 / sqrt by rcp_ieee below (the IEEE quotient, fast path verified over all inputs)
 __device__ __forceinline__ float rcp_ieee(float den);
@@ -115,15 +113,13 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
 
 // _rand's fract (:156-158) with one instruction: v_fract_f32 is x - floor(x) except where that
 // rounds to 1.0 (it returns 1 - 2^-24 there), i.e. for a negative x within 2^-25 of zero.  For
-// x = sin(y) * 43758.5453 no float rand() argument y in [1, 2^24 + 16] gives such an x (the
-// closest negative x is -2^-11.6): checked over all of them with the oracle's sin on the CPU and
-// with this kernel's on the GPU (tools/sqrt_check.hip).
-#ifndef RVCP_FAST_FRACT
-#define RVCP_FAST_FRACT 0
-#endif
+// x = sin(y) * 43758.5453 no float rand() argument y in [1, 2^25] (seed + an index that stops
+// growing at 2^24, plus at most 195 in coop_unit_sphere) gives such an x (the closest negative x
+// is -2^-11.6): checked over all of them with the oracle's sin on the CPU
+// (tests/test_rand_fract_cpu.py) and with this kernel's sin and v_fract_f32 on the GPU
+// (tools/sqrt_check.hip).  DESIGN.md §3.10.
 __device__ __forceinline__ float rand_of(float y) {
-    const float x = pt_sinf_rand(y) * 43758.5453f;
-    return RVCP_FAST_FRACT ? __builtin_amdgcn_fractf(x) : fractf(x);
+    return __builtin_amdgcn_fractf(pt_sinf_rand(y) * 43758.5453f);
 }
 // rand3's unit-cube coordinate 2 r - 1 (:197): 2 r is exact, so the fused form rounds the same
 // value once, as the written two-step form does
@@ -279,22 +275,7 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
 // branch-free variant that only flags non-normal reciprocals and re-runs the wave's scan with
 // the generic loop when a live ray was flagged is bit-exact too but measured 1.9x slower --
 // DESIGN.md §4.7.)
-#ifdef RVCP_SPEC_RCP_UNIFORM
-// A/B: the rare IEEE branch behind a wave-uniform test (a ballot and a scalar branch) instead
-// of a divergent one (exec save / restore around every test)
-__device__ __forceinline__ float rcp_scan_u(float den) {
-    const float r = __builtin_amdgcn_rcpf(den);
-    float f = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
-    const bool bad = !__builtin_amdgcn_classf(f, (1 << 8) | (1 << 3));
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0ull, 0)) {
-        if (bad && __builtin_amdgcn_classf(den, 0x39c)) f = 1.0f / den;
-    }
-    return f;
-}
-#define RVCP_SPEC_RCP(den) rcp_scan_u(den)
-#else
 #define RVCP_SPEC_RCP(den) rcp_scan(den)
-#endif
 #include RVCP_SPEC_SCAN
 // The specialised scan drops products with exact-zero triangle components.  That is exact
 // when no intermediate of the generic test overflows (inf * 0 = NaN rejects there, while the
@@ -783,15 +764,12 @@ __device__ __forceinline__ bool nee_sample(const FrameArgs &A, const LightRecord
                                            float seed, float &ridx, f3 &C, float &dist, f3 &ws) {
     const float pl = rnd(seed, ridx) * A.light_total;
     f3 Lv0, Lv1, Lv2, Ln, Lle;
-#ifndef RVCP_NEE_SAME_OFF
     if (A.lights_same) {
         // every record samples the same face, and pl <= the last cum always holds (pl =
         // rand * total <= total, the same sum), so the pick is record 0: wave-uniform reads
         const LightRecord &L = lights[0];
         Lv0 = ld3(L.v0); Lv1 = ld3(L.v1); Lv2 = ld3(L.v2); Ln = ld3(L.n); Lle = ld3(L.le);
-    } else
-#endif
-    {
+    } else {
         uint32_t li = A.n_lights;
         for (uint32_t i = 0; i < A.n_lights; ++i) {
             if (pl <= lights[i].cum) { li = i; break; }
@@ -2567,28 +2545,9 @@ extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_pa
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];
     __shared__ float state_lds[kStateCols * kBlock];
-#ifdef RVCP_SPEC_LDS_SCENE
-    // A/B: the scene's triangle and shading records (at most 64 faces in this module) copied
-    // into LDS once per workgroup, so the hit record's per-lane gathers are LDS reads
-    __shared__ TriRecord sh_tri[64];
-    __shared__ FaceShade sh_shade[64];
-    {
-        const float4 *src = reinterpret_cast<const float4 *>(tri);
-        float4 *dst = reinterpret_cast<float4 *>(sh_tri);
-        for (uint32_t e = threadIdx.x; e < 3u * A.n_faces; e += kBlock) dst[e] = src[e];
-        const float4 *src2 = reinterpret_cast<const float4 *>(shade);
-        float4 *dst2 = reinterpret_cast<float4 *>(sh_shade);
-        for (uint32_t e = threadIdx.x; e < 4u * A.n_faces; e += kBlock) dst2[e] = src2[e];
-        __syncthreads();
-    }
-    path_body<false, false, false, true>(
-        A, sh_tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, sh_shade, tail_tab,
-        nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
-#else
     path_body<false, false, false, true>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
-#endif
 }
 extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,

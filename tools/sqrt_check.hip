@@ -6,7 +6,7 @@
 // used iff x lies in [2^-100, 2^100] (the guard the kernel applies; NaN, inf, zero, negative,
 // subnormal and extreme inputs take the IEEE sequence).  Reports the inputs on the fast path and
 // every mismatch.  Also: v_fract_f32 against x - floor(x) for every rand() value the RNG can
-// form, x = sin(y) * 43758.5453 over every float y in [1, 2^24 + 16] (rand's arguments; the
+// form, x = sin(y) * 43758.5453 over every float y in [1, 2^25] (rand's arguments; the
 // contract's software sin): the two differ only where x - floor(x) rounds to
 // 1.0 (a negative x within 2^-25 of zero), which this range never produces.
 // Build: make -C tools build/sqrt_check
@@ -77,8 +77,8 @@ int main()
     printf("all 2^32 inputs: fast path taken for %llu, mismatches %llu", u, b);
     for (int i = 0; i < 8 && i < (int)b; i++) printf(" %08x", f[i]);
     printf("\n");
-    // fract: y over [1, 2^24 + 16] (0x3f800000 .. 0x4b800010)
-    const uint32_t lo = 0x3f800000u, n = 0x4b800010u - lo + 1u;
+    // fract: y over [1, 2^25] (0x3f800000 .. 0x4c000000)
+    const uint32_t lo = 0x3f800000u, n = 0x4c000000u - lo + 1u;
     hipMemset(bad, 0, 8);
     hipLaunchKernelGGL(check_fract, dim3((n + 255) / 256), dim3(256), 0, 0, lo, n, bad, first);
     unsigned long long fb = 0;
