@@ -713,6 +713,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     A.bvh_slots = ctx->bvh_slots;
     const bool legacy = ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY;
     A.n_spheres = legacy ? ctx->n_spheres : 0u;
+    A.n_mats = ctx->n_mats;
 
     // With MAX_BOUNCES == 0 or ATTENUATION_STOP_EPS > 1 every sample returns 0 before its
     // first traversal (:413-419): the frame is black.  ray_tracer.comp has no attenuation

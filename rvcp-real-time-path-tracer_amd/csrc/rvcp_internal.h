@@ -208,6 +208,7 @@ struct FrameArgs {
     uint32_t want_linear;
     int32_t variant;         // kernel schedule (rvcp_config_t::kernel_variant, resolved)
     uint32_t n_spheres;      // integrator RVCP_INTEGRATOR_LEGACY only
+    uint32_t n_mats;
     uint32_t dyn_chunk;      // largest frame-queue grab after the static chunk
     uint32_t chunk_min;      // smallest grab
     uint32_t chunk_window;   // grab = pixels this wave consumes in chunk_window ticks (10 ns)

@@ -2527,7 +2527,28 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
 {
     __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
+#ifdef RVCP_LEGACY_LDS_SCENE
+    // A/B (scenes of at most 64 spheres, materials and faces): the per-lane gathers of the hit
+    // record and the scatter read LDS copies instead of global memory
+    __shared__ TriRecord sh_tri[64];
+    __shared__ FaceShade sh_shade[64];
+    __shared__ rvcp_sphere_t sh_sph[64];
+    __shared__ rvcp_material_t sh_mat[64];
+    {
+        auto cp = [](float4 *dst, const float4 *src, uint32_t n) {
+            for (uint32_t e = threadIdx.x; e < n; e += kBlock) dst[e] = src[e];
+        };
+        cp(reinterpret_cast<float4 *>(sh_tri), reinterpret_cast<const float4 *>(tri), 3u * A.n_faces);
+        cp(reinterpret_cast<float4 *>(sh_shade), reinterpret_cast<const float4 *>(shade), 4u * A.n_faces);
+        cp(reinterpret_cast<float4 *>(sh_sph), reinterpret_cast<const float4 *>(sph), 2u * A.n_spheres);
+        cp(reinterpret_cast<float4 *>(sh_mat), reinterpret_cast<const float4 *>(mats),
+           2u * (A.n_mats < 64u ? A.n_mats : 64u));
+        __syncthreads();
+    }
+    legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab);
+#else
     legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
+#endif
 }
 #endif
 #endif  // !RVCP_JIT || RVCP_JIT_LEGACY

@@ -36,7 +36,12 @@ def main():
             print(json.dumps({"variant": a.variant, "integrator": a.integrator,
                               "traversals": int(st["traversals"]), "kernel_ms": round(float(st["kernel_ms"]), 3),
                               "executed": int(st["traversals_executed"]),
-                              "wave_iterations": int(st["wave_iterations"])}), flush=True)
+                              "wave_iterations": int(st["wave_iterations"]),
+                              # path-kernel rays per ray slot (2 per lane per wave iteration;
+                              # the pre-pass traced one primary ray per pixel)
+                              "slot_util": round((int(st["traversals_executed"]) - a.size * a.size)
+                                                 / max(1, 128 * int(st["wave_iterations"])), 4)
+                              if a.integrator == 0 else None}), flush=True)
 
 
 if __name__ == "__main__":

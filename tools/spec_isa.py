@@ -21,9 +21,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(CSRC, "build", "spec_isa"))
     ap.add_argument("--flags", default="")
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres"])
+    ap.add_argument("--legacy", action="store_true", help="the mode-2 module (RVCP_JIT_LEGACY)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
-    sc = rvcp_amd.Scene.default()
+    sc = rvcp_amd.Scene.default() if a.scene == "cornell" else rvcp_amd.scene.sphere_scene()
     V = sc.mesh.aligned_vertices()["position"][:, :3]
     F = sc.mesh.aligned_faces()["vertices"]
     p = V[F].astype(np.float32)
@@ -43,7 +45,8 @@ def main():
            "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-fast-math", "-fno-slp-vectorize",
            "-DRVCP_JIT", f'-DRVCP_SPEC_SCAN="{inc}"', "--cuda-device-only", "-S",
            "-o", os.path.join(a.out, "spec.s"), os.path.join(CSRC, "rvcp_kernels.hip"),
-           "-Rpass-analysis=kernel-resource-usage"] + a.flags.split()
+           "-Rpass-analysis=kernel-resource-usage"] + (["-DRVCP_JIT_LEGACY"] if a.legacy else []) + \
+          a.flags.split()
     with open(os.path.join(a.out, "resource-usage.txt"), "w") as f:
         subprocess.run(cmd, check=True, stderr=f)
     out = open(os.path.join(a.out, "resource-usage.txt")).read()
