@@ -1983,6 +1983,26 @@ __device__ __forceinline__ void path_body(
                 // exactly t_max -- neither occurs in a closed room) is settled by the generic
                 // scan of the wave's shadow rays, which finds the same nearest hit
                 spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, btB, bestB);
+            } else
+#endif
+            {
+            // the generic loop keeps no face index for the shadow ray either (as spec_scan2)
+#pragma unroll 1
+            for (uint32_t i = 0; i < A.n_faces; ++i) {
+                const TriRecord T = tri[i];
+                float tA, tB;
+                if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) {
+                    btA = tA;
+                    if (SINGLE) bestA = (int)i;
+                }
+                if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
+            }
+            }
+            if (!SINGLE) {
+                // The shadow ray's nearest face is not needed, only whether it hit (resolve A):
+                // a nearest t other than t_max is a hit; t_max itself (a miss, or a hit at
+                // exactly t_max -- neither occurs in a closed room) is settled by a re-scan of
+                // the wave's shadow rays that keeps the face, which finds the same nearest hit.
                 bestA = btA != A.t_max ? 0 : -1;
                 if (__builtin_expect(__any(hasA && btA == A.t_max), 0)) {
                     btA = A.t_max;
@@ -1992,16 +2012,6 @@ __device__ __forceinline__ void path_body(
                         if (tri_accept(tri[i], a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
                     }
                 }
-            } else
-#endif
-            {
-#pragma unroll 1
-            for (uint32_t i = 0; i < A.n_faces; ++i) {
-                const TriRecord T = tri[i];
-                float tA, tB;
-                if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) { btA = tA; bestA = (int)i; }
-                if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
-            }
             }
         }
 
