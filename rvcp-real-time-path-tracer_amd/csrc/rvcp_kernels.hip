@@ -536,45 +536,84 @@ __device__ __forceinline__ void bvh4_step(const Bvh4QNode *__restrict__ qn, lds_
     else { sp -= 1; ref = stk[sp * kBlock]; }
 }
 
-// Wave-pooled traversal (bvh_pool): the wave's shadow rays (lanes sA, in lane order) and
-// path rays (sB) form one list of up to 128 rays; every lane takes the next untaken ray as soon
+// Wave-pooled traversal (bvh_pool): the wave's new shadow rays (lanes nA, in lane order) and
+// path rays (nB) form one list of up to 128 rays; every lane takes the next untaken ray as soon
 // as its current one is finished, with the speculative while-while steps of bvh_nearest, so a
 // wave's 64 lanes share its rays instead of each waiting for its own longest traversal.  A
 // ray's (o, d) is read from its owner lane's registers (ds_bpermute via the wave's LDS table of
-// owners, tab[128]), its (t, face) is left in res[128] and read back by the owner.  Same
-// traversal per ray, so the same nearest hits.
+// owners, tab[128]), its (t, face) is left in res[2 owner + (path ray)] and read back by the
+// owner.  Same traversal per ray, so the same nearest hits.
 // (inlined into the path kernel with two-triangle leaf loads: 112 VGPRs without spills, C5
 // BVH 138 -> 97.5 ms per frame, profiles/r03zj_bvh_pool_ab.log, r03zk_bvh_pool_ab.log)
+//
+// Carried traversals: once every new ray is taken and at most kBvhCarryMax lanes still hold an
+// unfinished one, the pool may stop and let the wave go on with its next iteration; those lanes
+// keep their traversal (BvhCarry, its stack stays in the lane's LDS column) and resume it first
+// in the next call.  A wave's iteration otherwise lasts as long as its longest traversal, with
+// most lanes idle at the end (lane utilisation 0.30 in C5).  The owner of an unfinished ray is
+// `frozen`: it neither resolves nor emits rays until all its submitted rays have results (a
+// result slot holds the face -2 until written).  Carrying is allowed only while the frame
+// queue still has pixels and the call took at least kBvhCarryMinRays new rays, so each call
+// makes progress and the last iterations drain everything.
 constexpr uint32_t kBvhPoolChunk = 2;      // leaf triangles loaded together in bvh_pool
+#ifndef RVCP_BVH_CARRY_MAX
+#define RVCP_BVH_CARRY_MAX 8
+#endif
+#ifndef RVCP_BVH_CARRY_MIN_RAYS
+#define RVCP_BVH_CARRY_MIN_RAYS 32
+#endif
+constexpr uint32_t kBvhCarryMax = RVCP_BVH_CARRY_MAX;
+constexpr uint32_t kBvhCarryMinRays = RVCP_BVH_CARRY_MIN_RAYS;
+struct BvhCarry {
+    bool has = false;       // holds an unfinished traversal
+    uint32_t key = 0;       // its result slot: owner lane * 2 + (path ray ? 1 : 0)
+    int32_t ref = 0;        // next node (>= 0) or leaf (< 0)
+    int sp = 0;             // stack depth (the stack is the lane's LDS column)
+    float bt = 0.0f;
+    int best = -1;
+};
 __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
                                       const TriRecord *__restrict__ btri, int32_t root,
                                       lds_i32 *stk, uint8_t *tab, float2 *res, uint32_t lane,
-                                      bool sA, bool sB, f3 a_o, f3 a_d, f3 b_o, f3 b_d,
-                                      float tmin, float tmax, float &btA, int &bestA, float &btB,
-                                      int &bestB, uint32_t n4, uint32_t slots) {
-    const uint64_t mA = __ballot(sA), mB = __ballot(sB);
+                                      bool nA_, bool nB_, f3 a_o, f3 a_d, f3 b_o, f3 b_d,
+                                      float tmin, float tmax, bool may_carry, BvhCarry &c,
+                                      bool &subA, bool &subB, bool &frozen, float &btA, int &bestA,
+                                      float &btB, int &bestB, uint32_t n4, uint32_t slots) {
+    const uint64_t mA = __ballot(nA_), mB = __ballot(nB_);
     const uint32_t nA = (uint32_t)__builtin_popcountll(mA);
     const uint32_t nr = nA + (uint32_t)__builtin_popcountll(mB);
-    if (sA) tab[rank_in(mA)] = (uint8_t)lane;
-    if (sB) tab[nA + rank_in(mB)] = (uint8_t)lane;
+    const float2 pending = make_float2(tmax, __int_as_float(-2));
+    if (nA_) { tab[rank_in(mA)] = (uint8_t)lane; res[2 * lane] = pending; subA = true; }
+    if (nB_) { tab[nA + rank_in(mB)] = (uint8_t)lane; res[2 * lane + 1] = pending; subB = true; }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool carry_ok = may_carry && nr >= kBvhCarryMinRays;      // wave-uniform
     const Bvh4QNode *__restrict__ qn = reinterpret_cast<const Bvh4QNode *>(nodes + n4);
     uint32_t next = 0;                  // the list's next untaken ray (wave-uniform)
-    bool has = false, alive = false, parked = false;
-    uint32_t r = 0;
+    bool alive = c.has, parked = false;
     f3 o = mk(0, 0, 0), inv = mk(1, 1, 1), d = mk(0, 0, 1);
     bool px = true, py = true, pz = true;
-    int32_t ref = 0, lref = 0;
-    int sp = 0;
-    float bt = tmax;
-    int best = -1;
+    int32_t lref = 0;
+    if (__any(c.has)) {                 // resume the carried traversals: their rays' (o, d)
+        const int src = c.has ? (int)(c.key >> 1) : (int)lane;
+        const f3 oa = mk(__shfl(a_o.x, src), __shfl(a_o.y, src), __shfl(a_o.z, src));
+        const f3 da = mk(__shfl(a_d.x, src), __shfl(a_d.y, src), __shfl(a_d.z, src));
+        const f3 ob = mk(__shfl(b_o.x, src), __shfl(b_o.y, src), __shfl(b_o.z, src));
+        const f3 db = mk(__shfl(b_d.x, src), __shfl(b_d.y, src), __shfl(b_d.z, src));
+        if (c.has) {
+            const bool isA = (c.key & 1u) == 0u;
+            o = isA ? oa : ob;
+            d = isA ? da : db;
+            inv = slab_inv(d);
+            px = inv.x >= 0.0f; py = inv.y >= 0.0f; pz = inv.z >= 0.0f;
+        }
+    }
     for (;;) {
-        const uint64_t M = __ballot(!has);
+        const uint64_t M = __ballot(!c.has);
         if (M && next < nr) {
             const uint32_t k = rank_in(M);
-            const bool take = !has && next + k < nr;
+            const bool take = !c.has && next + k < nr;
             const uint32_t rr = next + k;
             const int src = take ? (int)tab[rr] : (int)lane;
             const f3 oa = mk(__shfl(a_o.x, src), __shfl(a_o.y, src), __shfl(a_o.z, src));
@@ -582,57 +621,60 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
             const f3 ob = mk(__shfl(b_o.x, src), __shfl(b_o.y, src), __shfl(b_o.z, src));
             const f3 db = mk(__shfl(b_d.x, src), __shfl(b_d.y, src), __shfl(b_d.z, src));
             if (take) {
-                r = rr;
                 const bool isA = rr < nA;
+                c.key = 2u * (uint32_t)src + (isA ? 0u : 1u);
                 o = isA ? oa : ob;
                 d = isA ? da : db;
                 inv = slab_inv(d);
                 px = inv.x >= 0.0f; py = inv.y >= 0.0f; pz = inv.z >= 0.0f;
-                ref = root;
-                sp = 0;
-                bt = tmax;
-                best = -1;
-                has = true;
+                c.ref = root;
+                c.sp = 0;
+                c.bt = tmax;
+                c.best = -1;
+                c.has = true;
                 alive = true;
                 parked = false;
             }
             const uint32_t pm = (uint32_t)__builtin_popcountll(M);
             next += pm < nr - next ? pm : nr - next;
         }
-        if (!__any(has)) break;
+        if (!__any(c.has)) break;
         // node phase: step until every lane with a ray holds a parked leaf or is finished
         for (;;) {
-            if (has && alive && ref < 0 && !parked) {
+            if (c.has && alive && c.ref < 0 && !parked) {
                 parked = true;
-                lref = ref;
-                if (sp == 0) alive = false;
-                else { sp -= 1; ref = stk[sp * kBlock]; }
+                lref = c.ref;
+                if (c.sp == 0) alive = false;
+                else { c.sp -= 1; c.ref = stk[c.sp * kBlock]; }
             }
-            const bool step = has && alive && ref >= 0;
-            if (!__any(step) || __all(!has || parked || !alive)) break;
-            if (step) bvh4_step(qn, stk, o, inv, px, py, pz, tmin, bt, ref, sp, alive);
+            const bool step = c.has && alive && c.ref >= 0;
+            if (!__any(step) || __all(!c.has || parked || !alive)) break;
+            if (step) bvh4_step(qn, stk, o, inv, px, py, pz, tmin, c.bt, c.ref, c.sp, alive);
         }
         if (parked) {
-            bvh_leaf<kBvhPoolChunk>(btri, lref, o, d, tmin, bt, best, slots);
+            bvh_leaf<kBvhPoolChunk>(btri, lref, o, d, tmin, c.bt, c.best, slots);
             parked = false;
         }
-        if (has && !alive) {            // this ray is done: leave its result for the owner
-            res[r] = make_float2(bt, __int_as_float(best));
-            has = false;
+        if (c.has && !alive) {          // this ray is done: leave its result for the owner
+            res[c.key] = make_float2(c.bt, __int_as_float(c.best));
+            c.has = false;
         }
+        if (carry_ok && next >= nr &&
+            (uint32_t)__builtin_popcountll(__ballot(c.has)) <= kBvhCarryMax)
+            break;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (sA) {
-        const float2 v = res[rank_in(mA)];
-        btA = v.x;
-        bestA = __float_as_int(v.y);
-    }
-    if (sB) {
-        const float2 v = res[nA + rank_in(mB)];
-        btB = v.x;
-        bestB = __float_as_int(v.y);
+    const float2 va = res[2 * lane], vb = res[2 * lane + 1];
+    const bool readyA = !subA || __float_as_int(va.y) != -2;
+    const bool readyB = !subB || __float_as_int(vb.y) != -2;
+    frozen = !(readyA && readyB);
+    if (!frozen) {
+        if (subA) { btA = va.x; bestA = __float_as_int(va.y); }
+        if (subB) { btB = vb.x; bestB = __float_as_int(vb.y); }
+        subA = false;
+        subB = false;
     }
 }
 
@@ -1494,6 +1536,11 @@ __device__ __forceinline__ void path_body(
     float nee_dist = 0.0f;
     bool hasB = false;
     f3 b_o = mk(0, 0, 0), b_d = mk(0, 0, 1);
+    // BVH pool (BVH, !SINGLE): rays submitted to the pool and not yet resolved, the traversal
+    // this lane carries into the next iteration, and whether this lane waits on a carried ray
+    constexpr bool CARRY = BVH && !SINGLE;
+    bool subA = false, subB = false;
+    BvhCarry carry;
 
     for (;;) {
         // ---- settle: end samples, take pixels, emit surface events ----
@@ -1627,7 +1674,12 @@ __device__ __forceinline__ void path_body(
             break;
         }
         if (wave_active) iters += 1;
-        trav_wave += (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
+        // CARRY: a lane waiting on a carried ray keeps hasA / hasB without new traversals
+        const bool newA = CARRY ? hasA && !subA : sA, newB = CARRY ? hasB && !subB : sB;
+        trav_wave += CARRY ? (uint32_t)__builtin_popcountll(__ballot(newA)) +
+                                 (uint32_t)__builtin_popcountll(__ballot(newB))
+                           : (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
+        bool frozen = false;
         if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
 
         int bestA = -1, bestB = -1;
@@ -1861,8 +1913,9 @@ __device__ __forceinline__ void path_body(
             if (!SINGLE) {
                 float4 *pl = pool + wv * 72;            // res: 64 float4 (128 float2), tab: 8 float4
                 bvh_pool(bvh_nodes, bvh_tris, A.bvh_root, stk, reinterpret_cast<uint8_t *>(pl + 64),
-                         reinterpret_cast<float2 *>(pl), lane, sA, sB, s_ao, s_ad, b_o, b_d, A.t_min,
-                         A.t_max, btA, bestA, btB, bestB, A.bvh_n4, A.bvh_slots);
+                         reinterpret_cast<float2 *>(pl), lane, newA, newB, s_ao, s_ad, b_o, b_d,
+                         A.t_min, A.t_max, !q.exhausted, carry, subA, subB, frozen, btA, bestA,
+                         btB, bestB, A.bvh_n4, A.bvh_slots);
             } else
             {
             if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA, A.bvh_n4, A.bvh_slots);
@@ -2022,7 +2075,7 @@ __device__ __forceinline__ void path_body(
 
         // ---- resolve A: visibility of the light sample (:447-459) ----
         if (LDS_STATE) col = st_get3(13);
-        if (hasA) {
+        if (hasA && !frozen) {
             if (LDS_STATE) {
                 a_p = st_get3(0);
                 nee_C = st_get3(3);
@@ -2038,7 +2091,9 @@ __device__ __forceinline__ void path_body(
         }
         // ---- resolve B: next bounce (:421-429) ----
         const bool defer_B = SINGLE && hasA && hasB;    // B was not traced this iteration
-        if (hasB && !defer_B) {
+        if (frozen) {
+            // waiting on a carried ray: nothing resolves, the rays stay pending
+        } else if (hasB && !defer_B) {
             if (bestB < 0) {
                 col = add(col, mk(0.1f, 0.1f, 0.1f));
                 if (LDS_STATE) st_put3(13, col);
@@ -2057,8 +2112,10 @@ __device__ __forceinline__ void path_body(
         } else if (hasA && !hasB) {
             ended = true;       // the path ended at its last surface event (RR / depth / att)
         }
-        hasA = false;
-        if (!defer_B) hasB = false;
+        if (!frozen) {
+            hasA = false;
+            if (!defer_B) hasB = false;
+        }
     }
     flush_wave_counters(counters, lane, trav_wave, iters);
     if (A.timeline && lane == 0) {

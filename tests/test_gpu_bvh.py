@@ -107,3 +107,11 @@ def test_bvh_full_c3_identical(cornell):
     a = _render(cornell, 1024, 1024, 123.0, spp=30)
     b = _render(cornell, 1024, 1024, 123.0, spp=30, accel=rvcp_amd.abi.ACCEL_BVH)
     assert np.array_equal(a[0], b[0])
+
+
+def test_bvh_carried_traversals(cornell):
+    """A frame large enough that the wave pools carry unfinished traversals into later
+    iterations (bvh_pool): frozen owners and resumed stacks must leave every
+    pixel and the traversal count as the brute-force scan has them."""
+    sc = rvcp_amd.scene.with_random_triangles(cornell, 20000)
+    _same(sc, 192, 160, spp=4, time=2.5)

@@ -86,6 +86,9 @@ for s in $STEPS; do
         abrcp) run ab_rcp 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3" "dbg=RVCP_LIB=$DBG::--workload c3" "unif=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_RCP_UNIFORM::--workload c3" "sqrt=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_SQRT=1::--workload c3" "fract=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_FRACT=1::--workload c3" "all=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_SQRT=1 -DRVCP_FAST_FRACT=1 -DRVCP_SPEC_RCP_UNIFORM::--workload c3" "ldsc=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_LDS_SCENE::--workload c3" "neeoff=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_NEE_SAME_OFF::--workload c3" ;;
         sqpmc3) run sqpmc3 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVE_CYCLES -d "$OUT/sqpmc3_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
         sqrtchk) run sqrt_check 300 tools/build/sqrt_check ;;
+        bvhtest) run pytest_bvh 600 python -u -m pytest tests/test_gpu_bvh.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+        abbvh) run ab_bvh 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" "c0=RVCP_LIB=tools/build/var_c0/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" "c4=RVCP_LIB=tools/build/var_c4/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" "c8=::--workload c5 --accel bvh --steps 10 --warmup 2" "c16=RVCP_LIB=tools/build/var_c16/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" "c8m16=RVCP_LIB=tools/build/var_c8m16/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" ;;
+        abm2b) run ab_m2b 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload spheres --steps 60" "w5=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_MIN_WAVES=5::--workload spheres --steps 60" "lds5=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=5::--workload spheres --steps 60" "lds6=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=6::--workload spheres --steps 60" "lds4=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=4::--workload spheres --steps 60" ;;
         abgen) run ab_gen 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3gen" "new=::--workload c3gen" ;;
         abm2) run ab_m2 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload spheres --steps 60" "lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE::--workload spheres --steps 60" "lds5=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=5::--workload spheres --steps 60" "c3m2=RVCP_LIB=$DBG::--workload c3m2" "c3m2lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE::--workload c3m2" ;;
         abgrp) run ab_grp 900 python tools/ab.py --runner frames --passes 2 "prod=::--size 384 --spp 10 --frames 20" "g2=RVCP_LIB=tools/build/var_g2/librvcp.so::--size 384 --spp 10 --frames 20" "g4=RVCP_LIB=tools/build/var_g4/librvcp.so::--size 384 --spp 10 --frames 20" "prodc3=::--frames 10" "g2c3=RVCP_LIB=tools/build/var_g2/librvcp.so::--frames 10" "g4c3=RVCP_LIB=tools/build/var_g4/librvcp.so::--frames 10" ;;
