@@ -421,7 +421,7 @@ JitKernels::~JitKernels()
 }
 
 int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
-                     bool legacy, int legacy_waves)
+                     bool legacy, int legacy_waves, bool lds_scene)
 {
     const RtcApi &api = rtc();
     if (!api.ok) {
@@ -444,6 +444,7 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
     if (legacy) opts.push_back("-DRVCP_JIT_LEGACY");
     const std::string lw = "-DRVCP_LEGACY_MIN_WAVES=" + std::to_string(legacy_waves);
     if (legacy && legacy_waves > 0) opts.push_back(lw.c_str());
+    if (legacy && lds_scene) opts.push_back("-DRVCP_LEGACY_LDS_SCENE");
     for (const std::string &x : extra) opts.push_back(x.c_str());
     const int rc = api.compile(prog, (int)opts.size(), opts.data());
     if (rc != 0) {
@@ -464,19 +465,25 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
 }
 
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
-                                             std::string &err, bool legacy, bool sphereless)
+                                             std::string &err, bool legacy, bool sphereless,
+                                             bool lds_fits)
 {
     // Mode 2 on a scene without spheres (the Cornell frame): 6 waves per SIMD measured 2.5 %
-    // faster than 5, with spheres 5 % slower (profiles/r02_legacy_waves_ab.log).
+    // faster than 5, with spheres 5 % slower (profiles/r02_legacy_waves_ab.log).  With the
+    // scene in LDS (lds_fits): the sphere room 0.288 -> 0.278 ms at 5 waves (4 and 6: 0.305,
+    // 0.308; 5 waves without LDS 0.290), the Cornell frame 1.867 -> 1.831 ms at 6
+    // (profiles/r04d_ab_m2.log, r04e_ab_m2b.log).
     // (debug build: RVCP_JIT_LEGACY_WAVES overrides; 0 = the compiler's choice)
-    int legacy_waves = legacy && sphereless ? 6 : 0;
+    const bool lds_scene = legacy && lds_fits;
+    int legacy_waves = legacy && sphereless ? 6 : lds_scene ? 5 : 0;
 #ifdef RVCP_DEBUG_KNOBS
     if (const char *e = std::getenv("RVCP_JIT_LEGACY_WAVES")) legacy_waves = std::atoi(e);
 #endif
     std::string key_flags;
     for (const std::string &x : jit_extra_flags()) key_flags += " " + x;
     const std::string scan = jit_scan_source(tri, n) +
-        (legacy ? "// +legacy " + std::to_string(legacy_waves) + "\n" : std::string()) +
+        (legacy ? "// +legacy " + std::to_string(legacy_waves) + (lds_scene ? " lds" : "") + "\n"
+                : std::string()) +
         (key_flags.empty() ? std::string() : "// +flags" + key_flags + "\n");
     const uint64_t h = fnv1a(scan);
     std::lock_guard<std::mutex> lock(g_mu);
@@ -487,7 +494,7 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         }
     }
     std::vector<char> code;
-    if (jit_compile_code(scan, code, err, legacy, legacy_waves) != 0) return nullptr;
+    if (jit_compile_code(scan, code, err, legacy, legacy_waves, lds_scene) != 0) return nullptr;
     auto k = std::make_shared<JitKernels>();
     k->device = device;
     if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&k->module, code.data()) != hipSuccess) {

@@ -34,13 +34,16 @@ std::vector<std::string> jit_extra_flags();
 std::string jit_scan_source(const TriRecord *tri, uint32_t n);
 // Compile rvcp_kernels.hip with the given scan for gfx950 (hipRTC); 0 or -1 with err set.
 // `legacy` also builds the mode-2 kernel (RVCP_JIT_LEGACY).
+// `lds_scene`: the mode-2 kernel copies the scene into LDS (RVCP_LEGACY_LDS_SCENE).
 int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
-                     bool legacy = false, int legacy_waves = 0);
+                     bool legacy = false, int legacy_waves = 0, bool lds_scene = false);
 // Compiled + loaded kernels for the scene on `device` (process-wide cache keyed by the scan
 // source and `legacy`); nullptr with err set when hipRTC is unavailable or compilation fails.
 // `sphereless`: the mode-2 kernel is built for 6 waves per SIMD.
+// `lds_fits`: at most 64 spheres and 64 materials (and, as always here, 64 faces): the mode-2
+// kernel reads its hit records, spheres and materials from LDS copies.
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
                                              std::string &err, bool legacy = false,
-                                             bool sphereless = false);
+                                             bool sphereless = false, bool lds_fits = false);
 
 }  // namespace rvcp

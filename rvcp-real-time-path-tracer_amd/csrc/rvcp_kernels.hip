@@ -2595,8 +2595,9 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
 {
     __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
 #ifdef RVCP_LEGACY_LDS_SCENE
-    // A/B (scenes of at most 64 spheres, materials and faces): the per-lane gathers of the hit
-    // record and the scatter read LDS copies instead of global memory
+    // scenes of at most 64 spheres, materials and faces (rvcp_jit.cpp, lds_fits): the per-lane
+    // gathers of the hit record, the spheres and the scatter's material read LDS copies
+    // instead of global memory (sphere room -3.5 %, mode 2 on the C3 frame -2 %)
     __shared__ TriRecord sh_tri[64];
     __shared__ FaceShade sh_shade[64];
     __shared__ rvcp_sphere_t sh_sph[64];
