@@ -557,7 +557,7 @@ __device__ __forceinline__ void bvh4_step(const Bvh4QNode *__restrict__ qn, lds_
 // makes progress and the last iterations drain everything.
 constexpr uint32_t kBvhPoolChunk = 2;      // leaf triangles loaded together in bvh_pool
 #ifndef RVCP_BVH_CARRY_MAX
-#define RVCP_BVH_CARRY_MAX 8
+#define RVCP_BVH_CARRY_MAX 48
 #endif
 #ifndef RVCP_BVH_CARRY_MIN_RAYS
 #define RVCP_BVH_CARRY_MIN_RAYS 32
@@ -2634,9 +2634,29 @@ extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_pa
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];
     __shared__ float state_lds[kStateCols * kBlock];
+#ifdef RVCP_SPEC_LDS_SCENE
+    // A/B: the scene's triangle and shading records (at most 64 faces in this module) copied
+    // into LDS once per workgroup, so the hit record's per-lane gathers and the tail
+    // partition's triangle reads are LDS reads (latency of a small frame's serial chain)
+    __shared__ TriRecord sh_tri[64];
+    __shared__ FaceShade sh_shade[64];
+    {
+        const float4 *src = reinterpret_cast<const float4 *>(tri);
+        float4 *dst = reinterpret_cast<float4 *>(sh_tri);
+        for (uint32_t e = threadIdx.x; e < 3u * A.n_faces; e += kBlock) dst[e] = src[e];
+        const float4 *src2 = reinterpret_cast<const float4 *>(shade);
+        float4 *dst2 = reinterpret_cast<float4 *>(sh_shade);
+        for (uint32_t e = threadIdx.x; e < 4u * A.n_faces; e += kBlock) dst2[e] = src2[e];
+        __syncthreads();
+    }
+    path_body<false, false, false, true>(
+        A, sh_tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, sh_shade, tail_tab,
+        nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+#else
     path_body<false, false, false, true>(
         A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+#endif
 }
 extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,

@@ -10,7 +10,8 @@ limit; one line per (pass, case), then the median per case.
 Runners:
   bench     python bench.py --no-cpu-baseline --launch-pass 0 --steps 40 --warmup 5 ARGS
             (ms_per_step, the driver's figure: frames in flight and batches as the bench
-            picks them unless ARGS fix them)
+            picks them unless ARGS fix them; --field picks another key of the line, e.g.
+            config.frame_latency_ms_alone with ARGS --launch-pass 40)
   frames    python tools/frames.py --frames 20 ARGS  (one frame at a time, path-kernel ms:
             median of the frames after the first 3)
   share     python tools/rank_share.py ARGS  (rank 0's share of the N-GPU C4 frame alone)
@@ -46,11 +47,15 @@ def parse_case(text):
     return label, env, shlex.split(args)
 
 
-def measure(runner, out):
-    """The case's figure from the runner's stdout (ms)."""
+def measure(runner, out, field="ms_per_step"):
+    """The case's figure from the runner's stdout (ms); `field`: the bench line's key, dotted
+    for nested ones (config.frame_latency_ms_alone)."""
     lines = [l for l in out.splitlines() if l.startswith("{")]
     if runner == "bench":
-        return json.loads(lines[-1])["ms_per_step"]
+        v = json.loads(lines[-1])
+        for k in field.split("."):
+            v = v[k]
+        return v
     if runner == "frames":
         ms = sorted(json.loads(l)["kernel_ms"] for l in lines[3:] or lines)
         return ms[len(ms) // 2]
@@ -63,6 +68,7 @@ def main():
     ap.add_argument("--runner", choices=sorted(RUNNERS), default="bench")
     ap.add_argument("--passes", type=int, default=2)
     ap.add_argument("--timeout", type=int, default=200)
+    ap.add_argument("--field", default="ms_per_step", help="bench runner: the figure to compare")
     ap.add_argument("cases", nargs="+")
     a = ap.parse_args()
     cases = [parse_case(c) for c in a.cases]
@@ -77,7 +83,7 @@ def main():
                 if r.returncode >= 124:      # time limit / signal: stop here
                     sys.exit(r.returncode)
                 continue
-            v = measure(a.runner, r.stdout)
+            v = measure(a.runner, r.stdout, a.field)
             got[label].append(v)
             print(f"pass {p} {label:>24}  {v:.4f} ms", flush=True)
     for label, vals in got.items():
