@@ -214,12 +214,22 @@ struct Gen {
     }
 };
 
+// Per ray: the t of its previous test and the name of that test's range mask, tmin <= t <= bt
+// evaluated before it.  The next test of the ray with the same t (the other triangle of an
+// axis-aligned quad: one plane, one denominator, one t) reuses the mask: between the two tests
+// bt changed only if the first accepted, and then to t itself, so t <= bt holds before the
+// second exactly when it held before the first (2 of the 5 compares of a quad's second test).
+struct RangeMask {
+    std::string t, name;
+};
+
 // One triangle's test for ray `r` ("" / "A" / "B"), split into its arithmetic (`decl`: every
-// value that does not depend on the running nearest hit, temporaries named <prefix>r<k>) and
-// its acceptance (`accept`: the compares with `t <= bt` and the update); false when it can
-// never accept.
+// value that does not depend on the running nearest hit, temporaries named <prefix>r<k>, then
+// the range mask, which reads the nearest hit as the previous commit left it) and its
+// acceptance (`accept`: the update); false when it can never accept.
 bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, uint32_t index,
-                   const char *r, std::map<std::string, std::string> &seen)
+                   const char *r, std::map<std::string, std::string> &seen,
+                   std::map<std::string, RangeMask> &prev)
 {
     Gen g;
     g.seen = &seen;
@@ -261,56 +271,47 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     if (!b1.empty() && !b2.empty()) add("(" + b1 + " + " + b2 + " <= 1.0f)");
     else if (!b1.empty()) add("(" + b1 + " <= 1.0f)");
     else if (!b2.empty()) add("(" + b2 + " <= 1.0f)");
-    add("(" + t + " >= tmin)");
     decl += g.out;
+    RangeMask &pm = prev[R];
+    if (pm.name.empty() || pm.t != t) {
+        pm.t = t;
+        pm.name = g.prefix + "q";
+        decl += "    const bool " + pm.name + " = (" + t + " >= tmin) & (" + t + " <= bt" + R + ");\n";
+    }
+    add(pm.name);
     // the dual scan's shadow ray (slot A) needs the nearest t and whether there was a hit, not
     // the face: only its t is kept (btA != t_max after the scan means a hit;
     // the caller resolves btA == t_max, a miss or a hit at exactly t_max, with the generic scan)
     if (R == "A")
-        accept += "        if (" + cond + " & (" + t + " <= btA)) btA = " + t + ";\n";
+        accept += "        if (" + cond + ") btA = " + t + ";\n";
     else
-        accept += "        if (" + cond + " & (" + t + " <= bt" + R + ")) { bt" + R + " = " + t + "; best" +
-                  R + " = " + std::to_string(index) + "; }\n";
+        accept += "        if (" + cond + ") { bt" + R + " = " + t + "; best" + R + " = " +
+                  std::to_string(index) + "; }\n";
     return true;
 }
 
-// Tests per commit group.  RVCP_SPEC_COMMIT(t, i) after a group makes its result final before
-// the next group starts: without it the compiler interleaves all unrolled tests and spills
-// hundreds of registers.  Within a group the arithmetic of every test comes first (it does not
-// depend on the running nearest hit) and the acceptances follow in triangle order, so the
-// tests of a group are independent chains (ILP) and the order rule is the loop's.
-#ifndef RVCP_SPEC_GROUP1
-#define RVCP_SPEC_GROUP1 1        // single-ray scan (mode 2, the compact scan): tests per group
-#endif
-#ifndef RVCP_SPEC_GROUP2
-#define RVCP_SPEC_GROUP2 1        // dual-ray scan: (triangle, ray) tests per group, in the order
-#endif                            // (0, A), (0, B), (1, A), ...
-
+// One test per commit: RVCP_SPEC_COMMIT(t, i) after each test makes its result final before
+// the next test starts (without it the compiler interleaves all unrolled tests and spills
+// hundreds of registers), in the order (0, A), (0, B), (1, A), ... of the dual scan.  Groups of
+// two or four tests between commits (their arithmetic first, then the acceptances in order)
+// measured within +-1 % and were removed: a range mask (RangeMask) must read
+// the nearest hit after the previous test's acceptance, which a group's shared prologue does
+// not.
 void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *const *rays,
-               int n_rays, uint32_t group)
+               int n_rays)
 {
-    const uint32_t units = n * (uint32_t)n_rays;
     std::map<std::string, std::string> seen;
-    for (uint32_t u0 = 0; u0 < units; u0 += group) {
+    std::map<std::string, RangeMask> prev;
+    for (uint32_t u = 0; u < n * (uint32_t)n_rays; u++) {
         std::string decl, accept;
-        bool used[2] = {false, false};
-        for (uint32_t u = u0; u < units && u < u0 + group; u++) {
-            const int r = (int)(u % (uint32_t)n_rays);
-            if (emit_triangle(decl, accept, tri[u / (uint32_t)n_rays], u / (uint32_t)n_rays, rays[r],
-                              seen))
-                used[r] = true;
-        }
-        if (accept.empty()) {
-            out += decl;
-            continue;
-        }
-        out += decl + "    {\n" + accept + "    }\n";
-        for (int r = 0; r < n_rays; r++) {
-            if (!used[r]) continue;
-            const std::string R(rays[r]);
-            out += R == "A" ? "    RVCP_SPEC_COMMIT1(btA);\n"
-                            : "    RVCP_SPEC_COMMIT(bt" + R + ", best" + R + ");\n";
-        }
+        const std::string R(rays[u % (uint32_t)n_rays]);
+        const bool used = emit_triangle(decl, accept, tri[u / (uint32_t)n_rays],
+                                        u / (uint32_t)n_rays, R.c_str(), seen, prev);
+        out += decl;
+        if (!used) continue;
+        out += "    {\n" + accept + "    }\n";
+        out += R == "A" ? "    RVCP_SPEC_COMMIT1(btA);\n"
+                        : "    RVCP_SPEC_COMMIT(bt" + R + ", best" + R + ");\n";
     }
 }
 
@@ -339,11 +340,11 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n)
     out += "__device__ __forceinline__ void spec_scan1(f3 o, f3 d, float tmin, float &bt, "
            "int &best) {\n";
     static const char *const one[] = {""}, *const two[] = {"A", "B"};
-    emit_scan(out, tri, n, one, 1, RVCP_SPEC_GROUP1);
+    emit_scan(out, tri, n, one, 1);
     out += "}\n";
     out += "__device__ __forceinline__ void spec_scan2(f3 oA, f3 dA, f3 oB, f3 dB, float tmin, "
            "float &btA, float &btB, int &bestB) {\n";
-    emit_scan(out, tri, n, two, 2, RVCP_SPEC_GROUP2);
+    emit_scan(out, tri, n, two, 2);
     out += "}\n";
     return out;
 }

@@ -117,11 +117,11 @@ def test_library_links_no_oracle():
 
 
 def test_product_library_reads_no_debug_knobs():
-    """Experiment knobs (RVCP_DEBUG_*, RVCP_NO_SPECIALIZE, RVCP_SPEC_GROUP*) live only in the
+    """Experiment knobs (RVCP_DEBUG_*, RVCP_NO_SPECIALIZE) live only in the
     -DRVCP_DEBUG_KNOBS build (csrc/build/librvcp_debug.so); the product library must not
     change behaviour with the environment."""
     blob = open(abi.LIB_PATH, "rb").read()
-    for knob in (b"RVCP_DEBUG_", b"RVCP_NO_SPECIALIZE", b"RVCP_SPEC_GROUP", b"RVCP_JIT_FLAGS"):
+    for knob in (b"RVCP_DEBUG_", b"RVCP_NO_SPECIALIZE", b"RVCP_JIT_FLAGS"):
         assert knob not in blob, knob
     dbg = os.path.join(os.path.dirname(abi.LIB_PATH), "librvcp_debug.so")
     if os.path.exists(dbg):
