@@ -84,6 +84,11 @@ struct alignas(16) TriRecord {
 };
 static_assert(sizeof(TriRecord) == 48, "TriRecord is 48 B");
 
+// Scenes up to this many faces get the scene-specialised scan (rvcp_jit.cpp; the unrolled code
+// grows with the face count, and the specialised kernels keep the scene in LDS arrays of this
+// size).
+constexpr uint32_t kJitMaxFaces = 64;
+
 // One entry of the light table: a luminous face as sample_light_games101 sees it
 // (ray_tracer_games101_branch.comp:384-404), with the std140 id quirk already applied.
 struct alignas(16) LightRecord {

@@ -12,9 +12,6 @@
 
 namespace rvcp {
 
-// Scenes up to this many faces get the specialised scan (the unrolled code grows with F).
-constexpr uint32_t kJitMaxFaces = 64;
-
 struct JitKernels {
     int device = 0;
     hipModule_t module = nullptr;

@@ -2634,12 +2634,15 @@ extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_pa
     __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
     __shared__ float4 compact_lds[kBlock / kWave * 2 * kWave];
     __shared__ float state_lds[kStateCols * kBlock];
-#ifdef RVCP_SPEC_LDS_SCENE
-    // A/B: the scene's triangle and shading records (at most 64 faces in this module) copied
+    // The scene's triangle and shading records (at most 64 faces in this module) are copied
     // into LDS once per workgroup, so the hit record's per-lane gathers and the tail
-    // partition's triangle reads are LDS reads (latency of a small frame's serial chain)
-    __shared__ TriRecord sh_tri[64];
-    __shared__ FaceShade sh_shade[64];
+    // partition's triangle reads are LDS reads: a small frame's serial chain waits on them
+    // every iteration (C2 one frame alone 0.492 -> 0.485 ms, its path kernel 0.470 -> 0.459;
+    // C3 unchanged, profiles/r04g_ab_c2lds*.log).  31.5 KB per workgroup: 5 per CU still fit.
+    __shared__ TriRecord sh_tri[kJitMaxFaces];
+    __shared__ FaceShade sh_shade[kJitMaxFaces];
+    static_assert(5 * (sizeof(tail_tab) + sizeof(compact_lds) + sizeof(state_lds) + sizeof(sh_tri) +
+                       sizeof(sh_shade)) <= 160 * 1024, "5 workgroups per CU");
     {
         const float4 *src = reinterpret_cast<const float4 *>(tri);
         float4 *dst = reinterpret_cast<float4 *>(sh_tri);
@@ -2652,11 +2655,6 @@ extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_pa
     path_body<false, false, false, true>(
         A, sh_tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, sh_shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
-#else
-    path_body<false, false, false, true>(
-        A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, shade, tail_tab,
-        nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
-#endif
 }
 extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,

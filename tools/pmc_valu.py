@@ -10,6 +10,10 @@
               profiles/r02_valu_rate_pmc.txt): how close the kernel is to the
               VALU issue rate actually reachable
 
+  lane_utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU), when the second pass
+              holds both (the active lanes per VALU instruction; 0.998 on the C5 pool kernel,
+              whose waves are full: DESIGN.md §4.7)
+
 GRBM_GUI_ACTIVE is summed over the 8 XCDs by rocprofv3, so it is divided by 8 to get the
 kernel's cycles.  Writes the JSON bench.py reads into roofline.valu_busy_pmc /
 roofline.valu_issue_frac_pmc.
@@ -44,6 +48,8 @@ def main():
     a = ap.parse_args()
     valu = per_kernel(a.sq_csv, "SQ_INSTS_VALU")
     grbm = per_kernel(a.grbm_csv, "GRBM_GUI_ACTIVE")
+    thr = per_kernel(a.grbm_csv, "SQ_THREAD_CYCLES_VALU")
+    act = per_kernel(a.grbm_csv, "SQ_ACTIVE_INST_VALU")
     out = {"workload": a.workload, "sources": [a.sq_csv, a.grbm_csv],
            "method": "SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE / xcds x simds), per launch; "
                      "issue_frac = SQ_INSTS_VALU / (cycles x simds) / measured issue peak",
@@ -55,6 +61,8 @@ def main():
         out["kernels"][k] = {"valu_insts": v, "cycles": g,
                              "valu_busy": round(2.0 * v / (g * a.simds), 4) if g else None,
                              "issue_frac": round(v / (g * a.simds) / a.issue_peak, 4) if g else None}
+        if thr.get(k) and act.get(k) and sum(act[k]) > 0:
+            out["kernels"][k]["lane_utilisation"] = round(sum(thr[k]) / (64.0 * sum(act[k])), 4)
     with open(a.out_json, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
