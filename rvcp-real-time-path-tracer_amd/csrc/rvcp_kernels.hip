@@ -2652,9 +2652,17 @@ extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_pa
         for (uint32_t e = threadIdx.x; e < 4u * A.n_faces; e += kBlock) dst2[e] = src2[e];
         __syncthreads();
     }
+#ifdef RVCP_SPEC_REG_STATE
+    // A/B: the path state in registers instead of LDS columns (fewer LDS round trips on a
+    // small frame's serial chain)
+    path_body<false, false, false, false>(
+        A, sh_tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, sh_shade, tail_tab,
+        nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+#else
     path_body<false, false, false, true>(
         A, sh_tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf, sh_shade, tail_tab,
         nullptr, nullptr, nullptr, nullptr, compact_lds, state_lds);
+#endif
 }
 extern "C" __global__ __launch_bounds__(kBlock, 6) void rvcp_spec_path_kernel6(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
