@@ -2332,11 +2332,8 @@ __device__ __forceinline__ void legacy_body(
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    uint8_t (*coop_tab)[kWave], const rvcp_sphere_t *__restrict__ sph_loop = nullptr)
+    uint8_t (*coop_tab)[kWave])
 {
-    // sph_loop: where the trace's sphere loop reads its (wave-uniform) records; the hit
-    // record's per-lane gather reads `sph`
-    if (!sph_loop) sph_loop = sph;
     uint8_t *tab = coop_tab[threadIdx.x / kWave];
     const uint32_t lane = lane_id();
     Queue q = queue_init(A);
@@ -2487,12 +2484,12 @@ __device__ __forceinline__ void legacy_body(
                 const float y = rcp_ieee(two_a);
                 for (uint32_t i = 0; i < A.n_spheres; ++i) {
                     float t;
-                    if (sphere_accept<true>(sph_loop[i], ro, rd, a, two_a, y, rtmin, bt, t)) { bt = t; best = (int)i; }
+                    if (sphere_accept<true>(sph[i], ro, rd, a, two_a, y, rtmin, bt, t)) { bt = t; best = (int)i; }
                 }
             } else {
                 for (uint32_t i = 0; i < A.n_spheres; ++i) {
                     float t;
-                    if (sphere_accept<false>(sph_loop[i], ro, rd, a, two_a, 0.0f, rtmin, bt, t)) { bt = t; best = (int)i; }
+                    if (sphere_accept<false>(sph[i], ro, rd, a, two_a, 0.0f, rtmin, bt, t)) { bt = t; best = (int)i; }
                 }
             }
 #ifdef RVCP_SPEC_SCAN
@@ -2616,13 +2613,9 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
            2u * (A.n_mats < 64u ? A.n_mats : 64u));
         __syncthreads();
     }
-#ifdef RVCP_LEGACY_SPH_GLOBAL
-    // A/B: the sphere loop's uniform records from global memory (scalar loads)
-    legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab,
-                sph);
-#else
+    // (the sphere loop's wave-uniform records read from global memory by scalar loads instead,
+    // beside the LDS copies for the per-lane gathers: 0.2855 vs 0.2814 ms, profiles/r04i_ab_m2c.log)
     legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab);
-#endif
 #else
     legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
 #endif
