@@ -17,8 +17,13 @@ DBG=rvcp-real-time-path-tracer_amd/csrc/build/librvcp_debug.so
 run() {  # run <name> <timeout> cmd...
     local name=$1 lim=$2; shift 2
     echo "=== $name ($(date +%T))"
+    # heartbeat: a fresh box's first `import torch` can take minutes (the image pages in); the
+    # step's own time limit, not silence, ends a step that hangs
+    ( while sleep 60; do echo "    ... $name running ($(date +%T))"; done ) &
+    local hb=$!
     timeout -k 10 "$lim" "$@" > "$OUT/${TAG}_$name.log" 2>&1
     local rc=$?
+    kill $hb 2>/dev/null; wait $hb 2>/dev/null
     echo "=== $name rc=$rc"
     tail -n 25 "$OUT/${TAG}_$name.log"
     case $rc in
@@ -95,6 +100,7 @@ for s in $STEPS; do
         tracec2) run tracec2 300 rocprofv3 --kernel-trace --stats -d "$OUT/tracec2_$TAG" -o run --output-format csv -- python3 tools/frames.py --size 384 --spp 10 --frames 30 ;;
         abc2lds) run ab_c2lds 900 python tools/ab.py --runner bench --field config.frame_latency_ms_alone --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload c2 --steps 40 --launch-pass 40" "lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_LDS_SCENE::--workload c2 --steps 40 --launch-pass 40" && run ab_c2lds_k 900 python tools/ab.py --runner frames --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--size 384 --spp 10 --frames 40" "lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_LDS_SCENE::--size 384 --spp 10 --frames 40" "c3dbg=RVCP_LIB=$DBG::--frames 12" "c3lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_LDS_SCENE::--frames 12" ;;
         abreg) run ab_reg_lat 900 python tools/ab.py --runner bench --field config.frame_latency_ms_alone --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload c2 --steps 40 --launch-pass 40" "reg=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_REG_STATE::--workload c2 --steps 40 --launch-pass 40" && run ab_reg 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "c3dbg=RVCP_LIB=$DBG::--workload c3" "c3reg=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_REG_STATE::--workload c3" "c2dbg=RVCP_LIB=$DBG::--workload c2 --steps 100" "c2reg=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_REG_STATE::--workload c2 --steps 100" ;;
+        abspread) run ab_spread 900 python tools/ab.py --runner bench --field config.frame_latency_ms_alone --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload c2 --steps 40 --launch-pass 40" "sp32=RVCP_LIB=$DBG,RVCP_DEBUG_SPREAD=32::--workload c2 --steps 40 --launch-pass 40" "sp24=RVCP_LIB=$DBG,RVCP_DEBUG_SPREAD=24::--workload c2 --steps 40 --launch-pass 40" "sp16=RVCP_LIB=$DBG,RVCP_DEBUG_SPREAD=16::--workload c2 --steps 40 --launch-pass 40" "sp16et=RVCP_LIB=$DBG,RVCP_DEBUG_SPREAD=16,RVCP_DEBUG_EARLY_TAIL=1::--workload c2 --steps 40 --launch-pass 40" "et=RVCP_LIB=$DBG,RVCP_DEBUG_EARLY_TAIL=1::--workload c2 --steps 40 --launch-pass 40" ;;
         abgen) run ab_gen 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3gen" "new=::--workload c3gen" ;;
         abm2) run ab_m2 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload spheres --steps 60" "lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE::--workload spheres --steps 60" "lds5=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=5::--workload spheres --steps 60" "c3m2=RVCP_LIB=$DBG::--workload c3m2" "c3m2lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE::--workload c3m2" ;;
         abgrp) run ab_grp 900 python tools/ab.py --runner frames --passes 2 "prod=::--size 384 --spp 10 --frames 20" "g2=RVCP_LIB=tools/build/var_g2/librvcp.so::--size 384 --spp 10 --frames 20" "g4=RVCP_LIB=tools/build/var_g4/librvcp.so::--size 384 --spp 10 --frames 20" "prodc3=::--frames 10" "g2c3=RVCP_LIB=tools/build/var_g2/librvcp.so::--frames 10" "g4c3=RVCP_LIB=tools/build/var_g4/librvcp.so::--frames 10" ;;
