@@ -32,6 +32,7 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -102,13 +103,45 @@ const RtcApi &rtc()
 // and `key` spells the magnitude's whole expression with commutative operands in a fixed
 // order, so that equal expressions anywhere in the scan are computed once: the shared
 // denominator of an axis-aligned quad's two triangles, the products d.y * c they repeat, ...
+//
+// `grain`: every value is an integer multiple of 2^grain (kNoGrain: not known).  A literal's is
+// its lowest set bit; a ray direction component's is kDirGrain, which the kernel's per-wave
+// check dir_grain_ok establishes (every component 0 or at least 2^-40 in magnitude, so a multiple
+// of its ulp >= 2^-63); o's is not known.  The exact product, sum or fma of multiples of 2^ga and
+// 2^gb is a multiple of 2^(ga + gb) resp. 2^min(ga, gb), and rounding to float keeps a multiple of
+// 2^g (g >= -149) a multiple of 2^g, non-zero values at least 2^g in magnitude (2^g is a float
+// and rounding is monotone).  `mag`: |value| <= 2^mag (ray_in_range: |d_i| <= 16, |o_i| <=
+// 2^41; a product 2^(ma + mb), a sum or fma 2^(max + 1), rounding being monotone).  So a
+// non-zero denominator with grain >= -126 and mag <= 126 is a normal number whose reciprocal is
+// normal, and the kernel's 1/den needs no class check (rcp_scan_fast).
+constexpr int kNoGrain = -100000;
+constexpr int kNoMag = 100000;
+constexpr int kDirGrain = -63;             // dir_grain_ok's bound 2^-40, 23 fraction bits
+constexpr int kDirMag = 4, kOrgMag = 41;   // ray_in_range's |d|_1 <= 16, |o|_1 <= 2^41
 struct Val {
     enum Kind { kZero, kVar, kLit } kind = kZero;
     std::string name;       // kVar: the variable holding the magnitude
     float lit = 0.0f;       // kLit: the magnitude (> 0)
     bool neg = false;
     std::string key = "0";  // the magnitude's expression
+    int grain = kNoGrain;
+    int mag = kNoMag;
 };
+int mag_mul(int a, int b) { return (a == kNoMag || b == kNoMag) ? kNoMag : a + b; }
+int mag_sum(int a, int b) { return (a == kNoMag || b == kNoMag) ? kNoMag : std::max(a, b) + 1; }
+
+int grain_of(float x)       // the exponent of x's lowest set bit (x finite, non-zero)
+{
+    int e = 0;
+    const float m = std::frexp(std::fabs(x), &e);    // x = m 2^e, m in [0.5, 1)
+    uint32_t s = (uint32_t)std::ldexp(m, 24);        // exact for normal x
+    if (s == 0) return kNoGrain;
+    int g = e - 24;
+    while ((s & 1u) == 0) { s >>= 1; g += 1; }
+    return g < -149 ? kNoGrain : g;
+}
+int grain_mul(int a, int b) { return (a == kNoGrain || b == kNoGrain || a + b < -149) ? kNoGrain : a + b; }
+int grain_min(int a, int b) { return (a == kNoGrain || b == kNoGrain) ? kNoGrain : std::min(a, b); }
 
 std::string lit_text(float x)
 {
@@ -120,7 +153,16 @@ std::string lit_text(float x)
 }
 
 Val zero() { return Val{}; }
-Val var(const std::string &n) { Val v; v.kind = Val::kVar; v.name = n; v.key = n; return v; }
+Val var(const std::string &n, int grain = kNoGrain, int mag = kNoMag)
+{
+    Val v;
+    v.kind = Val::kVar;
+    v.name = n;
+    v.key = n;
+    v.grain = grain;
+    v.mag = mag;
+    return v;
+}
 Val lit_or_zero(float x)
 {
     if (x == 0.0f) return zero();          // +0 and -0: dropped terms (see the header)
@@ -129,6 +171,10 @@ Val lit_or_zero(float x)
     v.lit = std::fabs(x);
     v.neg = std::signbit(x);
     v.key = lit_text(v.lit);
+    v.grain = grain_of(x);
+    int e = 0;
+    (void)std::frexp(v.lit, &e);           // |x| < 2^e
+    v.mag = e;
     return v;
 }
 Val negate(Val v)
@@ -156,12 +202,14 @@ struct Gen {
         if (v.kind == Val::kLit) return lit_text(v.neg ? -v.lit : v.lit);
         return v.neg ? "(-" + v.name + ")" : v.name;
     }
-    Val tmp(const std::string &expr, const std::string &key)
+    // (the grain is a function of the key, so a value found in `seen` has the one given here)
+    Val tmp(const std::string &expr, const std::string &key, int grain = kNoGrain,
+            int mag = kNoMag)
     {
         if (seen) {
             const auto it = seen->find(key);
             if (it != seen->end()) {
-                Val v = var(it->second);
+                Val v = var(it->second, grain, mag);
                 v.key = key;
                 return v;
             }
@@ -169,7 +217,7 @@ struct Gen {
         const std::string name = prefix + "r" + std::to_string(n++);
         out += "    const float " + name + " = " + expr + ";\n";
         if (seen) (*seen)[key] = name;
-        Val v = var(name);
+        Val v = var(name, grain, mag);
         v.key = key;
         return v;
     }
@@ -179,7 +227,8 @@ struct Gen {
         if (a.kind == Val::kZero || b.kind == Val::kZero) return zero();
         const bool swap = b.key < a.key;
         const Val &x = swap ? b : a, &y = swap ? a : b;
-        Val r = tmp(text(magnitude(x)) + " * " + text(magnitude(y)), "m(" + x.key + "," + y.key + ")");
+        Val r = tmp(text(magnitude(x)) + " * " + text(magnitude(y)), "m(" + x.key + "," + y.key + ")",
+                    grain_mul(a.grain, b.grain), mag_mul(a.mag, b.mag));
         r.neg = a.neg != b.neg;
         return r;
     }
@@ -195,14 +244,17 @@ struct Gen {
         const Val &x = swap ? b : a, &y = swap ? a : b;
         Val r = tmp("__builtin_fmaf(" + text(magnitude(x)) + ", " + text(magnitude(y)) + ", " +
                         text(cc) + ")",
-                    "f(" + x.key + "," + y.key + "," + signed_key(cc) + ")");
+                    "f(" + x.key + "," + y.key + "," + signed_key(cc) + ")",
+                    grain_min(grain_mul(a.grain, b.grain), c.grain),
+                    mag_sum(mag_mul(a.mag, b.mag), c.mag));
         r.neg = sp;
         return r;
     }
     Val sub(const Val &a, const Val &b)       // a - b; x - (+-0) == x exactly, so b = 0 drops
     {
         if (b.kind == Val::kZero) return a;
-        return tmp(text(a) + " - " + text(b), "s(" + signed_key(a) + "," + signed_key(b) + ")");
+        return tmp(text(a) + " - " + text(b), "s(" + signed_key(a) + "," + signed_key(b) + ")",
+                   grain_min(a.grain, b.grain), mag_sum(a.mag, b.mag));
     }
     // dot = fma(z, z', fma(y, y', x*x')), cross_i = fma(a_j, b_k, -(a_k*b_j)): DESIGN.md §3.1
     Val dot(const Val *a, const Val *b) { return fma(a[2], b[2], fma(a[1], b[1], mul(a[0], b[0]))); }
@@ -235,8 +287,10 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     g.seen = &seen;
     g.prefix = "t" + std::to_string(index) + r + "_";
     const std::string R(r);
-    Val o[3] = {var("o" + R + ".x"), var("o" + R + ".y"), var("o" + R + ".z")};
-    Val d[3] = {var("d" + R + ".x"), var("d" + R + ".y"), var("d" + R + ".z")};
+    Val o[3] = {var("o" + R + ".x", kNoGrain, kOrgMag), var("o" + R + ".y", kNoGrain, kOrgMag),
+                var("o" + R + ".z", kNoGrain, kOrgMag)};
+    Val d[3] = {var("d" + R + ".x", kDirGrain, kDirMag), var("d" + R + ".y", kDirGrain, kDirMag),
+                var("d" + R + ".z", kDirGrain, kDirMag)};
     Val v0[3], e1[3], e2[3];
     for (int k = 0; k < 3; k++) {
         v0[k] = lit_or_zero(T.v0[k]);
@@ -256,8 +310,11 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     const Val n2 = g.dot(s2, d);
     const Val tt = g.dot(s2, e2);
     // the reciprocal of the signed denominator (its sign stays inside: v_rcp's symmetry is
-    // not relied on)
-    const Val f = g.tmp("RVCP_SPEC_RCP(" + g.text(den) + ")", "r(" + signed_key(den) + ")");   // :254
+    // not relied on); without the class check when the denominator is zero or a normal number
+    // whose reciprocal is normal (grain >= -126, mag <= 126: see Val)
+    const char *rcp = den.grain != kNoGrain && den.grain >= -126 && den.mag <= 126
+                          ? "RVCP_SPEC_RCP_FAST(" : "RVCP_SPEC_RCP(";
+    const Val f = g.tmp(rcp + g.text(den) + ")", "r(" + signed_key(den) + ")");   // :254
     // t = f * dot(s2, e2) (:255); a vanished dot leaves t = +-0 or NaN, rejected by
     // t >= t_min > 0 in both forms
     const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.text(g.mul(f, tt));

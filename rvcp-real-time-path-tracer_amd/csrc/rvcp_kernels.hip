@@ -276,6 +276,17 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
 // the generic loop when a live ray was flagged is bit-exact too but measured 1.9x slower --
 // DESIGN.md §4.7.)
 #define RVCP_SPEC_RCP(den) rcp_scan(den)
+// rcp_scan without the class check and its branch, where the generator has proved (rvcp_jit.cpp
+// `grain`) that the denominator is +-0 or in [2^-126, 2^126] in magnitude for every ray the
+// wave admits (ray_in_range with dir_grain_ok): the reciprocal of such a number is normal, and
+// v_rcp + one Newton step equals the IEEE quotient wherever its result is normal (all 2^32
+// inputs, tools/rcp_check2.hip); a zero denominator gives NaN (rcp 0 = inf, fma(-0, inf, 1) =
+// NaN), which rejects, as rcp_scan's kept fast result does.
+__device__ __forceinline__ float rcp_scan_fast(float den) {
+    const float r = __builtin_amdgcn_rcpf(den);
+    return __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+}
+#define RVCP_SPEC_RCP_FAST(den) rcp_scan_fast(den)
 #include RVCP_SPEC_SCAN
 // The specialised scan drops products with exact-zero triangle components.  That is exact
 // when no intermediate of the generic test overflows (inf * 0 = NaN rejects there, while the
@@ -284,9 +295,18 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
 // every ray has |o|_1 <= 2^41 and |d|_1 <= 16.  Then |s| < 2^42, |s1| <= 2^46, |s2| <= 2^84,
 // |den|, |n1| < 2^90, |n2| < 2^91 and |s2.e2| < 2^127: all finite.  A NaN or infinite component
 // fails the compares, so non-finite rays take the generic loop too.  
+// dir_grain_ok: every direction component is +-0 or at least 2^-40 in magnitude -- the premise
+// of the generator's RVCP_SPEC_RCP_FAST reciprocals (rvcp_jit.cpp `kDirGrain`).  (bits << 1) - 1
+// maps +-0 to 0xFFFFFFFF and orders the other magnitudes.
+__device__ __forceinline__ bool dir_grain_ok(f3 d) {
+    const uint32_t x = (__float_as_uint(d.x) << 1) - 1u, y = (__float_as_uint(d.y) << 1) - 1u,
+                   z = (__float_as_uint(d.z) << 1) - 1u;
+    return min(min(x, y), z) >= (0x2B800000u << 1) - 1u;                     // 2^-40
+}
 __device__ __forceinline__ bool ray_in_range(f3 o, f3 d) {
     return (((__builtin_fabsf(o.x) + __builtin_fabsf(o.y)) + __builtin_fabsf(o.z)) <= 0x1p41f) &
-           (((__builtin_fabsf(d.x) + __builtin_fabsf(d.y)) + __builtin_fabsf(d.z)) <= 16.0f);
+           (((__builtin_fabsf(d.x) + __builtin_fabsf(d.y)) + __builtin_fabsf(d.z)) <= 16.0f) &
+           dir_grain_ok(d);
 }
 #endif
 // A necessary condition for tri_stage2 to accept, from stage 1 alone: |n1| and |n2| at most

@@ -31,6 +31,27 @@ PRELUDE = r"""
 struct f3 { float x, y, z; };
 static inline float RVCP_F32(uint32_t b) { float f; std::memcpy(&f, &b, 4); return f; }
 #define RVCP_SPEC_RCP(d) (1.0f / (d))
+// RVCP_SPEC_RCP_FAST: the kernel's reciprocal without the class check, which equals the IEEE
+// quotient for +-0 (rejected either way) and for |den| in [2^-126, 2^126] (tools/rcp_check2.hip);
+// the generator emits it only where that holds for every ray passing dir_grain_ok -- counted
+// here: a denominator outside that set while the current rays pass the guard is a violation
+static long g_fast_calls = 0, g_fast_bad = 0;
+static bool g_grain_ok = true;
+static inline float rcp_fast_check(float d) {
+    if (g_grain_ok) {
+        g_fast_calls++;
+        const float a = std::fabs(d);
+        if (!(d == 0.0f || (a >= 0x1p-126f && a <= 0x1p126f))) g_fast_bad++;
+    }
+    return 1.0f / d;
+}
+#define RVCP_SPEC_RCP_FAST(d) rcp_fast_check(d)
+static inline bool dir_grain_ok(f3 d) {       // the kernel's guard (rvcp_kernels.hip)
+    const float c[3] = {d.x, d.y, d.z};
+    for (float x : c)
+        if (x != 0.0f && !(std::fabs(x) >= 0x1p-40f)) return false;
+    return true;
+}
 #define RVCP_SPEC_COMMIT(t, i) ((void)0)
 #define RVCP_SPEC_COMMIT1(t) ((void)0)
 """
@@ -40,6 +61,7 @@ extern "C" void scan_all(const float *rays, int n, float tmin, float tmax, float
     for (int r = 0; r < n; r++) {
         const float *q = rays + 6 * r;
         f3 o{q[0], q[1], q[2]}, d{q[3], q[4], q[5]};
+        g_grain_ok = dir_grain_ok(d);
         float bt = tmax; int best = -1;
         if (dual) {
             // the two-ray form: the ray in slot B (nearest t and face), a different ray in
@@ -59,6 +81,8 @@ extern "C" void scan_all(const float *rays, int n, float tmin, float tmax, float
         bt_out[r] = bt; best_out[r] = best;
     }
 }
+extern "C" long fast_rcp_calls() { return g_fast_calls; }
+extern "C" long fast_rcp_violations() { return g_fast_bad; }
 """
 
 
@@ -92,6 +116,8 @@ def _build(tmp_path, rec, name):
     lib = ctypes.CDLL(str(so))
     lib.scan_all.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_float,
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    lib.fast_rcp_calls.restype = ctypes.c_long
+    lib.fast_rcp_violations.restype = ctypes.c_long
     return lib
 
 
@@ -121,6 +147,7 @@ def _check(lib, positions, rays, tmin=0.01, tmax=10000.0):
     best2 = np.zeros(n, np.int32)
     lib.scan_all(rays.ctypes.data, n, tmin, tmax, bt2.ctypes.data, best2.ctypes.data, 1)
     assert np.array_equal(best2, best) and np.array_equal(bt2.view(np.uint32), bt.view(np.uint32))
+    assert lib.fast_rcp_violations() == 0
     return hits
 
 
@@ -185,9 +212,45 @@ def test_generated_scan_cornell_bitexact(tmp_path):
     # with no zero component (-28 %)
     dense = _scan_source(_tri_records(np.random.default_rng(0).uniform(-5, 5, pos.shape)))
     assert src.count("const float ") < 0.75 * dense.count("const float ")
+    # every reciprocal of the Cornell scans skips the class check
+    assert "RVCP_SPEC_RCP(" not in src and src.count("RVCP_SPEC_RCP_FAST(") > 0
     lib = _build(tmp_path, rec, "cornell")
     hits = _check(lib, pos, _adversarial_rays(pos, np.random.default_rng(1), 2500))
     assert hits > 1500
+    assert lib.fast_rcp_calls() > 0
+    _check(lib, pos, _grain_edge_rays(pos, np.random.default_rng(7), 600))
+
+
+def _grain_edge_rays(positions, rng, n):
+    """Rays whose direction components sit at dir_grain_ok's bound: 0, +-2^-40 and a few ulps
+    above it, the rest random (the smallest denominators the fast reciprocal may meet)."""
+    lo, hi = positions.reshape(-1, 3).min(0), positions.reshape(-1, 3).max(0)
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = _norm(rng.normal(size=(n, 3)))
+    tiny = np.float32(2.0 ** -40) * (1 + rng.integers(0, 4, (n, 3)) * np.float32(2.0 ** -23))
+    pick = rng.random((n, 3)) < 0.4
+    d = np.where(pick, tiny * rng.choice([-1, 1], (n, 3)), d).astype(np.float32)
+    d[rng.random((n, 3)) < 0.2] = 0.0
+    d[(d == 0).all(1), 0] = 1.0
+    return np.concatenate([o, d], axis=1)
+
+
+def test_fast_reciprocal_grain_rule(tmp_path):
+    """The generator emits the class-check-free reciprocal only where its grain bound proves the
+    denominator zero or normal for every ray dir_grain_ok admits: triangles at unit scale get it,
+    triangles at 2^-10 scale (denominators down to 2^-129) do not; the premise holds on rays at
+    the guard's bound and the scan stays bit-exact vs the oracle."""
+    rng = np.random.default_rng(11)
+    unit = rng.uniform(-5, 5, (6, 3, 3)).astype(np.float32)
+    unit[:, :, 1] = np.float32(1.25)                   # horizontal: a zero denominator term
+    small = (rng.uniform(-5, 5, (6, 3, 3)) * 2.0 ** -10).astype(np.float32)
+    pos = np.concatenate([unit, small])
+    src = _scan_source(_tri_records(pos))
+    assert src.count("RVCP_SPEC_RCP_FAST(") > 0 and src.count("RVCP_SPEC_RCP(") > 0
+    lib = _build(tmp_path, _tri_records(pos), "grain")
+    _check(lib, pos, _grain_edge_rays(pos, rng, 800))
+    _check(lib, pos, _adversarial_rays(pos, rng, 400))
+    assert lib.fast_rcp_calls() > 0
 
 
 def test_generated_scan_sparse_random_bitexact(tmp_path):
