@@ -78,6 +78,7 @@ struct rvcp_ctx {
     unsigned long long *d_counters = nullptr;
     uint32_t n_faces = 0, n_lights = 0, n_mats = 0, n_verts = 0, n_spheres = 0;
     bool lights_same = false;      // every light record samples the same face
+    bool rcp_fast = false;         // scan_rcp_fast_scene (FrameArgs::rcp_fast)
     // scene-specialised path kernels (rvcp_jit.cpp), or null: generic kernels
     std::shared_ptr<JitKernels> jit;
     std::string jit_err;
@@ -601,6 +602,7 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
                                     n_spheres == 0, n_spheres <= 64 && n_materials <= 64);
         HIP_TRY(ctx, hipSetDevice(ctx->device));
     }
+    ctx->rcp_fast = scan_rcp_fast_scene(tri.data(), n_faces);
     ctx->n_faces = n_faces;
     ctx->n_verts = n_vertices;
     ctx->n_mats = n_materials;
@@ -685,6 +687,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     A.n_faces = ctx->n_faces;
     A.n_lights = ctx->n_lights;
     A.lights_same = ctx->lights_same ? 1u : 0u;
+    A.rcp_fast = ctx->rcp_fast ? 1u : 0u;
     A.light_total = ctx->light_total;
     A.light_pdf = ctx->light_pdf;
     {   // :465-471: denom = max(0.1, pdf) * rr, pdf = 0.5 / 3.1415926 (cos > 0) or 0; IEEE 1/denom

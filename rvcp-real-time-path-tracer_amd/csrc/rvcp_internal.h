@@ -207,6 +207,9 @@ struct FrameArgs {
     // every light record samples the same face (the std140 id quirk on the Cornell box maps
     // both entries to face 0): nee_sample's pick cannot change the sample, so it reads record 0
     uint32_t lights_same;
+    // every triangle's scan denominator is +-0 or within [2^-126, 2^126] for rays passing
+    // dir_fast_ok (scan_rcp_fast_scene): the generic scans may take 1/den without the class check
+    uint32_t rcp_fast;
     uint32_t static_chunks;  // pixels handed out statically (one chunk per wave)
     uint32_t static_chunk;   // pixels of each wave's static chunk (<= kChunk)
     uint32_t n_simds;        // SIMDs of the device (CUs x 4), for static_split

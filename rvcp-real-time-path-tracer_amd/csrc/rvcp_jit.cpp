@@ -374,6 +374,33 @@ void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *c
 
 }  // namespace
 
+bool scan_rcp_fast_scene(const TriRecord *tri, uint32_t n)
+{
+    // the generic test's den = dot(cross(d, e2), e1) equals the zero-dropped expression's value
+    // (a product with a zero factor is an exact zero, an fma with one adds nothing) as long as
+    // nothing overflows, so its grain and magnitude bounds (Val) hold for it: ask that s1 and den
+    // stay within 2^126 (no overflow, so no inf x 0 either) and that a non-zero den is at least
+    // 2^-126, for every ray passing dir_fast_ok
+    for (uint32_t i = 0; i < n; i++) {
+        Gen g;
+        Val d[3] = {var("d.x", kDirGrain, kDirMag), var("d.y", kDirGrain, kDirMag),
+                    var("d.z", kDirGrain, kDirMag)};
+        Val e1[3], e2[3], s1[3];
+        for (int k = 0; k < 3; k++) {
+            if (!std::isfinite(tri[i].e1[k]) || !std::isfinite(tri[i].e2[k])) return false;
+            e1[k] = lit_or_zero(tri[i].e1[k]);
+            e2[k] = lit_or_zero(tri[i].e2[k]);
+        }
+        g.cross(d, e2, s1);
+        for (int k = 0; k < 3; k++)
+            if (s1[k].kind != Val::kZero && s1[k].mag > 126) return false;
+        const Val den = g.dot(s1, e1);
+        if (den.kind == Val::kZero) continue;             // identically zero: f = NaN, rejected
+        if (den.grain == kNoGrain || den.grain < -126 || den.mag > 126) return false;
+    }
+    return true;
+}
+
 bool jit_scene_in_range(const TriRecord *tri, uint32_t n)
 {
     // the premise of the zero-dropping (header): with |v0| <= 2^40, |e1|, |e2| <= 2^41 and the
@@ -582,6 +609,13 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
 }
 
 }  // namespace rvcp
+
+// Self-test hook: may the generic scans of a scene with these n triangle records take 1/den
+// without the class check (scan_rcp_fast_scene; 1 / 0)?
+extern "C" int rvcp_internal_scan_rcp_fast_scene(const void *tri_records, uint32_t n)
+{
+    return rvcp::scan_rcp_fast_scene(static_cast<const rvcp::TriRecord *>(tri_records), n) ? 1 : 0;
+}
 
 // Self-test hook: would upload specialise a scene with these n triangle records (1 / 0)?
 extern "C" int rvcp_internal_jit_scene_in_range(const void *tri_records, uint32_t n)

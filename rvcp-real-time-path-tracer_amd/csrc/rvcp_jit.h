@@ -25,6 +25,11 @@ struct JitKernels {
 // Every |v0| <= 2^40 and |e1|, |e2| <= 2^41 (finite): the range in which dropping the products
 // with exact-zero components cannot turn the generic test's inf * 0 = NaN into a finite value.
 bool jit_scene_in_range(const TriRecord *tri, uint32_t n);
+// Every triangle's denominator, for any ray direction passing the kernel's dir_fast_ok (each
+// component +-0 or at least 2^-40, |d|_1 <= 16), is +-0 or within [2^-126, 2^126] in magnitude
+// with no overflow on the way: the generic scan may then take 1/den without the class check
+// (FrameArgs::rcp_fast).
+bool scan_rcp_fast_scene(const TriRecord *tri, uint32_t n);
 // Extra hipRTC options (debug build only; empty in the product library).
 std::vector<std::string> jit_extra_flags();
 // The generated scan (spec_scan1 / spec_scan2) for n triangle records.

@@ -249,18 +249,45 @@ __device__ __forceinline__ TriPart tri_stage1(const TriRecord &T, f3 o, f3 d) {
 }
 // Stage 2: f = 1/den, t = f (s2.e2), b1 = f n1, b2 = f n2 (:254-257); accept iff the shader
 // would replace the current nearest hit whose time is `bt`.  5-compare form, DESIGN.md §3.5.
+// FAST: 1/den without the class check (rcp_scan_fast) -- the scene passed scan_rcp_fast_scene
+// and the ray dir_fast_ok (FrameArgs::rcp_fast).
+__device__ __forceinline__ float rcp_scan_fast(float den);
+template <bool FAST = false>
 __device__ __forceinline__ bool tri_stage2(const TriRecord &T, const TriPart &P, float tmin,
                                            float bt, float &t_out) {
-    const float f = rcp_scan(P.den);
+    const float f = FAST ? rcp_scan_fast(P.den) : rcp_scan(P.den);
     const float t = f * dot(P.s2, ld3(T.e2));
     const float b1 = f * P.n1;
     const float b2 = f * P.n2;
     t_out = t;
     return (b1 >= 0.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f) & (t >= tmin) & (t <= bt);
 }
+template <bool FAST = false>
 __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float tmin, float bt,
                                            float &t_out) {
-    return tri_stage2(T, tri_stage1(T, o, d), tmin, bt, t_out);
+    return tri_stage2<FAST>(T, tri_stage1(T, o, d), tmin, bt, t_out);
+}
+// v_rcp + one Newton step, no class check: equals the IEEE quotient wherever its result is
+// normal (all 2^32 inputs, tools/rcp_check2.hip), i.e. for |den| in [2^-126, 2^126]; a zero
+// denominator gives NaN (rcp 0 = inf, fma(-0, inf, 1) = NaN), which rejects, as rcp_scan's kept
+// fast result does.  Used where the denominator is proved +-0 or within that range for every
+// ray the wave admits: the specialised scan's RVCP_SPEC_RCP_FAST (rvcp_jit.cpp `grain`) and the
+// generic scan of a scene that passed scan_rcp_fast_scene (FrameArgs::rcp_fast).
+__device__ __forceinline__ float rcp_scan_fast(float den) {
+    const float r = __builtin_amdgcn_rcpf(den);
+    return __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+}
+// dir_fast_ok: every direction component is +-0 or at least 2^-40 in magnitude (dir_grain_ok)
+// and |d|_1 <= 16 -- the ray side of both proofs (rvcp_jit.cpp `kDirGrain`, `kDirMag`).
+// (bits << 1) - 1 maps +-0 to 0xFFFFFFFF and orders the other magnitudes.
+__device__ __forceinline__ bool dir_grain_ok(f3 d) {
+    const uint32_t x = (__float_as_uint(d.x) << 1) - 1u, y = (__float_as_uint(d.y) << 1) - 1u,
+                   z = (__float_as_uint(d.z) << 1) - 1u;
+    return min(min(x, y), z) >= (0x2B800000u << 1) - 1u;                     // 2^-40
+}
+__device__ __forceinline__ bool dir_fast_ok(f3 d) {
+    return (((__builtin_fabsf(d.x) + __builtin_fabsf(d.y)) + __builtin_fabsf(d.z)) <= 16.0f) &
+           dir_grain_ok(d);
 }
 #ifdef RVCP_SPEC_SCAN        // the scene-specialised scan generated by rvcp_jit.cpp (§4.7)
 #define RVCP_F32(bits) __uint_as_float(bits)
@@ -278,14 +305,7 @@ __device__ __forceinline__ bool tri_accept(const TriRecord &T, f3 o, f3 d, float
 #define RVCP_SPEC_RCP(den) rcp_scan(den)
 // rcp_scan without the class check and its branch, where the generator has proved (rvcp_jit.cpp
 // `grain`) that the denominator is +-0 or in [2^-126, 2^126] in magnitude for every ray the
-// wave admits (ray_in_range with dir_grain_ok): the reciprocal of such a number is normal, and
-// v_rcp + one Newton step equals the IEEE quotient wherever its result is normal (all 2^32
-// inputs, tools/rcp_check2.hip); a zero denominator gives NaN (rcp 0 = inf, fma(-0, inf, 1) =
-// NaN), which rejects, as rcp_scan's kept fast result does.
-__device__ __forceinline__ float rcp_scan_fast(float den) {
-    const float r = __builtin_amdgcn_rcpf(den);
-    return __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
-}
+// wave admits (ray_in_range with dir_grain_ok)
 #define RVCP_SPEC_RCP_FAST(den) rcp_scan_fast(den)
 #include RVCP_SPEC_SCAN
 // The specialised scan drops products with exact-zero triangle components.  That is exact
@@ -295,14 +315,7 @@ __device__ __forceinline__ float rcp_scan_fast(float den) {
 // every ray has |o|_1 <= 2^41 and |d|_1 <= 16.  Then |s| < 2^42, |s1| <= 2^46, |s2| <= 2^84,
 // |den|, |n1| < 2^90, |n2| < 2^91 and |s2.e2| < 2^127: all finite.  A NaN or infinite component
 // fails the compares, so non-finite rays take the generic loop too.  
-// dir_grain_ok: every direction component is +-0 or at least 2^-40 in magnitude -- the premise
-// of the generator's RVCP_SPEC_RCP_FAST reciprocals (rvcp_jit.cpp `kDirGrain`).  (bits << 1) - 1
-// maps +-0 to 0xFFFFFFFF and orders the other magnitudes.
-__device__ __forceinline__ bool dir_grain_ok(f3 d) {
-    const uint32_t x = (__float_as_uint(d.x) << 1) - 1u, y = (__float_as_uint(d.y) << 1) - 1u,
-                   z = (__float_as_uint(d.z) << 1) - 1u;
-    return min(min(x, y), z) >= (0x2B800000u << 1) - 1u;                     // 2^-40
-}
+// (dir_grain_ok: the premise of the generator's RVCP_SPEC_RCP_FAST reciprocals)
 __device__ __forceinline__ bool ray_in_range(f3 o, f3 d) {
     return (((__builtin_fabsf(o.x) + __builtin_fabsf(o.y)) + __builtin_fabsf(o.z)) <= 0x1p41f) &
            (((__builtin_fabsf(d.x) + __builtin_fabsf(d.y)) + __builtin_fabsf(d.z)) <= 16.0f) &
@@ -1486,6 +1499,34 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
 // The BVH path kernel traces one ray per lane per iteration (the variant-5 form): C5 297 ->
 // 283 ms over the dual form, whose second traversal leaves the lanes without a path ray idle.
 constexpr int kTiledMinWaves = 4;
+// The generic nearest-hit scans of the non-tiled path kernels: every triangle in index order
+// (wave-uniform face index, the records in SGPRs), one ray (scan_generic1) or the lane's two
+// (scan_generic2; slot A keeps its face only for SINGLE); FAST as tri_stage2.
+template <bool FAST>
+__device__ __forceinline__ void scan_generic1(const TriRecord *__restrict__ tri, uint32_t n, f3 o,
+                                              f3 d, float tmin, float &bt, int &best) {
+#pragma unroll 1
+    for (uint32_t i = 0; i < n; ++i) {
+        const TriRecord T = tri[i];
+        float t;
+        if (tri_accept<FAST>(T, o, d, tmin, bt, t)) { bt = t; best = (int)i; }
+    }
+}
+template <bool FAST, bool SINGLE>
+__device__ __forceinline__ void scan_generic2(const TriRecord *__restrict__ tri, uint32_t n,
+                                              f3 a_o, f3 a_d, f3 b_o, f3 b_d, float tmin,
+                                              float &btA, int &bestA, float &btB, int &bestB) {
+#pragma unroll 1
+    for (uint32_t i = 0; i < n; ++i) {
+        const TriRecord T = tri[i];
+        float tA, tB;
+        if (tri_accept<FAST>(T, a_o, a_d, tmin, btA, tA)) {
+            btA = tA;
+            if (SINGLE) bestA = (int)i;
+        }
+        if (tri_accept<FAST>(T, b_o, b_d, tmin, btB, tB)) { btB = tB; bestB = (int)i; }
+    }
+}
 // The tiled scans issue the first pretest halves of two triangles together (ILP for the
 // latency-bound per-triangle chain; C5 -5 %); the one-slot schedule 5 too (3
 // and 4 triangles per step measured equal to 2).
@@ -1971,9 +2012,16 @@ __device__ __forceinline__ void path_body(
             float bt = A.t_max;
             int best = -1;
             if (worker) {
-                for (uint32_t i = part; i < A.n_faces; i += R) {
-                    float t;
-                    if (tri_accept(tri[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
+                if (A.rcp_fast && !__any(worker && !dir_fast_ok(d))) {
+                    for (uint32_t i = part; i < A.n_faces; i += R) {
+                        float t;
+                        if (tri_accept<true>(tri[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
+                    }
+                } else {
+                    for (uint32_t i = part; i < A.n_faces; i += R) {
+                        float t;
+                        if (tri_accept(tri[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
+                    }
                 }
             }
             for (uint32_t off = R >> 1; off >= 1; off >>= 1) {
@@ -2021,14 +2069,10 @@ __device__ __forceinline__ void path_body(
                 spec_scan1(o, d, A.t_min, bt, best);
             } else
 #endif
-            {
-#pragma unroll 1
-            for (uint32_t i = 0; i < A.n_faces; ++i) {
-                const TriRecord T = tri[i];
-                float t;
-                if (tri_accept(T, o, d, A.t_min, bt, t)) { bt = t; best = (int)i; }
-            }
-            }
+            if (A.rcp_fast && !__any(lane_r < nr && !dir_fast_ok(d)))
+                scan_generic1<true>(tri, A.n_faces, o, d, A.t_min, bt, best);
+            else
+                scan_generic1<false>(tri, A.n_faces, o, d, A.t_min, bt, best);
             // lanes >= nr traced stale rows; their results are never read
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -2060,16 +2104,10 @@ __device__ __forceinline__ void path_body(
 #endif
             {
             // the generic loop keeps no face index for the shadow ray either (as spec_scan2)
-#pragma unroll 1
-            for (uint32_t i = 0; i < A.n_faces; ++i) {
-                const TriRecord T = tri[i];
-                float tA, tB;
-                if (tri_accept(T, a_o, a_d, A.t_min, btA, tA)) {
-                    btA = tA;
-                    if (SINGLE) bestA = (int)i;
-                }
-                if (tri_accept(T, b_o, b_d, A.t_min, btB, tB)) { btB = tB; bestB = (int)i; }
-            }
+            if (A.rcp_fast && !__any((hasA && !dir_fast_ok(a_d)) || (hasB && !dir_fast_ok(b_d))))
+                scan_generic2<true, SINGLE>(tri, A.n_faces, a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
+            else
+                scan_generic2<false, SINGLE>(tri, A.n_faces, a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
             }
             if (!SINGLE) {
                 // The shadow ray's nearest face is not needed, only whether it hit (resolve A):
@@ -2328,7 +2366,11 @@ __device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d
     // below (!(delta < 0) fails, or NaN roots fail the compares), so the wave skips the
     // square root, the roots and the compares
     if (!__any(delta >= 0.0f)) { t_out = bt; return false; }
-    const float sq = sqrt_c(delta);
+    // the root matters only where delta >= 0: a lane with delta < 0 (or NaN) rejects the sphere
+    // whatever sq is (NaN from either form), so only delta >= 0 outside sqrt_fast_ok's range
+    // takes the IEEE sequence -- not every wave in which some lane misses the sphere
+    float sq = sqrt_fast_core(delta);
+    if (__builtin_expect((delta >= 0.0f) & !sqrt_fast_ok(delta), 0)) sq = __builtin_sqrtf(delta);
     float t0 = FAST ? quot_markstein(-b + sq, two_a, y) : (-b + sq) / two_a;
     float t1 = FAST ? quot_markstein(-b - sq, two_a, y) : (-b - sq) / two_a;
     if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
@@ -2498,6 +2540,7 @@ __device__ __forceinline__ void legacy_body(
 #ifdef RVCP_SPEC_SCAN
         const bool spec = __all(st != L_TRACE || (ray_in_range(ro, rd) && rtmin > 0.0f));
 #endif
+        const bool rfast = A.rcp_fast && __all(st != L_TRACE || dir_fast_ok(rd));
         if (st == L_TRACE) {
             trav += 1;
             if (fast) {
@@ -2520,7 +2563,13 @@ __device__ __forceinline__ void legacy_body(
                 if (bf >= 0) best = (int)A.n_spheres + bf;
             } else
 #endif
-            {
+            if (rfast) {
+#pragma unroll 2
+            for (uint32_t i = 0; i < A.n_faces; ++i) {
+                float t;
+                if (tri_accept<true>(tri[i], ro, rd, rtmin, bt, t)) { bt = t; best = (int)(A.n_spheres + i); }
+            }
+            } else {
 #pragma unroll 2
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 float t;

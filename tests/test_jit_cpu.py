@@ -352,3 +352,66 @@ def test_specialisation_range_guard(tmp_path):
     with np.errstate(over="ignore", invalid="ignore"):
         s2 = np.cross(sv, T["e1"]).astype(np.float32)
     assert not np.isfinite(s2).all()
+
+
+DEN_SRC = r"""
+#include <cmath>
+// the generic test's denominator, dot(cross(d, e2), e1) with the fused builtins of DESIGN.md §3.1
+extern "C" long den_violations(const float *tri, int n, const float *dirs, int m) {
+    long bad = 0;
+    for (int i = 0; i < n; i++) {
+        const float *e1 = tri + 12 * i + 3, *e2 = tri + 12 * i + 6;
+        for (int j = 0; j < m; j++) {
+            const float *d = dirs + 3 * j;
+            const float s1x = std::fma(d[1], e2[2], -(d[2] * e2[1]));
+            const float s1y = std::fma(d[2], e2[0], -(d[0] * e2[2]));
+            const float s1z = std::fma(d[0], e2[1], -(d[1] * e2[0]));
+            const float den = std::fma(s1z, e1[2], std::fma(s1y, e1[1], s1x * e1[0]));
+            const float a = std::fabs(den);
+            if (!(den == 0.0f || (a >= 0x1p-126f && a <= 0x1p126f))) bad++;
+        }
+    }
+    return bad;
+}
+"""
+
+
+def _rcp_fast_scene(rec):
+    L = rvcp_amd.abi.load()
+    fn = L.rvcp_internal_scan_rcp_fast_scene
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    return bool(fn(rec.ctypes.data, len(rec)))
+
+
+def test_generic_scan_fast_reciprocal_scene_rule(tmp_path):
+    """FrameArgs::rcp_fast (scan_rcp_fast_scene): the generic scans drop the reciprocal's class
+    check only for scenes whose every denominator is +-0 or within [2^-126, 2^126] for all
+    directions passing dir_fast_ok.  The Cornell box, its rotated copy and unit-scale random
+    meshes pass; 2^-40-scale and 1e30-scale triangles and non-finite edges do not; on the scenes
+    that pass, the denominators of directions at the guard's bound stay in range (C, the fused
+    builtins)."""
+    src = tmp_path / "den.cpp"
+    src.write_text(DEN_SRC)
+    so = tmp_path / "den.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-mfma",
+                    "-fno-fast-math", "-o", str(so), str(src)], check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.den_violations.restype = ctypes.c_long
+    lib.den_violations.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    rng = np.random.default_rng(12)
+    cornell = _cornell_positions()
+    scenes_ok = [cornell, rng.uniform(-5, 5, (40, 3, 3)).astype(np.float32)]
+    rot = np.float32(np.linalg.qr(rng.normal(size=(3, 3)))[0])
+    scenes_ok.append((cornell @ rot).astype(np.float32))
+    for pos in scenes_ok:
+        rec = _tri_records(pos)
+        assert _rcp_fast_scene(rec)
+        d = _grain_edge_rays(pos, rng, 4000)[:, 3:].copy()
+        d = np.concatenate([d, _norm(rng.normal(size=(2000, 3)))]).astype(np.float32)
+        assert lib.den_violations(rec.ctypes.data, len(rec), d.ctypes.data, len(d)) == 0
+    assert not _rcp_fast_scene(_tri_records(cornell * np.float32(2.0 ** -40)))
+    assert not _rcp_fast_scene(_tri_records(cornell * np.float32(1e30)))
+    bad = cornell.copy()
+    bad[3, 1, 0] = np.inf
+    assert not _rcp_fast_scene(_tri_records(bad))

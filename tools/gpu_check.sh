@@ -105,6 +105,11 @@ for s in $STEPS; do
         abm2) run ab_m2 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload spheres --steps 60" "lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE::--workload spheres --steps 60" "lds5=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=5::--workload spheres --steps 60" "c3m2=RVCP_LIB=$DBG::--workload c3m2" "c3m2lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE::--workload c3m2" ;;
         abgrp) run ab_grp 900 python tools/ab.py --runner frames --passes 2 "prod=::--size 384 --spp 10 --frames 20" "g2=RVCP_LIB=tools/build/var_g2/librvcp.so::--size 384 --spp 10 --frames 20" "g4=RVCP_LIB=tools/build/var_g4/librvcp.so::--size 384 --spp 10 --frames 20" "prodc3=::--frames 10" "g2c3=RVCP_LIB=tools/build/var_g2/librvcp.so::--frames 10" "g4c3=RVCP_LIB=tools/build/var_g4/librvcp.so::--frames 10" ;;
         abc3) run ab_c3 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3" "new=::--workload c3" ;;
+        abc2lat) run ab_c2lat 900 python tools/ab.py --runner bench --field config.frame_latency_ms_alone --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c2 --steps 40 --launch-pass 40" "new=::--workload c2 --steps 40 --launch-pass 40" ;;
+        abm2new) run ab_m2new 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload spheres --steps 60" "new=::--workload spheres --steps 60" "c3m2base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
+        abgen2) run ab_gen2 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3gen" "gfast=RVCP_LIB=tools/build/var_gfast/librvcp.so::--workload c3gen" "new=::--workload c3gen" "c3gfast=RVCP_LIB=tools/build/var_gfast/librvcp.so::--workload c3" "c3new=::--workload c3" ;;
+        abm2sq) run ab_m2sq 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_pipe/librvcp.so::--workload spheres --steps 60" "new=::--workload spheres --steps 60" "c3m2base=RVCP_LIB=tools/build/var_pipe/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
+        legacy) run pytest_legacy 600 python -u -m pytest tests/test_gpu_legacy.py tests/test_gpu_specialize.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         pipeline) run pytest_pipeline 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_bench.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         benchrot) run bench_c3rot 300 python bench.py --workload c3rot --steps 30 --warmup 5 --no-cpu-baseline ;;
         benchgen) run bench_c3gen 300 python bench.py --workload c3gen --steps 30 --warmup 5 --no-cpu-baseline ;;
