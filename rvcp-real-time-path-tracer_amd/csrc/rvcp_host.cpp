@@ -826,7 +826,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                     (void)hipFree(ctx->d_timeline);
                     ctx->d_timeline = nullptr;
                     ctx->cap_timeline = 0;
-                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_timeline, waves * 48));
+                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_timeline, waves * 64));
                     ctx->cap_timeline = waves;
                 }
                 A.timeline = ctx->d_timeline;
@@ -963,7 +963,7 @@ static int impl_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         stats->wave_iterations = c[2];
     }
     if (ctx->last_timeline_waves) {
-        std::vector<unsigned long long> t(6 * ctx->last_timeline_waves);
+        std::vector<unsigned long long> t(8 * ctx->last_timeline_waves);
         HIP_TRY(ctx, hipMemcpy(t.data(), ctx->d_timeline, t.size() * 8, hipMemcpyDeviceToHost));
         const char *path = RVCP_KNOB("RVCP_DEBUG_TIMELINE");
         if (FILE *f = path ? std::fopen(path, "ab") : nullptr) {

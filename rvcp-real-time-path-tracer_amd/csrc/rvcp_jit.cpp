@@ -273,6 +273,9 @@ struct Gen {
 // second exactly when it held before the first (2 of the 5 compares of a quad's second test).
 struct RangeMask {
     std::string t, name;
+    // tests of this ray with this t whose acceptance is still to be applied (emit_scan's quad
+    // regions): their acceptance flags and face indices, in order
+    std::vector<std::pair<std::string, uint32_t>> pending;
 };
 
 // One triangle's test for ray `r` ("" / "A" / "B"), split into its arithmetic (`decl`: every
@@ -281,7 +284,8 @@ struct RangeMask {
 // acceptance (`accept`: the update); false when it can never accept.
 bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, uint32_t index,
                    const char *r, std::map<std::string, std::string> &seen,
-                   std::map<std::string, RangeMask> &prev)
+                   std::map<std::string, RangeMask> &prev, bool *reused = nullptr,
+                   bool defer = false)
 {
     Gen g;
     g.seen = &seen;
@@ -330,6 +334,7 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     else if (!b2.empty()) add("(" + b2 + " <= 1.0f)");
     decl += g.out;
     RangeMask &pm = prev[R];
+    if (reused) *reused = !pm.name.empty() && pm.t == t;
     if (pm.name.empty() || pm.t != t) {
         pm.t = t;
         pm.name = g.prefix + "q";
@@ -339,6 +344,30 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     // the dual scan's shadow ray (slot A) needs the nearest t and whether there was a hit, not
     // the face: only its t is kept (btA != t_max after the scan means a hit;
     // the caller resolves btA == t_max, a miss or a hit at exactly t_max, with the generic scan)
+    if (defer) {
+        // the next test of this ray has the same t: keep the flag, apply both together
+        const std::string c = g.prefix + "c";
+        accept += "        " + c + " = " + cond + ";\n";
+        decl += "    bool " + c + ";\n";
+        pm.pending.emplace_back(c, index);
+        return true;
+    }
+    if (!pm.pending.empty()) {
+        // the last test of a run with one t: bt takes t if any test of the run accepted, the
+        // face is the last accepting one (the order the sequential updates would leave)
+        const std::string c = g.prefix + "c";
+        std::string any = c, best = "best" + R;
+        for (const auto &pc : pm.pending) {
+            any += " | " + pc.first;
+            best = "(" + pc.first + " ? " + std::to_string(pc.second) + " : " + best + ")";
+        }
+        accept += "        const bool " + c + " = " + cond + ";\n";
+        accept += "        if (" + any + ") bt" + R + " = " + t + ";\n";
+        if (R != "A")
+            accept += "        best" + R + " = " + c + " ? " + std::to_string(index) + " : " + best + ";\n";
+        pm.pending.clear();
+        return true;
+    }
     if (R == "A")
         accept += "        if (" + cond + ") btA = " + t + ";\n";
     else
@@ -354,19 +383,41 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
 // measured within +-1 % and were removed: a range mask (RangeMask) must read
 // the nearest hit after the previous test's acceptance, which a group's shared prologue does
 // not.
+//
+// Except inside a quad (round 4): a test whose ray's next test reuses its range mask (the same
+// t, RangeMask) is not committed on its own -- the two tests of each ray and the other ray's
+// tests between them form one region, so the compiler can merge the two acceptances of a ray
+// (both write the same t) into one select of bt.
 void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *const *rays,
                int n_rays)
 {
+    const uint32_t N = n * (uint32_t)n_rays;
+    std::vector<char> used(N), reused(N);
+    {   // dry run: which tests are emitted and which reuse their ray's previous range mask
+        std::map<std::string, std::string> seen;
+        std::map<std::string, RangeMask> prev;
+        for (uint32_t u = 0; u < N; u++) {
+            std::string decl, accept;
+            bool ru = false;
+            used[u] = emit_triangle(decl, accept, tri[u / (uint32_t)n_rays], u / (uint32_t)n_rays,
+                                    rays[u % (uint32_t)n_rays], seen, prev, &ru);
+            reused[u] = used[u] && ru;
+        }
+    }
     std::map<std::string, std::string> seen;
     std::map<std::string, RangeMask> prev;
-    for (uint32_t u = 0; u < n * (uint32_t)n_rays; u++) {
+    for (uint32_t u = 0; u < N; u++) {
         std::string decl, accept;
         const std::string R(rays[u % (uint32_t)n_rays]);
-        const bool used = emit_triangle(decl, accept, tri[u / (uint32_t)n_rays],
-                                        u / (uint32_t)n_rays, R.c_str(), seen, prev);
+        uint32_t v = u + (uint32_t)n_rays;                  // this ray's next emitted test
+        while (v < N && !used[v]) v += (uint32_t)n_rays;
+        const bool defer = used[u] && v < N && reused[v];   // same region as its quad partner
+        emit_triangle(decl, accept, tri[u / (uint32_t)n_rays], u / (uint32_t)n_rays, R.c_str(),
+                      seen, prev, nullptr, defer);
         out += decl;
-        if (!used) continue;
+        if (!used[u]) continue;
         out += "    {\n" + accept + "    }\n";
+        if (defer) continue;
         out += R == "A" ? "    RVCP_SPEC_COMMIT1(btA);\n"
                         : "    RVCP_SPEC_COMMIT(bt" + R + ", best" + R + ");\n";
     }

@@ -1563,6 +1563,9 @@ __device__ __forceinline__ void path_body(
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long c_start = A.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long t_exhausted = 0ull;
+    // RVCP_REGION_CLOCK (debug: hipRTC -D via RVCP_JIT_FLAGS): shader-clock cycles this wave
+    // spent in the scans and in everything else, summed over its iterations (timeline rec[6..7])
+    unsigned long long c_scan = 0ull, c_iter = 0ull;
     // the queue runs over the pre-pass's compact list; its length is in counters[3]
     FrameArgs Q = A;
     Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
@@ -1604,6 +1607,9 @@ __device__ __forceinline__ void path_body(
     BvhCarry carry;
 
     for (;;) {
+#ifdef RVCP_REGION_CLOCK
+        const unsigned long long c_top = __builtin_amdgcn_s_memtime();
+#endif
         // ---- settle: end samples, take pixels, emit surface events ----
         for (;;) {
             if (ended) {                                            // color += L / SPP (:495)
@@ -1745,6 +1751,9 @@ __device__ __forceinline__ void path_body(
 
         int bestA = -1, bestB = -1;
         float btA = A.t_max, btB = A.t_max;
+#ifdef RVCP_REGION_CLOCK
+        const unsigned long long c_scan0 = __builtin_amdgcn_s_memtime();
+#endif
         const uint32_t na = (uint32_t)__builtin_popcountll(mA);
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
         const bool tail = wave_active && (q.exhausted || A.early_tail) && nr <= kWave / 2 && !BVH &&
@@ -2130,6 +2139,9 @@ __device__ __forceinline__ void path_body(
             btB = btA;
             bestB = bestA;
         }
+#ifdef RVCP_REGION_CLOCK
+        c_scan += __builtin_amdgcn_s_memtime() - c_scan0;
+#endif
 
         // ---- resolve A: visibility of the light sample (:447-459) ----
         if (LDS_STATE) col = st_get3(13);
@@ -2174,11 +2186,16 @@ __device__ __forceinline__ void path_body(
             hasA = false;
             if (!defer_B) hasB = false;
         }
+#ifdef RVCP_REGION_CLOCK
+        c_iter += __builtin_amdgcn_s_memtime() - c_top;
+#endif
     }
     flush_wave_counters(counters, lane, trav_wave, iters);
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * BLK + threadIdx.x) / kWave;
-        unsigned long long *rec = A.timeline + 6ull * w;
+        unsigned long long *rec = A.timeline + 8ull * w;
+        rec[6] = c_scan;
+        rec[7] = c_iter;
         rec[0] = t_start;
         rec[1] = t_exhausted;
         rec[2] = __builtin_amdgcn_s_memrealtime();

@@ -33,7 +33,7 @@ run() {  # run <name> <timeout> cmd...
 }
 tl() {  # per-wave timeline + in-kernel clock: tl <name> <frames> frames.py-args...
     local name=$1 nf=$2; shift 2
-    run "$name" 300 bash -c "rm -f /tmp/tl_$name.bin && RVCP_LIB=$DBG RVCP_DEBUG_TIMELINE=/tmp/tl_$name.bin python tools/frames.py --frames $nf $* && python tools/timeline.py /tmp/tl_$name.bin --waves \$(python -c 'import os; print(os.path.getsize(\"/tmp/tl_$name.bin\") // 48 // $nf)')"
+    run "$name" 300 bash -c "rm -f /tmp/tl_$name.bin && RVCP_LIB=$DBG RVCP_DEBUG_TIMELINE=/tmp/tl_$name.bin python tools/frames.py --frames $nf $* && python tools/timeline.py /tmp/tl_$name.bin --waves \$(python -c 'import os; print(os.path.getsize(\"/tmp/tl_$name.bin\") // 64 // $nf)')"
 }
 
 rocm-smi --showproductname > "$OUT/${TAG}_rocm-smi.txt" 2>&1 || true
@@ -80,6 +80,7 @@ for s in $STEPS; do
         valu) run valu_rate 180 tools/build/valu_rate ;;
         valupmc) run valupmc 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/valupmc_$TAG" -o run --output-format csv -- tools/build/valu_rate ;;
         tlc3) tl tlc3 40 ;;
+        tlreg) run tlreg 300 bash -c "rm -f /tmp/tl_reg.bin && RVCP_LIB=$DBG RVCP_JIT_FLAGS=-DRVCP_REGION_CLOCK RVCP_DEBUG_TIMELINE=/tmp/tl_reg.bin python tools/frames.py --frames 6 && python tools/timeline.py /tmp/tl_reg.bin --waves \$(python -c 'import os; print(os.path.getsize(\"/tmp/tl_reg.bin\") // 64 // 6)')" ;;
         tlc2) tl tlc2 40 --size 384 --spp 10 ;;
         rehearse8c4) run rehearse8c4 400 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 --workload c4 --steps 5 --warmup 1 ;;
         rehearse8c4b) run rehearse8c4b 500 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29539 bench.py --gpus 8 --workload c4 --steps 20 --warmup 4 ;;
@@ -110,6 +111,7 @@ for s in $STEPS; do
         abgen2) run ab_gen2 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3gen" "gfast=RVCP_LIB=tools/build/var_gfast/librvcp.so::--workload c3gen" "new=::--workload c3gen" "c3gfast=RVCP_LIB=tools/build/var_gfast/librvcp.so::--workload c3" "c3new=::--workload c3" ;;
         abm2sq) run ab_m2sq 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_pipe/librvcp.so::--workload spheres --steps 60" "new=::--workload spheres --steps 60" "c3m2base=RVCP_LIB=tools/build/var_pipe/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
         legacy) run pytest_legacy 600 python -u -m pytest tests/test_gpu_legacy.py tests/test_gpu_specialize.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        abprev) run ab_prev 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload c3" "new=::--workload c3" "c2prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" "m2prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload spheres --steps 60" "m2new=::--workload spheres --steps 60" ;;
         pipeline) run pytest_pipeline 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_bench.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         benchrot) run bench_c3rot 300 python bench.py --workload c3rot --steps 30 --warmup 5 --no-cpu-baseline ;;
         benchgen) run bench_c3gen 300 python bench.py --workload c3gen --steps 30 --warmup 5 --no-cpu-baseline ;;
