@@ -820,7 +820,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
             // schedules 3/6 spreading a small surface list run the full resident grid
             if (A.spread_min && !legacy && !A.accel && (A.variant == 3 || A.variant == 6)) blocks = cap;
             ctx->last_timeline_waves = 0;
-            if (RVCP_KNOB("RVCP_DEBUG_TIMELINE") && !legacy && A.variant >= 3) {
+            if (RVCP_KNOB("RVCP_DEBUG_TIMELINE") && (legacy || A.variant >= 3)) {
                 const size_t waves = (size_t)blocks * wpb;
                 if (ctx->cap_timeline < waves) {
                     (void)hipFree(ctx->d_timeline);
@@ -847,10 +847,22 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                 lin = ctx->d_acc;
             }
             if (legacy) {
-                HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
+                // the pre-pass's surface list (legacy_primary_kernel), one record per pixel at most
+                if (ctx->cap_surf < split_px) {
+                    (void)hipFree(ctx->d_surf);
+                    ctx->d_surf = nullptr;
+                    ctx->cap_surf = 0;
+                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)split_px * sizeof(SurfRecord)));
+                    ctx->cap_surf = split_px;
+                }
+                // (debug build: RVCP_DEBUG_NO_LEGACY_PREPASS keeps the pixel starts and primary
+                // traces in the persistent kernel, for A/Bs)
+                const bool prepass = !RVCP_KNOB("RVCP_DEBUG_NO_LEGACY_PREPASS");
+                if (!prepass) HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_legacy(&A, ctx->d_tri, ctx->d_shade, ctx->d_spheres,
                                         ctx->d_rawmats, ctx->d_unorm, (uint32_t *)d_rgba8,
-                                        lin, ctx->d_counters, blocks, s,
+                                        lin, ctx->d_counters, prepass ? ctx->d_surf : nullptr,
+                                        blocks, s, prepass ? ctx->evm : nullptr,
                                         spec_legacy ? (void *)jk->legacy : nullptr);
                 if (spec_legacy) ctx->last_spec = true;
             } else if (A.variant >= 3) {

@@ -63,7 +63,19 @@ __device__ __forceinline__ float sqrt_c(float x) { return sqrt_ieee(x); }
 __device__ __forceinline__ float len(f3 a) { return sqrt_c(dot(a, a)); }
 // 1 / sqrt by rcp_ieee below (the IEEE quotient, fast path verified over all inputs)
 __device__ __forceinline__ float rcp_ieee(float den);
-__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, rcp_ieee(sqrt_c(dot(a, a)))); }
+// normalize(v) = v * RN(1 / RN(sqrt(dot(v, v)))).  Where sqrt_fast_ok admits x = dot(v, v) the
+// root s lies in [2^-50, 2^50] and its reciprocal is normal -- and wherever v_rcp + one Newton
+// step gives a normal result it equals the IEEE quotient (all 2^32 inputs, tools/rcp_check2.hip)
+// -- so the root's guard covers the reciprocal too: one guard and one rare branch instead of
+// two.  Any other x takes the IEEE root and rcp_ieee.
+__device__ __forceinline__ f3 normalize(f3 a) {
+    const float x = dot(a, a);
+    const float s = sqrt_fast_core(x);
+    const float y = __builtin_amdgcn_rcpf(s);
+    float r = __builtin_fmaf(__builtin_fmaf(-s, y, 1.0f), y, y);
+    if (__builtin_expect(!sqrt_fast_ok(x), 0)) r = rcp_ieee(__builtin_sqrtf(x));
+    return muls(a, r);
+}
 __device__ __forceinline__ float fractf(float x) { return x - __builtin_floorf(x); }
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 
@@ -94,13 +106,15 @@ __device__ __forceinline__ float pt_sinf(float x) {
 // pt_sinf for rand()'s arguments only: seed + index with seed in [0, 1] (a fract) and index a
 // float counter that stops growing at 2^24, so x lies in [1, 2^24 + 4]: finite and positive,
 // q = rint(x / pi) < 2^23 is an exact integer, and its parity is the low bit of (int)q, moved
-// into the sign bit.  The same arithmetic as pt_sinf without its range guard.
+// into the sign bit.  The same arithmetic as pt_sinf without its range guard.  (The flip is an
+// add: q << 31 is 0 or 2^31, and adding 2^31 mod 2^32 flips bit 31 alone -- one v_lshl_add_u32
+// instead of a shift and an xor.)
 __device__ __forceinline__ float pt_sinf_rand(float x) {
     const float q = __builtin_rintf(x * kInvPi);
     float r = __builtin_fmaf(q, -kPiHi, x);
     r = __builtin_fmaf(q, kPiLo, r);
     const float s = sin_poly(r);
-    return __uint_as_float(__float_as_uint(s) ^ ((uint32_t)(int)q << 31));
+    return __uint_as_float(__float_as_uint(s) + ((uint32_t)(int)q << 31));
 }
 
 __device__ __forceinline__ uint32_t lane_id() {
@@ -858,8 +872,19 @@ __device__ __forceinline__ bool nee_sample(const FrameArgs &A, const LightRecord
     const f3 Xp = add(add(muls(Lv0, 1.0f - x), muls(Lv1, x * (1.0f - y))),
                       muls(Lv2, x * y));                                           // :324
     const f3 dv = sub(Xp, S_pos);
-    dist = len(dv);                                                                // :438
-    ws = divs_pos(dv, dist);                                                       // :439
+    {   // dist = length(dv) (:438), ws = dv / dist (:439): as normalize, the root's guard makes
+        // the fast reciprocal of dist exact and puts dist in quot_box's range, so one guard
+        // (with the components' box) covers the root, the reciprocal and the quotients
+        const float x2 = dot(dv, dv);
+        dist = sqrt_fast_core(x2);
+        const float y0 = __builtin_amdgcn_rcpf(dist);
+        const float y = __builtin_fmaf(__builtin_fmaf(-dist, y0, 1.0f), y0, y0);
+        ws = mk(quot_refine(dv.x, dist, y), quot_refine(dv.y, dist, y), quot_refine(dv.z, dist, y));
+        if (__builtin_expect(!(sqrt_fast_ok(x2) & quot_box(dv)), 0)) {
+            dist = len(dv);
+            ws = divs_pos(dv, dist);
+        }
+    }
     const float cosp = dot(S_nrm, ws);
     const f3 f = cosp > 0.0f ? alb_pi : mk(0, 0, 0);                               // :344-349
     C = mulv(mulv(att, Lle), f);                                                   // :450-458
@@ -938,8 +963,11 @@ __device__ __forceinline__ void coop_unit_sphere(bool need, float seed, float &r
             continue;
         }
         // floor(log2(64 / n)) = 6 - ceil(log2 n) (64 / n >= 2^k <=> n <= 2^(6-k)), from the
-        // wave-uniform n without an integer division
-        const uint32_t lgK = 6u - (n > 1u ? 32u - (uint32_t)__builtin_clz(n - 1u) : 0u);
+        // wave-uniform n without an integer division; at most 32 candidates per lane (n = 1
+        // leaves half the wave idle, a 0.476^32 chance of another round), so that every owner's
+        // segment of the acceptance ballot lies in one 32-bit half
+        const uint32_t lgK0 = 6u - (n > 1u ? 32u - (uint32_t)__builtin_clz(n - 1u) : 0u);
+        const uint32_t lgK = lgK0 < 5u ? lgK0 : 5u;
         const uint32_t K = 1u << lgK;
         const uint32_t r = rank_in(M);
         if (need) tab[r] = (uint8_t)lane;
@@ -955,12 +983,17 @@ __device__ __forceinline__ void coop_unit_sphere(bool need, float seed, float &r
         const float ry = rand_of(s_seed + (base + 2.0f));
         const float rz = rand_of(s_seed + (base + 3.0f));
         const f3 p = mk(cube_coord(rx), cube_coord(ry), cube_coord(rz));
-        const uint64_t AM = __ballot(worker && !(dot(p, p) >= 1.0f));
-        const uint64_t segmask = K >= 64u ? ~0ull : ((1ull << K) - 1ull);
-        const uint64_t seg = need ? ((AM >> (r << lgK)) & segmask) : 0ull;
-        const bool got = seg != 0ull;
-        const uint32_t cstar = got ? (uint32_t)__builtin_ctzll(seg) : 0u;
-        const int src = got ? (int)((r << lgK) + cstar) : (int)lane;
+        // (the acceptance and the worker masks ANDed in scalar registers: a ballot of the
+        // combined predicate materialised it in a VGPR and compared it again)
+        const uint64_t AM = __builtin_amdgcn_ballot_w64(!(dot(p, p) >= 1.0f)) &
+                            __builtin_amdgcn_ballot_w64(worker);
+        // this owner's K acceptance bits (workers r K .. r K + K - 1, K <= 32)
+        const uint32_t off = r << lgK;
+        const uint32_t segmask = K >= 32u ? ~0u : ((1u << K) - 1u);
+        const uint32_t seg = (uint32_t)(AM >> off) & segmask;
+        const bool got = need && seg != 0u;
+        const uint32_t cstar = (uint32_t)__builtin_ctz(seg | 0x80000000u);   // seg != 0: its lowest bit
+        const int src = got ? (int)(off + cstar) : (int)lane;
         const f3 pp = mk(__shfl(p.x, src), __shfl(p.y, src), __shfl(p.z, src));
         if (got) {
             p_out = pp;
@@ -1563,9 +1596,18 @@ __device__ __forceinline__ void path_body(
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long c_start = A.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long t_exhausted = 0ull;
-    // RVCP_REGION_CLOCK (debug: hipRTC -D via RVCP_JIT_FLAGS): shader-clock cycles this wave
-    // spent in the scans and in everything else, summed over its iterations (timeline rec[6..7])
+    // RVCP_REGION_CLOCK=k (debug builds of the specialised module only): shader-clock cycles this wave
+    // spent in region k and in its iterations as a whole, summed (timeline rec[6..7]); regions:
+    // 1 the scans, 2 the settle loop, 3 the resolve step, 4 the unit-ball sample + BRDF update,
+    // 5 the light sample (nee_sample)
     unsigned long long c_scan = 0ull, c_iter = 0ull;
+#ifdef RVCP_REGION_CLOCK
+#define RC_BEGIN(k) const unsigned long long rc_t##k = (RVCP_REGION_CLOCK == k) ? __builtin_amdgcn_s_memtime() : 0ull
+#define RC_END(k) do { if (RVCP_REGION_CLOCK == k) c_scan += __builtin_amdgcn_s_memtime() - rc_t##k; } while (0)
+#else
+#define RC_BEGIN(k) do {} while (0)
+#define RC_END(k) do {} while (0)
+#endif
     // the queue runs over the pre-pass's compact list; its length is in counters[3]
     FrameArgs Q = A;
     Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
@@ -1610,6 +1652,7 @@ __device__ __forceinline__ void path_body(
 #ifdef RVCP_REGION_CLOCK
         const unsigned long long c_top = __builtin_amdgcn_s_memtime();
 #endif
+        RC_BEGIN(2);
         // ---- settle: end samples, take pixels, emit surface events ----
         for (;;) {
             if (ended) {                                            // color += L / SPP (:495)
@@ -1661,8 +1704,11 @@ __device__ __forceinline__ void path_body(
                 surf_ev = false;
                 if (LDS_STATE) att = st_get3(10);
                 f3 ws;
-                if (nee_sample(A, lights, S_alb, S_pos, S_nrm, att, seed, ridx, nee_C, nee_dist,
-                               ws)) {
+                RC_BEGIN(5);
+                const bool nee_ok = nee_sample(A, lights, S_alb, S_pos, S_nrm, att, seed, ridx,
+                                               nee_C, nee_dist, ws);
+                RC_END(5);
+                if (nee_ok) {
                     a_o = add(S_pos, muls(ws, A.eps));
                     a_d = ws;
                     a_p = S_pos;
@@ -1677,6 +1723,7 @@ __device__ __forceinline__ void path_body(
                 if (!need_dir && !hasA) ended = true;
             }
             f3 p = mk(0, 0, 0);
+            RC_BEGIN(4);
             coop_unit_sphere(need_dir, seed, ridx, p, lane, tail_tab[wv]);
             if (need_dir) {                                         // :464-478
                 f3 wi;
@@ -1690,8 +1737,10 @@ __device__ __forceinline__ void path_body(
                 }
                 if (!hasA && !hasB) ended = true;
             }
+            RC_END(4);
             if (!__any(ended)) break;
         }
+        RC_END(2);
         // The shading point is dead until the next surface event sets it again (resolve B, or
         // a sample / pixel start): say so, so that it is not held in 9 VGPRs across the scan.
         S_pos = mk(0, 0, 0);
@@ -1751,9 +1800,7 @@ __device__ __forceinline__ void path_body(
 
         int bestA = -1, bestB = -1;
         float btA = A.t_max, btB = A.t_max;
-#ifdef RVCP_REGION_CLOCK
-        const unsigned long long c_scan0 = __builtin_amdgcn_s_memtime();
-#endif
+        RC_BEGIN(1);
         const uint32_t na = (uint32_t)__builtin_popcountll(mA);
         const uint32_t nr = na + (uint32_t)__builtin_popcountll(mB);
         const bool tail = wave_active && (q.exhausted || A.early_tail) && nr <= kWave / 2 && !BVH &&
@@ -2139,9 +2186,8 @@ __device__ __forceinline__ void path_body(
             btB = btA;
             bestB = bestA;
         }
-#ifdef RVCP_REGION_CLOCK
-        c_scan += __builtin_amdgcn_s_memtime() - c_scan0;
-#endif
+        RC_END(1);
+        RC_BEGIN(3);
 
         // ---- resolve A: visibility of the light sample (:447-459) ----
         if (LDS_STATE) col = st_get3(13);
@@ -2186,6 +2232,7 @@ __device__ __forceinline__ void path_body(
             hasA = false;
             if (!defer_B) hasB = false;
         }
+        RC_END(3);
 #ifdef RVCP_REGION_CLOCK
         c_iter += __builtin_amdgcn_s_memtime() - c_top;
 #endif
@@ -2399,6 +2446,53 @@ __device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d
 
 constexpr int L_IDLE = 0, L_TRACE = 1, L_SCATTER = 2, L_END = 3;
 
+// The sphere half of get_intersection_with_scene (:369-381) for the tracing lanes (`active`);
+// FAST as sphere_accept, chosen per wave by the caller.
+template <bool FAST>
+__device__ __forceinline__ void legacy_spheres(const FrameArgs &A, const rvcp_sphere_t *__restrict__ sph,
+                                               f3 ro, f3 rd, float a, float two_a, float rtmin,
+                                               float &bt, int &best) {
+    const float y = FAST ? rcp_ieee(two_a) : 0.0f;
+    for (uint32_t i = 0; i < A.n_spheres; ++i) {
+        float t;
+        if (sphere_accept<FAST>(sph[i], ro, rd, a, two_a, y, rtmin, bt, t)) { bt = t; best = (int)i; }
+    }
+}
+
+// The hit record of the nearest hit `best` (spheres first, then faces) of ray (ro, rd) at time
+// bt: position, the normal against the ray and whether the ray hit the front face
+// (:314-319 spheres, :348-363 faces), and the material.
+__device__ __forceinline__ void legacy_hit(const FrameArgs &A, const TriRecord *__restrict__ tri,
+                                           const FaceShade *__restrict__ shade,
+                                           const rvcp_sphere_t *__restrict__ sph, int best, f3 ro,
+                                           f3 rd, float bt, f3 &hpos, f3 &hn, uint32_t &hm,
+                                           bool &ho) {
+    ho = true;
+    hpos = add(ro, muls(rd, bt));
+    if ((uint32_t)best < A.n_spheres) {                         // :314-319
+        const rvcp_sphere_t S = sph[best];
+        const f3 ce = ld3(S.center);
+        hn = normalize(sub(hpos, ce));
+        const f3 oc = sub(ro, ce);
+        if (dot(oc, oc) < S.radius * S.radius) { hn = neg(hn); ho = false; }
+        hm = S.material_id;
+    } else {                                                    // :348-363
+        const int fi = best - (int)A.n_spheres;
+        const TriRecord T = tri[fi];
+        const FaceShade fs = shade[fi];
+        const f3 s = mk(ro.x - T.v0[0], ro.y - T.v0[1], ro.z - T.v0[2]);
+        const f3 s1 = cross(rd, ld3(T.e2));
+        const f3 s2 = cross(s, ld3(T.e1));
+        const float f = rcp_ieee(dot(s1, ld3(T.e1)));
+        const float b1 = f * dot(s1, s);
+        const float b2 = f * dot(s2, rd);
+        hn = normalize(add(add(muls(ld3(fs.n0), 1.0f - b1 - b2), muls(ld3(fs.n1), b1)),
+                           muls(ld3(fs.n2), b2)));
+        if (dot(hn, rd) > 0.0f) { hn = neg(hn); ho = false; }
+        hm = fs.mat;
+    }
+}
+
 // kLegacyDefer: the most lanes left ending a sample that sit out one trace (below).  16
 // measured best: sphere room 0.367 -> 0.345 ms, mode 2 on the C3 frame 2.237 -> 2.156 ms per
 // frame (profiles/r03v_m2_defer_sweep.log; 8, 24, 32, 40 and 64 less good).
@@ -2411,15 +2505,43 @@ __device__ __forceinline__ void legacy_body(
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    uint8_t (*coop_tab)[kWave])
+    uint8_t (*coop_tab)[kWave], const SurfRecord *__restrict__ lsurf)
 {
     uint8_t *tab = coop_tab[threadIdx.x / kWave];
     const uint32_t lane = lane_id();
-    Queue q = queue_init(A);
+    // The queue runs over legacy_primary_kernel's list of surface pixels (its length in
+    // counters[3]), each with its seed and cached primary hit; static chunks as path_body's.
+    // (RVCP_LEGACY_NO_PREPASS, debug builds of the specialised module for A/Bs: the pixels'
+    // starts and primary traces run here, lsurf is null.)
+#ifdef RVCP_LEGACY_NO_PREPASS
+    constexpr bool kPre = false;
+#else
+    constexpr bool kPre = true;
+    if (!lsurf) return;
+#endif
+    FrameArgs Q = A;
+    if (kPre) {
+        Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
+        uint32_t waves, c;
+        static_split(Q.n_pixels, gridDim.x * (kBlock / kWave), A.n_simds, waves, c);
+        Q.static_chunk = c;
+        Q.static_chunks = c * waves;
+    }
+    Queue q = queue_init(Q);
     const float sppf = (float)A.spp;
     const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
     const float inv_rr = rcp_ieee(A.rr);
+    // RR = 1.0 (ray_tracer.comp's own setting): rand() < 1 (v_fract_f32 never returns 1), so
+    // the roulette never ends a path and only advances the rand() index, and att / 1.0 = att
+    // exactly -- neither the sine nor the division is computed (wave-uniform)
+    const bool rr_one = A.rr == 1.0f;
 
+    // debug timeline (FrameArgs::timeline) and RVCP_REGION_CLOCK=k as in path_body; regions:
+    // 1 the trace (spheres + faces), 2 the settle loop, 3 the hit record, 4 the scatter block,
+    // 5 taking new pixels (queue + srand + sample_ray)
+    const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long c_start = A.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
+    unsigned long long c_scan = 0ull, c_iter = 0ull;
     int st = L_IDLE;
     bool need_pixel = true, done = false, primary = false;
     uint32_t pix = 0, k = 0, left = 0, trav = 0, iters = 0;
@@ -2435,13 +2557,17 @@ __device__ __forceinline__ void legacy_body(
     float rtmin = 0.0f, rtmax = 0.0f;
 
     for (;;) {
+#ifdef RVCP_REGION_CLOCK
+        const unsigned long long c_top = __builtin_amdgcn_s_memtime();
+#endif
+        RC_BEGIN(2);
         // ============ settle: advance every lane until it has a ray or is done ============
         for (;;) {
             if (st == L_END) {                                      // color += ray_trace (:817)
                 acc = add(acc, col);
                 k += 1;
-                if (k >= A.spp) {
-                    store_acc(batch_out(A, pix), divs_y(acc, sppf, inv_spp), out_lin);   // :819-821
+                if (k >= A.spp) {                                   // :819-821
+                    store_acc(kPre ? pix : batch_out(A, pix), divs_y(acc, sppf, inv_spp), out_lin);
                     need_pixel = true;
                     st = L_IDLE;
                 } else {                                            // next sample, cached hit
@@ -2452,11 +2578,29 @@ __device__ __forceinline__ void legacy_body(
                     st = L_SCATTER;
                 }
             }
+            RC_BEGIN(5);
             {   // take new pixels from the frame queue (wave-uniform control flow)
                 bool got;
                 uint32_t np = pix;
-                queue_take(q, __ballot(need_pixel && !done), lane, A, counters, got, np);
-                if (got) {
+                queue_take(q, __ballot(need_pixel && !done), lane, Q, counters, got, np);
+                if (kPre && got) {
+                    // a surface pixel of the pre-pass: its first scatter is from the cached hit
+                    const SurfRecord r = lsurf[np];
+                    pix = r.pix;                                    // the output index
+                    seed = r.seed;
+                    ridx = 0.0f;
+                    P_pos = ld3(r.pos); P_nrm = ld3(r.nrm); P_dir = ld3(r.alb_pi);
+                    P_mat = r.mat & 0x7FFFFFFFu;
+                    P_out = (r.mat >> 31) == 0u;
+                    H_pos = P_pos; H_nrm = P_nrm; H_dir = P_dir; H_mat = P_mat; H_out = P_out;
+                    left = A.max_bounces - 1u;
+                    need_pixel = false;
+                    k = 0;
+                    acc = mk(0, 0, 0);
+                    att = mk(1, 1, 1);
+                    col = mk(0, 0, 0);
+                    st = L_SCATTER;
+                } else if (!kPre && got) {
                     pix = np;
                     if (A.batch_cams) start_batch_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
                     else start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
@@ -2471,6 +2615,8 @@ __device__ __forceinline__ void legacy_body(
                     done = true;
                 }
             }
+            RC_END(5);
+            RC_BEGIN(4);
             if (__any(st == L_SCATTER)) {
                 // material_scatter (:585-602), then the tail of the bounce loop (:668-686)
                 const bool sc = st == L_SCATTER;
@@ -2523,10 +2669,11 @@ __device__ __forceinline__ void legacy_body(
                     rtmax = A.t_max;
                     if (att.x < A.eps && att.y < A.eps && att.z < A.eps) {  // :673-676
                         st = L_END;
-                    } else if (rnd(seed, ridx) >= A.rr) {                   // :679-681
+                    } else if (rr_one ? (ridx = ridx + 1.0f, false)          // :679-681
+                                      : rnd(seed, ridx) >= A.rr) {
                         st = L_END;
                     } else {
-                        att = divs_y(att, A.rr, inv_rr);                     // :683
+                        if (!rr_one) att = divs_y(att, A.rr, inv_rr);        // :683
                         if (left == 0u) {
                             st = L_END;                                     // :633
                         } else {
@@ -2536,6 +2683,7 @@ __device__ __forceinline__ void legacy_body(
                     }
                 }
             }
+            RC_END(4);
             if (!__any(st == L_END)) break;
             // Lanes whose sample ended in this scatter (bounce limit) sit out one trace when
             // few of them did and other lanes have rays: their next sample's scatter then runs
@@ -2543,8 +2691,10 @@ __device__ __forceinline__ void legacy_body(
             // now.  Timing only: each lane's own sequence of operations is unchanged.
             if (__any(st == L_TRACE) && __popcll(__ballot(st == L_END)) <= kLegacyDefer) break;
         }
+        RC_END(2);
         if (!__any(st == L_TRACE)) break;
         iters += 1;
+        RC_BEGIN(1);
 
         // ============ trace: get_intersection_with_scene, spheres then faces (:369-393) ============
         int best = -1;
@@ -2560,18 +2710,8 @@ __device__ __forceinline__ void legacy_body(
         const bool rfast = A.rcp_fast && __all(st != L_TRACE || dir_fast_ok(rd));
         if (st == L_TRACE) {
             trav += 1;
-            if (fast) {
-                const float y = rcp_ieee(two_a);
-                for (uint32_t i = 0; i < A.n_spheres; ++i) {
-                    float t;
-                    if (sphere_accept<true>(sph[i], ro, rd, a, two_a, y, rtmin, bt, t)) { bt = t; best = (int)i; }
-                }
-            } else {
-                for (uint32_t i = 0; i < A.n_spheres; ++i) {
-                    float t;
-                    if (sphere_accept<false>(sph[i], ro, rd, a, two_a, 0.0f, rtmin, bt, t)) { bt = t; best = (int)i; }
-                }
-            }
+            if (fast) legacy_spheres<true>(A, sph, ro, rd, a, two_a, rtmin, bt, best);
+            else legacy_spheres<false>(A, sph, ro, rd, a, two_a, rtmin, bt, best);
 #ifdef RVCP_SPEC_SCAN
             if (spec) {
                 // the scene-specialised scan (§4.7), exact for finite rays with t_min > 0
@@ -2595,6 +2735,8 @@ __device__ __forceinline__ void legacy_body(
             }
         }
 
+        RC_END(1);
+        RC_BEGIN(3);
         // ============ hit record + emission / miss (:636-661) ============
         if (st == L_TRACE) {
             if (best < 0) {
@@ -2603,30 +2745,8 @@ __device__ __forceinline__ void legacy_body(
             } else {
                 f3 hpos, hn;
                 uint32_t hm;
-                bool ho = true;
-                hpos = add(ro, muls(rd, bt));
-                if ((uint32_t)best < A.n_spheres) {                         // :314-319
-                    const rvcp_sphere_t S = sph[best];
-                    const f3 ce = ld3(S.center);
-                    hn = normalize(sub(hpos, ce));
-                    const f3 oc = sub(ro, ce);
-                    if (dot(oc, oc) < S.radius * S.radius) { hn = neg(hn); ho = false; }
-                    hm = S.material_id;
-                } else {                                                    // :348-363
-                    const int fi = best - (int)A.n_spheres;
-                    const TriRecord T = tri[fi];
-                    const FaceShade fs = shade[fi];
-                    const f3 s = mk(ro.x - T.v0[0], ro.y - T.v0[1], ro.z - T.v0[2]);
-                    const f3 s1 = cross(rd, ld3(T.e2));
-                    const f3 s2 = cross(s, ld3(T.e1));
-                    const float f = rcp_ieee(dot(s1, ld3(T.e1)));
-                    const float b1 = f * dot(s1, s);
-                    const float b2 = f * dot(s2, rd);
-                    hn = normalize(add(add(muls(ld3(fs.n0), 1.0f - b1 - b2), muls(ld3(fs.n1), b1)),
-                                       muls(ld3(fs.n2), b2)));
-                    if (dot(hn, rd) > 0.0f) { hn = neg(hn); ho = false; }
-                    hm = fs.mat;
-                }
+                bool ho;
+                legacy_hit(A, tri, shade, sph, best, ro, rd, bt, hpos, hn, hm, ho);
                 const rvcp_material_t &M = mats[hm];
                 if (M.ty == kLight) {                                       // :656-660
                     col = add(col, mulv(att, ld3(M.albedo)));
@@ -2636,7 +2756,7 @@ __device__ __forceinline__ void legacy_body(
                     st = L_SCATTER;
                 }
             }
-            if (primary) {
+            if (!kPre && primary) {
                 primary = false;
                 if (st == L_END) {
                     // miss / light: every sample returns this same color without touching the
@@ -2651,11 +2771,124 @@ __device__ __forceinline__ void legacy_body(
                 }
             }
         }
+        RC_END(3);
+#ifdef RVCP_REGION_CLOCK
+        c_iter += __builtin_amdgcn_s_memtime() - c_top;
+#endif
     }
     flush_counters(counters, lane, trav, iters);
+    if (A.timeline && lane == 0) {
+        const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;
+        unsigned long long *rec = A.timeline + 8ull * w;
+        rec[0] = t_start;
+        rec[1] = 0ull;
+        rec[2] = __builtin_amdgcn_s_memrealtime();
+        rec[3] = iters;
+        rec[4] = c_start;
+        rec[5] = __builtin_amdgcn_s_memtime();
+        rec[6] = c_scan;
+        rec[7] = c_iter;
+    }
 }
 
 #ifndef RVCP_JIT
+// Mode 2's pre-pass (round 4): one pixel per lane, every pixel of the frame (or batch) -- srand,
+// sample_ray and the primary trace (spheres, then faces with the generic scan), which depend on
+// no rand() (:802-816) -- as legacy_body would do them for the pixel's first trace.  A miss or
+// a light finishes the pixel in closed form (its colour summed SPP times, :816-821, as
+// legacy_body's primary step); every other pixel is appended, with its seed, output index and
+// hit record, to the list legacy_body then takes pixels from: the persistent kernel no longer
+// starts pixels (srand's three sines, sample_ray) or traces primary rays in passes where a
+// few of its lanes need them.  SurfRecord as mode 2 uses it: pos, pix = output index, nrm,
+// seed, alb_pi = the ray direction, mat = material | (back face ? 2^31 : 0).
+__global__ __launch_bounds__(kPrimaryBlock) void legacy_primary_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
+    const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
+    SurfRecord *__restrict__ surf)
+{
+    __shared__ uint32_t block_count, block_base;
+    const uint32_t lane = lane_id();
+    const uint32_t pix = blockIdx.x * kPrimaryBlock + threadIdx.x;
+    const bool live = pix < A.n_pixels;
+    if (threadIdx.x == 0) block_count = 0;
+    __syncthreads();
+    float seed = 0.0f, ridx = 0.0f, rtmin = 0.0f, rtmax = 0.0f;
+    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1);
+    if (live) {
+        if (A.batch_cams) start_batch_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
+        else start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
+    }
+    int best = -1;
+    float bt = rtmax;
+    const float a = dot(rd, rd), two_a = 2.0f * a;
+    const bool fast = A.t_max < 0x1p29f &&
+                      __all(!live || ((two_a >= 0x1p-30f) & (two_a <= 0x1p30f) & (rtmin >= 0x1p-29f)));
+    const bool rfast = A.rcp_fast && __all(!live || dir_fast_ok(rd));
+    bool is_surf = false;
+    f3 hpos = mk(0, 0, 0), hn = mk(0, 0, 0);
+    uint32_t hm = 0;
+    bool ho = true;
+    const uint32_t opix = live ? batch_out(A, pix) : 0u;
+    if (live) {
+        if (fast) legacy_spheres<true>(A, sph, ro, rd, a, two_a, rtmin, bt, best);
+        else legacy_spheres<false>(A, sph, ro, rd, a, two_a, rtmin, bt, best);
+        if (rfast) {
+#pragma unroll 2
+            for (uint32_t i = 0; i < A.n_faces; ++i) {
+                float t;
+                if (tri_accept<true>(tri[i], ro, rd, rtmin, bt, t)) { bt = t; best = (int)(A.n_spheres + i); }
+            }
+        } else {
+#pragma unroll 2
+            for (uint32_t i = 0; i < A.n_faces; ++i) {
+                float t;
+                if (tri_accept(tri[i], ro, rd, rtmin, bt, t)) { bt = t; best = (int)(A.n_spheres + i); }
+            }
+        }
+        f3 col = mk(0, 0, 0);
+        const f3 att = mk(1, 1, 1);
+        bool end = true;
+        if (best < 0) {
+            col = add(col, mulv(att, mk(0, 0, 0)));     // sample_infinite_light = 0 (:600-606)
+        } else {
+            legacy_hit(A, tri, shade, sph, best, ro, rd, bt, hpos, hn, hm, ho);
+            const rvcp_material_t &M = mats[hm];
+            if (M.ty == kLight) col = add(col, mulv(att, ld3(M.albedo)));   // :656-660
+            else end = false;
+        }
+        if (end) {
+            // every sample returns this colour without touching the RNG: sum it SPP times
+            f3 acc = mk(0, 0, 0);
+            for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, col);
+            const float sppf = (float)A.spp;
+            store_acc(opix, divs_y(acc, sppf, rcp_ieee(sppf)), out_lin);
+        } else {
+            is_surf = true;
+        }
+    }
+    // append the block's surface pixels (LDS aggregation, one global atomic per block)
+    const uint64_t m = __ballot(is_surf);
+    uint32_t wave_off = 0;
+    if (lane == 0 && m) wave_off = atomicAdd(&block_count, (uint32_t)__builtin_popcountll(m));
+    wave_off = __shfl(wave_off, 0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        block_base = block_count ? atomicAdd((unsigned int *)&counters[3], block_count) : 0u;
+        const uint32_t lim = A.n_pixels - blockIdx.x * kPrimaryBlock;
+        atomicAdd(&counters[0], (unsigned long long)(lim < kPrimaryBlock ? lim : kPrimaryBlock));
+    }
+    __syncthreads();
+    if (is_surf) {
+        SurfRecord r;
+        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.pix = opix;
+        r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.seed = seed;
+        r.alb_pi[0] = rd.x; r.alb_pi[1] = rd.y; r.alb_pi[2] = rd.z;
+        r.mat = hm | (ho ? 0u : 0x80000000u);
+        surf[block_base + wave_off + rank_in(m)] = r;
+    }
+}
+
 #ifndef RVCP_LEGACY_MIN_WAVES
 #define RVCP_LEGACY_MIN_WAVES 1
 #endif
@@ -2663,10 +2896,11 @@ __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void legacy_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
-    float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
+    const SurfRecord *__restrict__ lsurf)
 {
     __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
-    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
+    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab, lsurf);
 }
 #else
 // mode 2 with the scene-specialised triangle scan (rvcp_jit.cpp, RVCP_JIT_LEGACY)
@@ -2677,7 +2911,8 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
     FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
-    float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
+    const SurfRecord *__restrict__ lsurf)
 {
     __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
 #ifdef RVCP_LEGACY_LDS_SCENE
@@ -2701,9 +2936,10 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
     }
     // (the sphere loop's wave-uniform records read from global memory by scalar loads instead,
     // beside the LDS copies for the per-lane gathers: 0.2855 vs 0.2814 ms, profiles/r04i_ab_m2c.log)
-    legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab);
+    legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab,
+                lsurf);
 #else
-    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
+    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab, lsurf);
 #endif
 }
 #endif
@@ -2901,20 +3137,32 @@ extern "C" int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRe
                                   const rvcp::FaceShade *shade, const void *spheres,
                                   const void *materials, const float *unorm_t, uint32_t *out_rgba,
                                   float *out_lin, unsigned long long *counters,
-                                  uint32_t grid_blocks, void *stream, void *spec_legacy_fn)
+                                  rvcp::SurfRecord *surf, uint32_t grid_blocks, void *stream,
+                                  void *main_event, void *spec_legacy_fn)
 {
+    if (surf) {     // the pre-pass: closed-form pixels and the surface list (legacy_primary_kernel)
+        const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
+        hipLaunchKernelGGL(rvcp::legacy_primary_kernel, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock),
+                           0, (hipStream_t)stream, *args, tri, shade, (const rvcp_sphere_t *)spheres,
+                           (const rvcp_material_t *)materials, out_lin, counters, surf);
+        if (hipGetLastError() != hipSuccess) return -2;
+    }
+    if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
+        return -2;
+    const rvcp::SurfRecord *lsurf = surf;
     if (spec_legacy_fn) {
         // the mode-2 kernel with the scene-specialised triangle scan (rvcp_jit.cpp)
         rvcp::FrameArgs a = *args;
         void *params[] = {&a, &tri, &shade, &spheres, &materials, &unorm_t, &out_rgba, &out_lin,
-                          &counters};
+                          &counters, &lsurf};
         if (hipModuleLaunchKernel((hipFunction_t)spec_legacy_fn, grid_blocks, 1, 1, rvcp::kBlock,
                                   1, 1, 0, (hipStream_t)stream, params, nullptr) != hipSuccess)
             return -2;
     } else {
         hipLaunchKernelGGL(rvcp::legacy_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, shade, (const rvcp_sphere_t *)spheres,
-                           (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters);
+                           (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters,
+                           lsurf);
         if (hipGetLastError() != hipSuccess) return -2;
     }
     // the frame's UNORM8 store (no gamma in mode 2) from the linear colours (a batch's frames

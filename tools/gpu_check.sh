@@ -9,6 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r03}
 shift || true
 STEPS=${*:-"smoke tests bench"}
+TLARGS=${TLARGS:-}
 OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -80,7 +81,7 @@ for s in $STEPS; do
         valu) run valu_rate 180 tools/build/valu_rate ;;
         valupmc) run valupmc 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/valupmc_$TAG" -o run --output-format csv -- tools/build/valu_rate ;;
         tlc3) tl tlc3 40 ;;
-        tlreg) run tlreg 300 bash -c "rm -f /tmp/tl_reg.bin && RVCP_LIB=$DBG RVCP_JIT_FLAGS=-DRVCP_REGION_CLOCK RVCP_DEBUG_TIMELINE=/tmp/tl_reg.bin python tools/frames.py --frames 6 && python tools/timeline.py /tmp/tl_reg.bin --waves \$(python -c 'import os; print(os.path.getsize(\"/tmp/tl_reg.bin\") // 64 // 6)')" ;;
+        tlreg) for k in 1 2 3 4 5; do run tlreg$k 300 bash -c "rm -f /tmp/tl_reg.bin && RVCP_LIB=$DBG RVCP_JIT_FLAGS=-DRVCP_REGION_CLOCK=$k RVCP_DEBUG_TIMELINE=/tmp/tl_reg.bin python tools/frames.py --frames 6 $TLARGS && python tools/timeline.py /tmp/tl_reg.bin --waves \$(python -c 'import os; print(os.path.getsize(\"/tmp/tl_reg.bin\") // 64 // 6)')"; done ;;
         tlc2) tl tlc2 40 --size 384 --spp 10 ;;
         rehearse8c4) run rehearse8c4 400 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 --workload c4 --steps 5 --warmup 1 ;;
         rehearse8c4b) run rehearse8c4b 500 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29539 bench.py --gpus 8 --workload c4 --steps 20 --warmup 4 ;;
@@ -112,6 +113,9 @@ for s in $STEPS; do
         abm2sq) run ab_m2sq 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_pipe/librvcp.so::--workload spheres --steps 60" "new=::--workload spheres --steps 60" "c3m2base=RVCP_LIB=tools/build/var_pipe/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
         legacy) run pytest_legacy 600 python -u -m pytest tests/test_gpu_legacy.py tests/test_gpu_specialize.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         abprev) run ab_prev 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload c3" "new=::--workload c3" "c2prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" "m2prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload spheres --steps 60" "m2new=::--workload spheres --steps 60" ;;
+        abcoop) run ab_coop 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "rand=RVCP_LIB=tools/build/var_rand/librvcp.so::--workload c3" "new=::--workload c3" "c2rand=RVCP_LIB=tools/build/var_rand/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" ;;
+        abnorm) run ab_norm 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3" "new=::--workload c3" "c2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" ;;
+        abpre) run ab_pre 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload spheres --steps 60" "new=::--workload spheres --steps 60" "nopre=RVCP_LIB=$DBG,RVCP_DEBUG_NO_LEGACY_PREPASS=1,RVCP_JIT_FLAGS=-DRVCP_LEGACY_NO_PREPASS::--workload spheres --steps 60" "pre=RVCP_LIB=$DBG::--workload spheres --steps 60" "c3m2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
         pipeline) run pytest_pipeline 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_bench.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         benchrot) run bench_c3rot 300 python bench.py --workload c3rot --steps 30 --warmup 5 --no-cpu-baseline ;;
         benchgen) run bench_c3gen 300 python bench.py --workload c3gen --steps 30 --warmup 5 --no-cpu-baseline ;;
