@@ -847,22 +847,10 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                 lin = ctx->d_acc;
             }
             if (legacy) {
-                // the pre-pass's surface list (legacy_primary_kernel), one record per pixel at most
-                if (ctx->cap_surf < split_px) {
-                    (void)hipFree(ctx->d_surf);
-                    ctx->d_surf = nullptr;
-                    ctx->cap_surf = 0;
-                    HIP_TRY(ctx, hipMalloc((void **)&ctx->d_surf, (size_t)split_px * sizeof(SurfRecord)));
-                    ctx->cap_surf = split_px;
-                }
-                // (debug build: RVCP_DEBUG_NO_LEGACY_PREPASS keeps the pixel starts and primary
-                // traces in the persistent kernel, for A/Bs)
-                const bool prepass = !RVCP_KNOB("RVCP_DEBUG_NO_LEGACY_PREPASS");
-                if (!prepass) HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
+                HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_legacy(&A, ctx->d_tri, ctx->d_shade, ctx->d_spheres,
                                         ctx->d_rawmats, ctx->d_unorm, (uint32_t *)d_rgba8,
-                                        lin, ctx->d_counters, prepass ? ctx->d_surf : nullptr,
-                                        blocks, s, prepass ? ctx->evm : nullptr,
+                                        lin, ctx->d_counters, blocks, s,
                                         spec_legacy ? (void *)jk->legacy : nullptr);
                 if (spec_legacy) ctx->last_spec = true;
             } else if (A.variant >= 3) {

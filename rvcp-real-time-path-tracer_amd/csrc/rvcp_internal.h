@@ -282,13 +282,10 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_frames, uint
                             void *spec_path_fn);
 // Integrator RVCP_INTEGRATOR_LEGACY (ray_tracer.comp): materials / spheres are the raw
 // rvcp_material_t / rvcp_sphere_t arrays, unorm_t the UNORM8 threshold table.
-// surf: legacy_primary_kernel's surface list (mode 2's pre-pass; nullptr = the persistent
-// kernel starts its pixels itself); main_event is recorded between the pre-pass and the kernel
 int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,
                        const rvcp::FaceShade *shade, const void *spheres, const void *materials,
                        const float *unorm_t, uint32_t *out_rgba, float *out_lin,
-                       unsigned long long *counters, rvcp::SurfRecord *surf,
-                       uint32_t grid_blocks, void *stream, void *main_event,
+                       unsigned long long *counters, uint32_t grid_blocks, void *stream,
                        void *spec_legacy_fn);
 int rvcp_legacy_occupancy(int *blocks_per_cu);
 // mandelbrot.comp (rvcp_mandelbrot.hip)

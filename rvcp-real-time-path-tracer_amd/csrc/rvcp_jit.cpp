@@ -578,6 +578,9 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
                                       "-fno-fast-math", "-fno-slp-vectorize", "-DRVCP_JIT",
                                       "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
     if (legacy) opts.push_back("-DRVCP_JIT_LEGACY");
+#ifdef RVCP_TIMELINE
+    opts.push_back("-DRVCP_TIMELINE");      // the debug library's modules keep the per-wave timeline
+#endif
     const std::string lw = "-DRVCP_LEGACY_MIN_WAVES=" + std::to_string(legacy_waves);
     if (legacy && legacy_waves > 0) opts.push_back(lw.c_str());
     if (legacy && lds_scene) opts.push_back("-DRVCP_LEGACY_LDS_SCENE");

@@ -185,7 +185,13 @@ __device__ __forceinline__ f3 divs_y(f3 v, float s, float y) {
     if (__builtin_expect(!ok, 0)) o = divs(v, s);
     return o;
 }
-__device__ __forceinline__ f3 divs_pos(f3 v, float s) { return divs_y(v, s, rcp_ieee(s)); }
+// v / s with y = RN(1/s) from v_rcp + one Newton step without rcp_ieee's class check: divs_y's
+// guard admits only s in [2^-50, 2^50], where that step is the IEEE reciprocal (§3.11), and
+// every other lane takes the IEEE divisions -- one guard and one rare branch instead of two.
+__device__ __forceinline__ f3 divs_pos(f3 v, float s) {
+    const float r = __builtin_amdgcn_rcpf(s);
+    return divs_y(v, s, __builtin_fmaf(__builtin_fmaf(-s, r, 1.0f), r, r));
+}
 
 // The scan's 1 / den: rcp_ieee, except that a zero or NaN denominator keeps the fast result
 // (NaN) instead of taking the IEEE division (+-inf / NaN).  Exact for the scan's decision: with
@@ -1593,9 +1599,14 @@ __device__ __forceinline__ void path_body(
     const uint32_t lane = lane_id();
     // this wave's index in the block, made wave-uniform (an SGPR) for the LDS row bases
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    // the per-wave timeline (FrameArgs::timeline) exists in the debug build only (RVCP_TIMELINE,
+    // also passed to its specialised modules): its clocks held across the kernel cost the
+    // product kernel SGPRs, spilled into VGPR lanes read back inside the loop
+#ifdef RVCP_TIMELINE
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long c_start = A.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long t_exhausted = 0ull;
+#endif
     // RVCP_REGION_CLOCK=k (debug builds of the specialised module only): shader-clock cycles this wave
     // spent in region k and in its iterations as a whole, summed (timeline rec[6..7]); regions:
     // 1 the scans, 2 the settle loop, 3 the resolve step, 4 the unit-ball sample + BRDF update,
@@ -1796,7 +1807,9 @@ __device__ __forceinline__ void path_body(
                                  (uint32_t)__builtin_popcountll(__ballot(newB))
                            : (uint32_t)__builtin_popcountll(mA) + (uint32_t)__builtin_popcountll(mB);
         bool frozen = false;
+#ifdef RVCP_TIMELINE
         if (A.timeline && q.exhausted && t_exhausted == 0ull) t_exhausted = __builtin_amdgcn_s_memrealtime();
+#endif
 
         int bestA = -1, bestB = -1;
         float btA = A.t_max, btB = A.t_max;
@@ -2238,6 +2251,7 @@ __device__ __forceinline__ void path_body(
 #endif
     }
     flush_wave_counters(counters, lane, trav_wave, iters);
+#ifdef RVCP_TIMELINE
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * BLK + threadIdx.x) / kWave;
         unsigned long long *rec = A.timeline + 8ull * w;
@@ -2250,6 +2264,7 @@ __device__ __forceinline__ void path_body(
         rec[4] = c_start;                              // shader-clock ticks (s_memtime)
         rec[5] = __builtin_amdgcn_s_memtime();
     }
+#endif
 }
 
 #ifndef RVCP_JIT
@@ -2505,29 +2520,11 @@ __device__ __forceinline__ void legacy_body(
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    uint8_t (*coop_tab)[kWave], const SurfRecord *__restrict__ lsurf)
+    uint8_t (*coop_tab)[kWave])
 {
     uint8_t *tab = coop_tab[threadIdx.x / kWave];
     const uint32_t lane = lane_id();
-    // The queue runs over legacy_primary_kernel's list of surface pixels (its length in
-    // counters[3]), each with its seed and cached primary hit; static chunks as path_body's.
-    // (RVCP_LEGACY_NO_PREPASS, debug builds of the specialised module for A/Bs: the pixels'
-    // starts and primary traces run here, lsurf is null.)
-#ifdef RVCP_LEGACY_NO_PREPASS
-    constexpr bool kPre = false;
-#else
-    constexpr bool kPre = true;
-    if (!lsurf) return;
-#endif
-    FrameArgs Q = A;
-    if (kPre) {
-        Q.n_pixels = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&counters[3]);
-        uint32_t waves, c;
-        static_split(Q.n_pixels, gridDim.x * (kBlock / kWave), A.n_simds, waves, c);
-        Q.static_chunk = c;
-        Q.static_chunks = c * waves;
-    }
-    Queue q = queue_init(Q);
+    Queue q = queue_init(A);
     const float sppf = (float)A.spp;
     const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
     const float inv_rr = rcp_ieee(A.rr);
@@ -2539,8 +2536,10 @@ __device__ __forceinline__ void legacy_body(
     // debug timeline (FrameArgs::timeline) and RVCP_REGION_CLOCK=k as in path_body; regions:
     // 1 the trace (spheres + faces), 2 the settle loop, 3 the hit record, 4 the scatter block,
     // 5 taking new pixels (queue + srand + sample_ray)
+#ifdef RVCP_TIMELINE
     const unsigned long long t_start = A.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const unsigned long long c_start = A.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
     unsigned long long c_scan = 0ull, c_iter = 0ull;
     int st = L_IDLE;
     bool need_pixel = true, done = false, primary = false;
@@ -2567,7 +2566,7 @@ __device__ __forceinline__ void legacy_body(
                 acc = add(acc, col);
                 k += 1;
                 if (k >= A.spp) {                                   // :819-821
-                    store_acc(kPre ? pix : batch_out(A, pix), divs_y(acc, sppf, inv_spp), out_lin);
+                    store_acc(batch_out(A, pix), divs_y(acc, sppf, inv_spp), out_lin);
                     need_pixel = true;
                     st = L_IDLE;
                 } else {                                            // next sample, cached hit
@@ -2582,25 +2581,8 @@ __device__ __forceinline__ void legacy_body(
             {   // take new pixels from the frame queue (wave-uniform control flow)
                 bool got;
                 uint32_t np = pix;
-                queue_take(q, __ballot(need_pixel && !done), lane, Q, counters, got, np);
-                if (kPre && got) {
-                    // a surface pixel of the pre-pass: its first scatter is from the cached hit
-                    const SurfRecord r = lsurf[np];
-                    pix = r.pix;                                    // the output index
-                    seed = r.seed;
-                    ridx = 0.0f;
-                    P_pos = ld3(r.pos); P_nrm = ld3(r.nrm); P_dir = ld3(r.alb_pi);
-                    P_mat = r.mat & 0x7FFFFFFFu;
-                    P_out = (r.mat >> 31) == 0u;
-                    H_pos = P_pos; H_nrm = P_nrm; H_dir = P_dir; H_mat = P_mat; H_out = P_out;
-                    left = A.max_bounces - 1u;
-                    need_pixel = false;
-                    k = 0;
-                    acc = mk(0, 0, 0);
-                    att = mk(1, 1, 1);
-                    col = mk(0, 0, 0);
-                    st = L_SCATTER;
-                } else if (!kPre && got) {
+                queue_take(q, __ballot(need_pixel && !done), lane, A, counters, got, np);
+                if (got) {
                     pix = np;
                     if (A.batch_cams) start_batch_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
                     else start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
@@ -2756,7 +2738,7 @@ __device__ __forceinline__ void legacy_body(
                     st = L_SCATTER;
                 }
             }
-            if (!kPre && primary) {
+            if (primary) {
                 primary = false;
                 if (st == L_END) {
                     // miss / light: every sample returns this same color without touching the
@@ -2777,6 +2759,7 @@ __device__ __forceinline__ void legacy_body(
 #endif
     }
     flush_counters(counters, lane, trav, iters);
+#ifdef RVCP_TIMELINE
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;
         unsigned long long *rec = A.timeline + 8ull * w;
@@ -2789,106 +2772,10 @@ __device__ __forceinline__ void legacy_body(
         rec[6] = c_scan;
         rec[7] = c_iter;
     }
+#endif
 }
 
 #ifndef RVCP_JIT
-// Mode 2's pre-pass (round 4): one pixel per lane, every pixel of the frame (or batch) -- srand,
-// sample_ray and the primary trace (spheres, then faces with the generic scan), which depend on
-// no rand() (:802-816) -- as legacy_body would do them for the pixel's first trace.  A miss or
-// a light finishes the pixel in closed form (its colour summed SPP times, :816-821, as
-// legacy_body's primary step); every other pixel is appended, with its seed, output index and
-// hit record, to the list legacy_body then takes pixels from: the persistent kernel no longer
-// starts pixels (srand's three sines, sample_ray) or traces primary rays in passes where a
-// few of its lanes need them.  SurfRecord as mode 2 uses it: pos, pix = output index, nrm,
-// seed, alb_pi = the ray direction, mat = material | (back face ? 2^31 : 0).
-__global__ __launch_bounds__(kPrimaryBlock) void legacy_primary_kernel(
-    FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
-    const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
-    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    SurfRecord *__restrict__ surf)
-{
-    __shared__ uint32_t block_count, block_base;
-    const uint32_t lane = lane_id();
-    const uint32_t pix = blockIdx.x * kPrimaryBlock + threadIdx.x;
-    const bool live = pix < A.n_pixels;
-    if (threadIdx.x == 0) block_count = 0;
-    __syncthreads();
-    float seed = 0.0f, ridx = 0.0f, rtmin = 0.0f, rtmax = 0.0f;
-    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1);
-    if (live) {
-        if (A.batch_cams) start_batch_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
-        else start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
-    }
-    int best = -1;
-    float bt = rtmax;
-    const float a = dot(rd, rd), two_a = 2.0f * a;
-    const bool fast = A.t_max < 0x1p29f &&
-                      __all(!live || ((two_a >= 0x1p-30f) & (two_a <= 0x1p30f) & (rtmin >= 0x1p-29f)));
-    const bool rfast = A.rcp_fast && __all(!live || dir_fast_ok(rd));
-    bool is_surf = false;
-    f3 hpos = mk(0, 0, 0), hn = mk(0, 0, 0);
-    uint32_t hm = 0;
-    bool ho = true;
-    const uint32_t opix = live ? batch_out(A, pix) : 0u;
-    if (live) {
-        if (fast) legacy_spheres<true>(A, sph, ro, rd, a, two_a, rtmin, bt, best);
-        else legacy_spheres<false>(A, sph, ro, rd, a, two_a, rtmin, bt, best);
-        if (rfast) {
-#pragma unroll 2
-            for (uint32_t i = 0; i < A.n_faces; ++i) {
-                float t;
-                if (tri_accept<true>(tri[i], ro, rd, rtmin, bt, t)) { bt = t; best = (int)(A.n_spheres + i); }
-            }
-        } else {
-#pragma unroll 2
-            for (uint32_t i = 0; i < A.n_faces; ++i) {
-                float t;
-                if (tri_accept(tri[i], ro, rd, rtmin, bt, t)) { bt = t; best = (int)(A.n_spheres + i); }
-            }
-        }
-        f3 col = mk(0, 0, 0);
-        const f3 att = mk(1, 1, 1);
-        bool end = true;
-        if (best < 0) {
-            col = add(col, mulv(att, mk(0, 0, 0)));     // sample_infinite_light = 0 (:600-606)
-        } else {
-            legacy_hit(A, tri, shade, sph, best, ro, rd, bt, hpos, hn, hm, ho);
-            const rvcp_material_t &M = mats[hm];
-            if (M.ty == kLight) col = add(col, mulv(att, ld3(M.albedo)));   // :656-660
-            else end = false;
-        }
-        if (end) {
-            // every sample returns this colour without touching the RNG: sum it SPP times
-            f3 acc = mk(0, 0, 0);
-            for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, col);
-            const float sppf = (float)A.spp;
-            store_acc(opix, divs_y(acc, sppf, rcp_ieee(sppf)), out_lin);
-        } else {
-            is_surf = true;
-        }
-    }
-    // append the block's surface pixels (LDS aggregation, one global atomic per block)
-    const uint64_t m = __ballot(is_surf);
-    uint32_t wave_off = 0;
-    if (lane == 0 && m) wave_off = atomicAdd(&block_count, (uint32_t)__builtin_popcountll(m));
-    wave_off = __shfl(wave_off, 0);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        block_base = block_count ? atomicAdd((unsigned int *)&counters[3], block_count) : 0u;
-        const uint32_t lim = A.n_pixels - blockIdx.x * kPrimaryBlock;
-        atomicAdd(&counters[0], (unsigned long long)(lim < kPrimaryBlock ? lim : kPrimaryBlock));
-    }
-    __syncthreads();
-    if (is_surf) {
-        SurfRecord r;
-        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.pix = opix;
-        r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.seed = seed;
-        r.alb_pi[0] = rd.x; r.alb_pi[1] = rd.y; r.alb_pi[2] = rd.z;
-        r.mat = hm | (ho ? 0u : 0x80000000u);
-        surf[block_base + wave_off + rank_in(m)] = r;
-    }
-}
-
 #ifndef RVCP_LEGACY_MIN_WAVES
 #define RVCP_LEGACY_MIN_WAVES 1
 #endif
@@ -2896,11 +2783,10 @@ __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void legacy_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
-    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    const SurfRecord *__restrict__ lsurf)
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
 {
     __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
-    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab, lsurf);
+    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
 }
 #else
 // mode 2 with the scene-specialised triangle scan (rvcp_jit.cpp, RVCP_JIT_LEGACY)
@@ -2911,8 +2797,7 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
     FrameArgs A, const TriRecord *__restrict__ tri, const FaceShade *__restrict__ shade,
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
-    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    const SurfRecord *__restrict__ lsurf)
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
 {
     __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
 #ifdef RVCP_LEGACY_LDS_SCENE
@@ -2936,10 +2821,9 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
     }
     // (the sphere loop's wave-uniform records read from global memory by scalar loads instead,
     // beside the LDS copies for the per-lane gathers: 0.2855 vs 0.2814 ms, profiles/r04i_ab_m2c.log)
-    legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab,
-                lsurf);
+    legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab);
 #else
-    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab, lsurf);
+    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
 #endif
 }
 #endif
@@ -3137,32 +3021,20 @@ extern "C" int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRe
                                   const rvcp::FaceShade *shade, const void *spheres,
                                   const void *materials, const float *unorm_t, uint32_t *out_rgba,
                                   float *out_lin, unsigned long long *counters,
-                                  rvcp::SurfRecord *surf, uint32_t grid_blocks, void *stream,
-                                  void *main_event, void *spec_legacy_fn)
+                                  uint32_t grid_blocks, void *stream, void *spec_legacy_fn)
 {
-    if (surf) {     // the pre-pass: closed-form pixels and the surface list (legacy_primary_kernel)
-        const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
-        hipLaunchKernelGGL(rvcp::legacy_primary_kernel, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock),
-                           0, (hipStream_t)stream, *args, tri, shade, (const rvcp_sphere_t *)spheres,
-                           (const rvcp_material_t *)materials, out_lin, counters, surf);
-        if (hipGetLastError() != hipSuccess) return -2;
-    }
-    if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
-        return -2;
-    const rvcp::SurfRecord *lsurf = surf;
     if (spec_legacy_fn) {
         // the mode-2 kernel with the scene-specialised triangle scan (rvcp_jit.cpp)
         rvcp::FrameArgs a = *args;
         void *params[] = {&a, &tri, &shade, &spheres, &materials, &unorm_t, &out_rgba, &out_lin,
-                          &counters, &lsurf};
+                          &counters};
         if (hipModuleLaunchKernel((hipFunction_t)spec_legacy_fn, grid_blocks, 1, 1, rvcp::kBlock,
                                   1, 1, 0, (hipStream_t)stream, params, nullptr) != hipSuccess)
             return -2;
     } else {
         hipLaunchKernelGGL(rvcp::legacy_kernel, dim3(grid_blocks), dim3(rvcp::kBlock), 0,
                            (hipStream_t)stream, *args, tri, shade, (const rvcp_sphere_t *)spheres,
-                           (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters,
-                           lsurf);
+                           (const rvcp_material_t *)materials, unorm_t, out_rgba, out_lin, counters);
         if (hipGetLastError() != hipSuccess) return -2;
     }
     // the frame's UNORM8 store (no gamma in mode 2) from the linear colours (a batch's frames

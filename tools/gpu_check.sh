@@ -115,7 +115,7 @@ for s in $STEPS; do
         abprev) run ab_prev 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload c3" "new=::--workload c3" "c2prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" "m2prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload spheres --steps 60" "m2new=::--workload spheres --steps 60" ;;
         abcoop) run ab_coop 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "rand=RVCP_LIB=tools/build/var_rand/librvcp.so::--workload c3" "new=::--workload c3" "c2rand=RVCP_LIB=tools/build/var_rand/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" ;;
         abnorm) run ab_norm 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3" "new=::--workload c3" "c2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" ;;
-        abpre) run ab_pre 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload spheres --steps 60" "new=::--workload spheres --steps 60" "nopre=RVCP_LIB=$DBG,RVCP_DEBUG_NO_LEGACY_PREPASS=1,RVCP_JIT_FLAGS=-DRVCP_LEGACY_NO_PREPASS::--workload spheres --steps 60" "pre=RVCP_LIB=$DBG::--workload spheres --steps 60" "c3m2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
+        abtl) run ab_tl 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3" "new=::--workload c3" "c2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" "m2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload spheres --steps 60" "m2new=::--workload spheres --steps 60" "c3m2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
         pipeline) run pytest_pipeline 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_bench.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         benchrot) run bench_c3rot 300 python bench.py --workload c3rot --steps 30 --warmup 5 --no-cpu-baseline ;;
         benchgen) run bench_c3gen 300 python bench.py --workload c3gen --steps 30 --warmup 5 --no-cpu-baseline ;;
