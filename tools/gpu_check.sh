@@ -59,7 +59,7 @@ for s in $STEPS; do
         # (per-launch durations that do not overlap -- roofline.per_launch)
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         # every launch timed (no warm-up, no launch pass): tools/trace_busy.py's busy time per frame
-        profbusy) run profbusy 600 rocprofv3 --kernel-trace --stats -d "$OUT/profbusy_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 0 --launch-pass 0 --no-cpu-baseline && python3 tools/trace_busy.py "$OUT/profbusy_$TAG/run_kernel_trace.csv" --frames 20 >> "$OUT/${TAG}_profbusy.log" ;;
+        profbusy) run profbusy 600 rocprofv3 --kernel-trace --stats -d "$OUT/profbusy_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 0 --launch-pass 0 --no-cpu-baseline && python3 tools/trace_busy.py "$OUT/profbusy_$TAG/run_kernel_trace.csv" --frames 20 --skip 2 >> "$OUT/${TAG}_profbusy.log" ;;
         prof1) run prof1 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof1_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
         # PMC passes, one counter group per run (one frame in flight and one frame per launch, so
         # each dispatch is one frame of its own)

@@ -10,7 +10,9 @@ bench.py's ms_per_step (it must not exceed it by more than the host-side gaps al
 
 --frames: the frames the traced run rendered.  Trace a run whose every launch is timed
 (`bench.py --warmup 0 --launch-pass 0`, gpu_check.sh step `profbusy`), so that the busy time per
-frame compares with that run's ms_per_step.
+frame compares with that run's ms_per_step.  --skip K: leave out the first K path-kernel launches
+and everything up to their end -- bench.py warms every frame-in-flight context with one full
+batch even at --warmup 0 (its warm-up rule), so K = frames in flight.
 """
 import argparse
 import csv
@@ -22,17 +24,23 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--frames", type=int, required=True)
+    ap.add_argument("--skip", type=int, default=0)
     a = ap.parse_args()
-    iv = []
-    n_path = 0
+    rows = []
     for r in csv.DictReader(open(a.trace)):
         name = r["Kernel_Name"]
         if not any(k in name for k in KERNELS):
             continue
-        iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-        if "path_kernel" in name or "legacy_kernel" in name or "tiled" in name:
-            n_path += 1
-    iv.sort()
+        is_path = "path_kernel" in name or "legacy_kernel" in name or "tiled" in name
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), is_path))
+    rows.sort()
+    if a.skip:
+        # the warm-up launches and what ran with them: everything that starts no later than the
+        # last of them ends (their pre-passes before, their tone maps at that end)
+        t_cut = max(e for _, e, _ in [r for r in rows if r[2]][:a.skip])
+        rows = [r for r in rows if r[0] > t_cut]
+    n_path = sum(1 for r in rows if r[2])
+    iv = [(s_, e_) for s_, e_, _ in rows]
     busy, cur_s, cur_e = 0, None, None
     for s, e in iv:
         if cur_e is None or s > cur_e:
