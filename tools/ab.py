@@ -19,6 +19,7 @@ Runners:
   python tools/ab.py --runner bench --passes 2 \\
       "base=::--workload c3" "v2=RVCP_LIB=tools/build/var_v2/librvcp.so::--workload c3"
   python tools/ab.py --runner frames "s3=::--variant 3" "s10=::--variant 10 --tris 2000"
+  python tools/ab.py --cases-file tools/ab_cases/c3_lib.txt      (one case per line)
 """
 import argparse
 import json
@@ -69,9 +70,20 @@ def main():
     ap.add_argument("--passes", type=int, default=2)
     ap.add_argument("--timeout", type=int, default=200)
     ap.add_argument("--field", default="ms_per_step", help="bench runner: the figure to compare")
-    ap.add_argument("cases", nargs="+")
+    ap.add_argument("--cases-file", help="cases one per line (# comments), after the positional ones; "
+                    "$DBG is the debug library")
+    ap.add_argument("cases", nargs="*")
     a = ap.parse_args()
-    cases = [parse_case(c) for c in a.cases]
+    texts = list(a.cases)
+    if a.cases_file:
+        dbg = "rvcp-real-time-path-tracer_amd/csrc/build/librvcp_debug.so"
+        for line in open(os.path.join(ROOT, a.cases_file)):
+            line = line.strip()
+            if line and not line.startswith("#"):
+                texts.append(line.replace("$DBG", dbg))
+    if not texts:
+        ap.error("no cases")
+    cases = [parse_case(c) for c in texts]
     got = {label: [] for label, _, _ in cases}
     for p in range(1, a.passes + 1):
         for label, env, args in cases:

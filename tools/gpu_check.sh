@@ -90,32 +90,16 @@ for s in $STEPS; do
         # schedules 4 / 10 on meshes (tools/ab.py, one frame at a time)
         c5pool) run c5pool 900 python tools/ab.py --runner frames "s4=::--variant 4 --tris 2000 --size 1024 --spp 8 --frames 6" "s10=::--variant 10 --tris 2000 --size 1024 --spp 8 --frames 6" ;;
         spec) run pytest_spec 900 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_pipeline.py tests/test_gpu_batch.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
-        abrcp) run ab_rcp 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3" "dbg=RVCP_LIB=$DBG::--workload c3" "unif=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_RCP_UNIFORM::--workload c3" "sqrt=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_SQRT=1::--workload c3" "fract=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_FRACT=1::--workload c3" "all=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_FAST_SQRT=1 -DRVCP_FAST_FRACT=1 -DRVCP_SPEC_RCP_UNIFORM::--workload c3" "ldsc=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_LDS_SCENE::--workload c3" "neeoff=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_NEE_SAME_OFF::--workload c3" ;;
         sqpmc3) run sqpmc3 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVE_CYCLES -d "$OUT/sqpmc3_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
         sqrtchk) run sqrt_check 300 tools/build/sqrt_check ;;
         bvhtest) run pytest_bvh 600 python -u -m pytest tests/test_gpu_bvh.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
-        abbvh) run ab_bvh 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" "c0=RVCP_LIB=tools/build/var_c0/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" "c4=RVCP_LIB=tools/build/var_c4/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" "c8=::--workload c5 --accel bvh --steps 10 --warmup 2" "c16=RVCP_LIB=tools/build/var_c16/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" "c8m16=RVCP_LIB=tools/build/var_c8m16/librvcp.so::--workload c5 --accel bvh --steps 10 --warmup 2" ;;
-        abm2b) run ab_m2b 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload spheres --steps 60" "w5=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_MIN_WAVES=5::--workload spheres --steps 60" "lds5=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=5::--workload spheres --steps 60" "lds6=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=6::--workload spheres --steps 60" "lds4=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=4::--workload spheres --steps 60" ;;
         m2test) run pytest_m2 600 python -u -m pytest tests/test_gpu_legacy.py tests/test_gpu_specialize.py tests/test_gpu_batch.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         benchsp) run bench_spheres 300 python bench.py --workload spheres --steps 60 --warmup 5 --no-cpu-baseline ;;
-        abbvh2) B="--workload c5 --accel bvh --steps 10 --warmup 2"; run ab_bvh2 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "c16=RVCP_LIB=tools/build/var_c16/librvcp.so::$B" "c24=RVCP_LIB=tools/build/var_c24/librvcp.so::$B" "c32=RVCP_LIB=tools/build/var_c32/librvcp.so::$B" "c48=RVCP_LIB=tools/build/var_c48/librvcp.so::$B" "c64=RVCP_LIB=tools/build/var_c64/librvcp.so::$B" "c32m16=RVCP_LIB=tools/build/var_c32m16/librvcp.so::$B" "c32m64=RVCP_LIB=tools/build/var_c32m64/librvcp.so::$B" ;;
         tracec2) run tracec2 300 rocprofv3 --kernel-trace --stats -d "$OUT/tracec2_$TAG" -o run --output-format csv -- python3 tools/frames.py --size 384 --spp 10 --frames 30 ;;
-        abc2lds) run ab_c2lds 900 python tools/ab.py --runner bench --field config.frame_latency_ms_alone --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload c2 --steps 40 --launch-pass 40" "lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_LDS_SCENE::--workload c2 --steps 40 --launch-pass 40" && run ab_c2lds_k 900 python tools/ab.py --runner frames --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--size 384 --spp 10 --frames 40" "lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_LDS_SCENE::--size 384 --spp 10 --frames 40" "c3dbg=RVCP_LIB=$DBG::--frames 12" "c3lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_LDS_SCENE::--frames 12" ;;
-        abreg) run ab_reg_lat 900 python tools/ab.py --runner bench --field config.frame_latency_ms_alone --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload c2 --steps 40 --launch-pass 40" "reg=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_REG_STATE::--workload c2 --steps 40 --launch-pass 40" && run ab_reg 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "c3dbg=RVCP_LIB=$DBG::--workload c3" "c3reg=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_REG_STATE::--workload c3" "c2dbg=RVCP_LIB=$DBG::--workload c2 --steps 100" "c2reg=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_SPEC_REG_STATE::--workload c2 --steps 100" ;;
-        abspread) run ab_spread 900 python tools/ab.py --runner bench --field config.frame_latency_ms_alone --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload c2 --steps 40 --launch-pass 40" "sp32=RVCP_LIB=$DBG,RVCP_DEBUG_SPREAD=32::--workload c2 --steps 40 --launch-pass 40" "sp24=RVCP_LIB=$DBG,RVCP_DEBUG_SPREAD=24::--workload c2 --steps 40 --launch-pass 40" "sp16=RVCP_LIB=$DBG,RVCP_DEBUG_SPREAD=16::--workload c2 --steps 40 --launch-pass 40" "sp16et=RVCP_LIB=$DBG,RVCP_DEBUG_SPREAD=16,RVCP_DEBUG_EARLY_TAIL=1::--workload c2 --steps 40 --launch-pass 40" "et=RVCP_LIB=$DBG,RVCP_DEBUG_EARLY_TAIL=1::--workload c2 --steps 40 --launch-pass 40" ;;
-        abgen) run ab_gen 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3gen" "new=::--workload c3gen" ;;
-        abm2) run ab_m2 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "dbg=RVCP_LIB=$DBG::--workload spheres --steps 60" "lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE::--workload spheres --steps 60" "lds5=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE -DRVCP_LEGACY_MIN_WAVES=5::--workload spheres --steps 60" "c3m2=RVCP_LIB=$DBG::--workload c3m2" "c3m2lds=RVCP_LIB=$DBG,RVCP_JIT_FLAGS=-DRVCP_LEGACY_LDS_SCENE::--workload c3m2" ;;
-        abgrp) run ab_grp 900 python tools/ab.py --runner frames --passes 2 "prod=::--size 384 --spp 10 --frames 20" "g2=RVCP_LIB=tools/build/var_g2/librvcp.so::--size 384 --spp 10 --frames 20" "g4=RVCP_LIB=tools/build/var_g4/librvcp.so::--size 384 --spp 10 --frames 20" "prodc3=::--frames 10" "g2c3=RVCP_LIB=tools/build/var_g2/librvcp.so::--frames 10" "g4c3=RVCP_LIB=tools/build/var_g4/librvcp.so::--frames 10" ;;
-        abc3) run ab_c3 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3" "new=::--workload c3" ;;
-        abc2lat) run ab_c2lat 900 python tools/ab.py --runner bench --field config.frame_latency_ms_alone --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c2 --steps 40 --launch-pass 40" "new=::--workload c2 --steps 40 --launch-pass 40" ;;
-        abm2new) run ab_m2new 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload spheres --steps 60" "new=::--workload spheres --steps 60" "c3m2base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
-        abgen2) run ab_gen2 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_base/librvcp.so::--workload c3gen" "gfast=RVCP_LIB=tools/build/var_gfast/librvcp.so::--workload c3gen" "new=::--workload c3gen" "c3gfast=RVCP_LIB=tools/build/var_gfast/librvcp.so::--workload c3" "c3new=::--workload c3" ;;
-        abm2sq) run ab_m2sq 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "base=RVCP_LIB=tools/build/var_pipe/librvcp.so::--workload spheres --steps 60" "new=::--workload spheres --steps 60" "c3m2base=RVCP_LIB=tools/build/var_pipe/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
         legacy) run pytest_legacy 600 python -u -m pytest tests/test_gpu_legacy.py tests/test_gpu_specialize.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
-        abprev) run ab_prev 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload c3" "new=::--workload c3" "c2prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" "m2prev=RVCP_LIB=tools/build/var_prev/librvcp.so::--workload spheres --steps 60" "m2new=::--workload spheres --steps 60" ;;
-        abcoop) run ab_coop 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "rand=RVCP_LIB=tools/build/var_rand/librvcp.so::--workload c3" "new=::--workload c3" "c2rand=RVCP_LIB=tools/build/var_rand/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" ;;
-        abnorm) run ab_norm 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3" "new=::--workload c3" "c2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" ;;
-        abtl) run ab_tl 900 python tools/ab.py --runner bench --passes ${PASSES:-3} "coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3" "new=::--workload c3" "c2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c2 --steps 100" "c2new=::--workload c2 --steps 100" "m2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload spheres --steps 60" "m2new=::--workload spheres --steps 60" "c3m2coop=RVCP_LIB=tools/build/var_coop/librvcp.so::--workload c3m2" "c3m2new=::--workload c3m2" ;;
+        # same-box A/Bs: tools/ab_cases/$AB.txt (one case per line; the round's experiments are
+        # recorded there with the variant libraries they compared, tools/build_variant.sh)
+        ab) run ab_${AB} 900 python tools/ab.py --runner ${ABRUNNER:-bench} ${ABFIELD:+--field $ABFIELD} --passes ${PASSES:-3} --cases-file tools/ab_cases/${AB}.txt ;;
         pipeline) run pytest_pipeline 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_bench.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         benchrot) run bench_c3rot 300 python bench.py --workload c3rot --steps 30 --warmup 5 --no-cpu-baseline ;;
         benchgen) run bench_c3gen 300 python bench.py --workload c3gen --steps 30 --warmup 5 --no-cpu-baseline ;;
