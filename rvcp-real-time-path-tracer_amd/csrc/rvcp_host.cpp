@@ -701,14 +701,15 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     // automatic schedule: 10 / 5 (LDS tiles; the workgroup's rays pooled into full passes on
     // large frames, one ray per lane on small ones) for large meshes, 10 also for mid-size
     // meshes on large frames, else 3, or 6 (6 waves/SIMD) for
-    // large frames -- except with the scene-specialised scan, whose 6-wave build spills and
-    // measures slower than its 5-wave one at every size
+    // large frames -- with the scene-specialised scan only for very large frames
+    // (kSpecWideMinSamples: its 6-wave build is slower below)
     const bool jit_ok = ctx->jit && ctx->cfg.ray_t_min > 0.0f;
     const bool big_frame = (uint64_t)A.n_pixels * A.spp >= kTiledDualMinSamples;
     A.variant = ctx->cfg.kernel_variant != 0 ? ctx->cfg.kernel_variant
               : ctx->n_faces >= kTiledMinFaces ? (big_frame ? kTiledPoolVariant : 5)
               : (!jit_ok && ctx->n_faces > kTiledWideMinFaces && big_frame) ? kTiledPoolVariant
-              : (!jit_ok && (uint64_t)A.n_pixels * A.spp >= kWideMinSamples) ? 6 : kDefaultVariant;
+              : ((uint64_t)A.n_pixels * A.spp >= (jit_ok ? kSpecWideMinSamples : kWideMinSamples)) ? 6
+              : kDefaultVariant;
     A.accel = (ctx->cfg.accel == RVCP_ACCEL_BVH && ctx->n_faces > 0) ? RVCP_ACCEL_BVH : RVCP_ACCEL_NONE;
     if (A.accel == RVCP_ACCEL_BVH) A.variant = 3;    // the BVH traversal lives in the v3 kernels
     A.bvh_root = ctx->bvh_root;

@@ -59,6 +59,10 @@ constexpr int kMaxVariant = 10;
 constexpr int kTiledPoolVariant = 10;
 constexpr int variant_block(int v) { return v == kTiledPoolVariant ? kTiledPoolWaves * kWave : kBlock; }
 constexpr uint64_t kWideMinSamples = 8ull << 20;   // auto: variant 6 from 8 Msamples per frame
+// auto, scene-specialised scan: its 6-wave build (variant 6) from 256 Msamples per frame -- C4's
+// 2048^2 SPP=64 frame 23.39 -> 23.00 ms, while C3 (31 M) is 0.3 % and C2 6 % slower at 6 waves
+// (profiles/r04z_ab_waves6.log)
+constexpr uint64_t kSpecWideMinSamples = 256ull << 20;
 constexpr int kOccupancyBvh = 100;          // rvcp_games101_occupancy code of the BVH kernel
 #ifndef RVCP_TILE
 #define RVCP_TILE 256

@@ -178,6 +178,10 @@ def test_stats_report_schedule(cornell):
         assert int(rt.last_stats["kernel_variant"]) == 3 | spec      # 5 waves beats 6 here
         rt.render(64, 64, TIME)
         assert int(rt.last_stats["kernel_variant"]) == 3 | spec
+    with rvcp_amd.RayTracer(spp=64) as rt:          # C4's frame (>= 256 Msamples): 6 waves
+        rt.upload_scene(cornell)
+        rt.render(2048, 2048, TIME)
+        assert int(rt.last_stats["kernel_variant"]) == 6 | spec
     with rvcp_amd.RayTracer(spp=30, specialize=rvcp_amd.abi.SPECIALIZE_OFF) as rt:
         rt.upload_scene(cornell)
         rt.render(1024, 1024, TIME)
