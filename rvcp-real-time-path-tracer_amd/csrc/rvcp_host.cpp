@@ -79,6 +79,7 @@ struct rvcp_ctx {
     uint32_t n_faces = 0, n_lights = 0, n_mats = 0, n_verts = 0, n_spheres = 0;
     bool lights_same = false;      // every light record samples the same face
     bool rcp_fast = false;         // scan_rcp_fast_scene (FrameArgs::rcp_fast)
+    bool has_metal = false;        // a material of type 1 (FrameArgs::has_metal)
     // scene-specialised path kernels (rvcp_jit.cpp), or null: generic kernels
     std::shared_ptr<JitKernels> jit;
     std::string jit_err;
@@ -606,6 +607,9 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     ctx->n_faces = n_faces;
     ctx->n_verts = n_vertices;
     ctx->n_mats = n_materials;
+    ctx->has_metal = false;
+    for (uint32_t i = 0; i < n_materials; i++)
+        if (materials[i].ty == 1u) ctx->has_metal = true;
     ctx->n_lights = n_lum_face_ids;
     ctx->lights_same = n_lum_face_ids >= 1;
     for (uint32_t i = 1; i < n_lum_face_ids; i++)
@@ -688,6 +692,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     A.n_lights = ctx->n_lights;
     A.lights_same = ctx->lights_same ? 1u : 0u;
     A.rcp_fast = ctx->rcp_fast ? 1u : 0u;
+    A.has_metal = ctx->has_metal ? 1u : 0u;
     A.light_total = ctx->light_total;
     A.light_pdf = ctx->light_pdf;
     {   // :465-471: denom = max(0.1, pdf) * rr, pdf = 0.5 / 3.1415926 (cos > 0) or 0; IEEE 1/denom

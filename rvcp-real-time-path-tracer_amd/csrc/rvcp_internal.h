@@ -214,6 +214,8 @@ struct FrameArgs {
     // every triangle's scan denominator is +-0 or within [2^-126, 2^126] for rays passing
     // dir_fast_ok (scan_rcp_fast_scene): the generic scans may take 1/den without the class check
     uint32_t rcp_fast;
+    // the scene has a metal material (type 1): mode 2's scatter needs the reflected direction
+    uint32_t has_metal;
     uint32_t static_chunks;  // pixels handed out statically (one chunk per wave)
     uint32_t static_chunk;   // pixels of each wave's static chunk (<= kChunk)
     uint32_t n_simds;        // SIMDs of the device (CUs x 4), for static_split

@@ -2613,8 +2613,11 @@ __device__ __forceinline__ void legacy_body(
                     ior = M.refraction_ratio;
                 }
                 f3 dir = mk(0, 0, 0);
-                f3 refl = reflect_glsl(H_dir, H_nrm);                       // metal :526-527
-                if (dot(refl, H_nrm) < 0.0f) refl = neg(refl);
+                f3 refl = mk(0, 0, 0);
+                if (A.has_metal) {      // (only metal reads it; a scene-wide uniform test)
+                    refl = reflect_glsl(H_dir, H_nrm);                      // metal :526-527
+                    if (dot(refl, H_nrm) < 0.0f) refl = neg(refl);
+                }
                 bool pend = sc && (ty == 0u || ty == 1u);
                 while (__any(pend)) {
                     f3 p = mk(0, 0, 0);
