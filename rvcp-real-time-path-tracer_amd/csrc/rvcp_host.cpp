@@ -736,9 +736,10 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     std::vector<FrameArgs> FA;          // per frame of the batch (camera, time, pixel base)
     const uint32_t frame_px = A.n_pixels;
     const uint32_t split_px = frame_px * n_frames;          // the queue of the whole batch
-    if (n_frames > 1 && !trivial && legacy && frame_px > 0) {
-        // mode 2 has no pre-pass: its one kernel queues the batch's pixels frame after frame
-        // and reads each frame's camera and time from d_cams (FrameArgs::batch_cams)
+    // a batch's cameras and times in device memory: mode 2's one kernel and the pre-pass
+    // schedules' one pre-pass launch read them per frame
+    const bool cams = n_frames > 1 && !trivial && frame_px > 0 && (legacy || A.variant >= 3);
+    if (cams) {
         if (ctx->cap_cams < n_frames) {
             (void)hipFree(ctx->d_cams);
             (void)hipHostFree(ctx->h_cams);
@@ -764,6 +765,10 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
         }
         HIP_TRY(ctx, hipMemcpyAsync(ctx->d_cams, ctx->h_cams, (size_t)n_frames * 64,
                                     hipMemcpyHostToDevice, s));
+    }
+    if (cams && legacy) {
+        // mode 2 has no pre-pass: its one kernel queues the batch's pixels frame after frame
+        // and reads each frame's camera and time from d_cams (FrameArgs::batch_cams)
         A.batch_cams = ctx->d_cams;
         A.frame_pixels = frame_px;
         A.frame_stride = stride;
@@ -882,7 +887,9 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                                                  ctx->d_bvh_nodes, ctx->d_bvh_tris,
                                                  blocks, s, ctx->evm,
                                                  spec ? (void *)(A.variant == 6 ? jk->path6 : jk->path5)
-                                                      : nullptr);
+                                                      : nullptr,
+                                                 cams && frame_px <= kPrepassBatchMaxPixels
+                                                     ? ctx->d_cams : nullptr);
                 }
                 if (spec) ctx->last_spec = true;
             } else {

@@ -62,6 +62,11 @@ constexpr uint64_t kWideMinSamples = 8ull << 20;   // auto: variant 6 from 8 Msa
 // auto, scene-specialised scan: its 6-wave build (variant 6) from 256 Msamples per frame -- C4's
 // 2048^2 SPP=64 frame 23.39 -> 23.00 ms, while C3 (31 M) is 0.3 % and C2 6 % slower at 6 waves
 // (profiles/r04z_ab_waves6.log)
+// A batch's pre-passes run as one launch (one frame per grid row) for frames up to this many
+// pixels, whose per-frame pre-pass is too small to fill the GPU (C2: 0.1666 -> 0.1645 ms per
+// frame); larger frames keep one launch per frame (C3 at 60 frames: 2.810 vs 2.827 ms,
+// profiles/r04pb_ab_prebatch.log).
+constexpr uint32_t kPrepassBatchMaxPixels = 512u * 1024u;
 constexpr uint64_t kSpecWideMinSamples = 256ull << 20;
 constexpr int kOccupancyBvh = 100;          // rvcp_games101_occupancy code of the BVH kernel
 #ifndef RVCP_TILE
@@ -285,7 +290,7 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_frames, uint
                             rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
                             const rvcp::Bvh4Node *bvh_nodes, const rvcp::TriRecord *bvh_tris,
                             uint32_t grid_blocks, void *stream, void *main_event,
-                            void *spec_path_fn);
+                            void *spec_path_fn, const float *cams);
 // Integrator RVCP_INTEGRATOR_LEGACY (ray_tracer.comp): materials / spheres are the raw
 // rvcp_material_t / rvcp_sphere_t arrays, unorm_t the UNORM8 threshold table.
 int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,

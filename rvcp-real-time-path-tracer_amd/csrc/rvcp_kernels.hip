@@ -1454,11 +1454,16 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
     SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade,
-    const Bvh4Node *__restrict__ bvh_nodes, const TriRecord *__restrict__ bvh_tris)
+    const Bvh4Node *__restrict__ bvh_nodes, const TriRecord *__restrict__ bvh_tris,
+    const float *__restrict__ cams, uint32_t frame_stride)
 {
     __shared__ uint32_t block_count, block_base;
     const uint32_t lane = lane_id();
     const uint32_t pix = blockIdx.x * kPrimaryBlock + threadIdx.x;
+    // a batch's frames in one launch (cams != nullptr): frame blockIdx.y, its camera and time
+    // from the call's 16-float records, its outputs frame_stride pixels after the previous one's
+    const Cam C = cams ? cam_load(cams + 16u * blockIdx.y) : cam_of(A);
+    const uint32_t pix_base = A.pix_base + blockIdx.y * frame_stride;
     const bool live = pix < A.n_pixels;
     if (threadIdx.x == 0) block_count = 0;
     __syncthreads();
@@ -1470,7 +1475,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
         float tmin, tmax;
         f3 o, d;
         pixel_uv(A, pix, u_, v_);
-        primary_ray(A, u_, v_, o, d, tmin, tmax);
+        primary_ray(C, u_, v_, o, d, tmin, tmax);
         int best = -1;
         float bt = tmax;
         if (BVH) {
@@ -1496,7 +1501,7 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
             const f3 Ls = divs(L, (float)A.spp);
             f3 acc = mk(0, 0, 0);
             for (uint32_t i = 0; i < A.spp; ++i) acc = add(acc, Ls);
-            store_acc(A.pix_base + pix, acc, out_lin);
+            store_acc(pix_base + pix, acc, out_lin);
         } else {
             is_surf = true;
         }
@@ -1515,8 +1520,8 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     __syncthreads();
     if (is_surf) {
         SurfRecord r;
-        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.pix = A.pix_base + pix;
-        r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.seed = pixel_seed(A, u_, v_);
+        r.pos[0] = hpos.x; r.pos[1] = hpos.y; r.pos[2] = hpos.z; r.pix = pix_base + pix;
+        r.nrm[0] = hn.x; r.nrm[1] = hn.y; r.nrm[2] = hn.z; r.seed = pixel_seed(C, u_, v_);
         r.alb_pi[0] = halb.x; r.alb_pi[1] = halb.y; r.alb_pi[2] = halb.z; r.mat = hmat;
         surf[block_base + wave_off + rank_in(m)] = r;
     }
@@ -2919,16 +2924,25 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_f
                                        const rvcp::Bvh4Node *bvh_nodes,
                                        const rvcp::TriRecord *bvh_tris,
                                        uint32_t grid_blocks, void *stream, void *main_event,
-                                       void *spec_path_fn)
+                                       void *spec_path_fn, const float *cams)
 {
     const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
     auto pre = args->accel ? rvcp::games101_primary_kernel<true> : rvcp::games101_primary_kernel<false>;
-    // the frames' pre-passes append to one surface list (stream order: frame 0's pixels first)
-    for (uint32_t k = 0; k < n_frames; ++k)
-        hipLaunchKernelGGL(pre, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
-                           (hipStream_t)stream, args[k], tri, (const rvcp_face_t *)faces,
+    // the frames' pre-passes append to one surface list (the path kernel reads each record's
+    // pixel and seed, so the list's order is free): a batch with its cameras in device memory
+    // in one launch, one frame per grid row, else one launch per frame
+    if (cams && n_frames > 1)
+        hipLaunchKernelGGL(pre, dim3(pre_blocks, n_frames), dim3(rvcp::kPrimaryBlock), 0,
+                           (hipStream_t)stream, args[0], tri, (const rvcp_face_t *)faces,
                            (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,
-                           surf, shade, bvh_nodes, bvh_tris);
+                           surf, shade, bvh_nodes, bvh_tris, cams, frame_stride);
+    else
+        for (uint32_t k = 0; k < n_frames; ++k)
+            hipLaunchKernelGGL(pre, dim3(pre_blocks), dim3(rvcp::kPrimaryBlock), 0,
+                               (hipStream_t)stream, args[k], tri, (const rvcp_face_t *)faces,
+                               (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin,
+                               counters, surf, shade, bvh_nodes, bvh_tris, (const float *)nullptr,
+                               0u);
     if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
         return -2;
     if (spec_path_fn) {
