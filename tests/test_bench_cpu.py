@@ -33,16 +33,16 @@ def test_workloads_match_baseline_configs():
 
 def test_auto_pipeline():
     """Frames in flight, grid per frame and frames per launch: games101 on a
-    small scene (or the BVH) in batches of about 3 Mpixel and at least 2 frames (at most 16,
+    small scene (or the BVH) in batches of about 3 Mpixel (4 from 1-Mpixel frames) and at least 2 frames (at most 16,
     at most a quarter of the timed steps), 2 in flight; mode 2 up to 1.5 Mpixel 3 in flight on
     3 waves per SIMD; larger mode-2 frames and meshes the full grid, one frame per launch;
     never more contexts than the hardware queues minus one."""
     ap = bench.auto_pipeline
-    assert ap(1024 * 1024, 30, False, True, "4", "none", 20) == (2, 0, 3)          # C3
-    assert ap(1024 * 1024, 30, False, True, "4") == (2, 0, 3)
+    assert ap(1024 * 1024, 30, False, True, "4", "none", 20) == (2, 0, 4)          # C3
+    assert ap(1024 * 1024, 30, False, True, "4") == (2, 0, 4)
     assert ap(2048 * 256, 64, False, True, "4", "none", 40) == (2, 0, 6)           # C4, N=8 share
     assert ap(2048 * 256, 64, False, True, "4", "none", 20) == (2, 0, 5)
-    assert ap(2048 * 512, 64, False, True, "4", "none", 20) == (2, 0, 3)           # C4, N=4 share
+    assert ap(2048 * 512, 64, False, True, "4", "none", 20) == (2, 0, 4)           # C4, N=4 share
     assert ap(2048 * 1024, 64, False, True, "4", "none", 20) == (2, 0, 2)          # C4, N=2 share
     assert ap(2048 * 2048, 64, False, True, "4", "none", 20) == (2, 0, 2)          # C4, one GPU
     assert ap(2048 * 2048, 64, False, True, "4", "none", 4) == (2, 0, 1)           # 4 steps
@@ -55,9 +55,9 @@ def test_auto_pipeline():
     assert ap(384 * 384, 5, True, True, "8", "none", 20) == (4, 0, 1)              # small mode-2 frame
     assert ap(384 * 384, 5, True, True, "4", "none", 20) == (3, 0, 1)              # ... on 4 queues
     assert ap(1024 * 1024, 30, False, False, "4", "none", 20) == (2, 0, 1)         # C5 (mesh)
-    assert ap(1024 * 1024, 30, False, False, "4", "bvh", 20) == (2, 0, 3)          # C5 with the BVH
-    assert ap(1024 * 1024, 30, False, True, "2", "none", 20) == (1, 0, 3)
-    assert ap(1024 * 1024, 30, False, True, "x", "none", 20) == (2, 0, 3)
+    assert ap(1024 * 1024, 30, False, False, "4", "bvh", 20) == (2, 0, 4)          # C5 with the BVH
+    assert ap(1024 * 1024, 30, False, True, "2", "none", 20) == (1, 0, 4)
+    assert ap(1024 * 1024, 30, False, True, "x", "none", 20) == (2, 0, 4)
 
 
 def test_roofline_constants():
