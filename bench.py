@@ -339,8 +339,13 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
         frame 26.28-26.30 -> 26.13-26.15 ms;
       - runs with too few steps for a batch (fewer than 8): frames up to 1.5 Mpixel as mode 2
         below;
-      - mode 2 (no pre-pass, no batches), up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD --
-        mode 2 on the C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms;
+      - mode 2 (no pre-pass), up to 1.5 Mpixel and at least 16 Msamples per frame: batches of
+        up to 8 frames (at most a quarter of the timed steps), 2 in flight, full grid -- round 4,
+        mode 2 on the C3 frame 1.667 -> 1.595 ms at 40 frames, 1.710 -> 1.633 ms at 20 with 5
+        (profiles/r04m2p2_ab_m2pipe2.log);
+      - other mode-2 frames up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD -- mode 2 on the
+        C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms (round 4: batches of 4 / 8 for
+        the sphere room 0.2654 / 0.2621 vs 0.2544 ms, r04m2p_ab_m2pipe.log);
       - larger mode-2 frames and meshes: full grid, one frame per launch, 2 in flight (3 in
         mode 2: one kernel per frame, no pre-pass);
       - other small frames (below 4 Msamples): 4 in flight (C2 0.59/0.32/0.27/0.33 ms for
@@ -357,6 +362,10 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
             fif, grid = 3, 3        # too few steps for batches: single frames, smaller grid
     elif pixels * spp < (4 << 20):
         fif, grid, batch = 4, 0, 1
+    elif (legacy and small_scene and pixels <= 1536 * 1024 and pixels * spp >= (16 << 20)
+          and (steps == 0 or steps >= 8)):
+        # mode 2 with long pixel chains (the C3 frame): batches of up to 8 frames, 2 in flight
+        fif, grid, batch = 2, 0, min(8, steps // 4 if steps else 8)
     elif small_scene and pixels <= 1536 * 1024:
         fif, grid, batch = 3, 3, 1
     else:

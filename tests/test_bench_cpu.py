@@ -34,8 +34,9 @@ def test_workloads_match_baseline_configs():
 def test_auto_pipeline():
     """Frames in flight, grid per frame and frames per launch: games101 on a
     small scene (or the BVH) in batches of about 3 Mpixel (4 from 1-Mpixel frames) and at least 2 frames (at most 16,
-    at most a quarter of the timed steps), 2 in flight; mode 2 up to 1.5 Mpixel 3 in flight on
-    3 waves per SIMD; larger mode-2 frames and meshes the full grid, one frame per launch;
+    at most a quarter of the timed steps), 2 in flight; mode 2 up to 1.5 Mpixel with at least 16
+    Msamples per frame in batches of up to 8, 2 in flight, other mode-2 frames up to 1.5 Mpixel
+    3 in flight on 3 waves per SIMD; larger mode-2 frames and meshes the full grid, one frame per launch;
     never more contexts than the hardware queues minus one."""
     ap = bench.auto_pipeline
     assert ap(1024 * 1024, 30, False, True, "4", "none", 20) == (2, 0, 4)          # C3
@@ -50,7 +51,9 @@ def test_auto_pipeline():
     assert ap(384 * 384, 10, False, True, "4", "none", 20) == (2, 0, 5)
     assert ap(384 * 384, 10, False, True, "4", "none", 3) == (3, 3, 1)             # too few steps
     assert ap(1024 * 1024, 30, False, True, "4", "none", 5) == (3, 3, 1)
-    assert ap(1024 * 1024, 30, True, True, "4", "none", 20) == (3, 3, 1)           # mode 2, C3 frame
+    assert ap(1024 * 1024, 30, True, True, "4", "none", 20) == (2, 0, 5)           # mode 2, C3 frame
+    assert ap(1024 * 1024, 30, True, True, "4", "none", 40) == (2, 0, 8)
+    assert ap(1024 * 1024, 30, True, True, "4", "none", 5) == (3, 3, 1)            # too few steps
     assert ap(1024 * 1024, 5, True, True, "4", "none", 20) == (3, 3, 1)            # sphere room
     assert ap(384 * 384, 5, True, True, "8", "none", 20) == (4, 0, 1)              # small mode-2 frame
     assert ap(384 * 384, 5, True, True, "4", "none", 20) == (3, 0, 1)              # ... on 4 queues
