@@ -325,7 +325,8 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
     grid per frame with a third frame beside it, whose waves start in the tail:
       - games101, brute-force scan of a small scene or the opt-in BVH, up to 1.5 Mpixel or
         below 4 Msamples: batches of about 3 Mpixel, 4 Mpixel for frames of 1 Mpixel and more
-        (at most 16 frames, and at most a quarter of the timed steps), 2 in flight.  Round 4
+        (at most 32 frames -- 16 before round 4, C2 0.1652 -> 0.1606 / 0.1596 ms with 20 / 25,
+        r04c2b2_ab_c2batch2.log -- and at most a quarter of the timed steps), 2 in flight.  Round 4
         (profiles/r04b20b_ab_b20b.log, r04shb_ab_share_b.log, r04c5b_ab_c5b.log): C3 2.910 ->
         2.871 ms at 20 frames and 2.819 -> 2.799 at 60 with 4 frames instead of 3, the N=4
         share 5.990 -> 5.961 ms, C5 with the BVH 70.32 -> 69.21 ms; the N=8 share keeps 6
@@ -353,10 +354,10 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
     Contexts beyond the hardware queues minus one contend for queues."""
     if not legacy and (small_scene or accel == "bvh"):
         # about 3 Mpixel per launch (4 for frames of 1 Mpixel and more) and at least 2 frames,
-        # at most 16 frames, and at least 4 launches in the run
+        # at most 32 frames, and at least 4 launches in the run
         per_launch = (4 if pixels >= 1024 * 1024 else 3) * 1024 * 1024
-        batch = max(1, min(max(2, -(-per_launch // max(1, pixels))), 16,
-                           steps // 4 if steps else 16))
+        batch = max(1, min(max(2, -(-per_launch // max(1, pixels))), 32,
+                           steps // 4 if steps else 32))
         fif, grid = 2, 0
         if batch == 1 and pixels <= 1536 * 1024:
             fif, grid = 3, 3        # too few steps for batches: single frames, smaller grid

@@ -33,7 +33,7 @@ def test_workloads_match_baseline_configs():
 
 def test_auto_pipeline():
     """Frames in flight, grid per frame and frames per launch: games101 on a
-    small scene (or the BVH) in batches of about 3 Mpixel (4 from 1-Mpixel frames) and at least 2 frames (at most 16,
+    small scene (or the BVH) in batches of about 3 Mpixel (4 from 1-Mpixel frames) and at least 2 frames (at most 32,
     at most a quarter of the timed steps), 2 in flight; mode 2 up to 1.5 Mpixel with at least 16
     Msamples per frame in batches of up to 8, 2 in flight, other mode-2 frames up to 1.5 Mpixel
     3 in flight on 3 waves per SIMD; larger mode-2 frames and meshes the full grid, one frame per launch;
@@ -47,7 +47,9 @@ def test_auto_pipeline():
     assert ap(2048 * 1024, 64, False, True, "4", "none", 20) == (2, 0, 2)          # C4, N=2 share
     assert ap(2048 * 2048, 64, False, True, "4", "none", 20) == (2, 0, 2)          # C4, one GPU
     assert ap(2048 * 2048, 64, False, True, "4", "none", 4) == (2, 0, 1)           # 4 steps
-    assert ap(384 * 384, 10, False, True, "4", "none", 200) == (2, 0, 16)          # C2
+    assert ap(384 * 384, 10, False, True, "4", "none", 200) == (2, 0, 22)          # C2
+    assert ap(384 * 384, 10, False, True, "4", "none", 100) == (2, 0, 22)
+    assert ap(256 * 256, 10, False, True, "4", "none", 400) == (2, 0, 32)
     assert ap(384 * 384, 10, False, True, "4", "none", 20) == (2, 0, 5)
     assert ap(384 * 384, 10, False, True, "4", "none", 3) == (3, 3, 1)             # too few steps
     assert ap(1024 * 1024, 30, False, True, "4", "none", 5) == (3, 3, 1)
