@@ -25,6 +25,9 @@ Workloads (per BASELINE.json configs; the N=1 default is the headline C3):
       BASELINE.json 8-GPU config and the default for N>1.  Rank 0 also renders the same frame
       alone after the timed region (bit-exactness check, and `one_gpu_ms` for the speedup).
   c5: Cornell + 100k random triangles, 1024x1024 SPP=30.
+  c6: Cornell + 310 random triangles (342 faces, 998 vertices: the largest unshared-vertex
+      scene within the reference's own 1000-vertex / 1000-face buffers,
+      ray_tracer_games101_branch.comp:18-19), 1024x1024 SPP=30.
   spheres: integrator mode 2 (ray_tracer.comp) on the deprecated host's sphere room,
       1024x1024 at its SPP=5 (not a BASELINE config; reported for coverage).
   c3m2: the C3 frame (Cornell 1024x1024 SPP=30) through integrator mode 2 (ray_tracer.comp,
@@ -81,6 +84,7 @@ N_SIMDS = 1024
 VALU_ISSUE_PER_CLK = 0.5
 SHADER_CLOCK_GHZ = 2.29
 FLOP_PER_TEST = 52
+C6_EXTRA_TRIS = 310            # Cornell + 310 = 342 faces, 998 vertices (workload c6)
 # the time seed of frame 0 (the tests' fixed seed); frame f renders with
 # TIME0 + f, as the reference re-stamps `time` every frame (vulkan.rs:418-421)
 TIME0 = 123.0
@@ -119,6 +123,12 @@ def workload(name, n_gpus):
     if name == "c5":
         return dict(workload="cornell_plus_100k_tris_1024sq_spp30", W=1024, H=1024, spp=30,
                     extra_tris=100000, scaling="strong")
+    if name == "c6":
+        # the largest unshared-vertex scene the reference itself can load: its shader caps the
+        # buffers at 1000 vertices and 1000 faces (ray_tracer_games101_branch.comp:18-19), so
+        # Cornell (68 vertices) + 310 random triangles (930) = 998 vertices, 342 faces
+        return dict(workload="cornell_plus_310_tris_1024sq_spp30", W=1024, H=1024, spp=30,
+                    extra_tris=C6_EXTRA_TRIS, scaling="strong")
     if name == "spheres":
         return dict(workload="spheres_mode2_1024sq_spp5", W=1024, H=1024, spp=5, extra_tris=0,
                     scaling="strong", integrator=1, scene="spheres")
@@ -273,9 +283,11 @@ def negotiate_gather(dist, rank, n_comms, make_id, init_comm, probe_render=None,
        rank enters the collective gather while another rank's render already failed (its
        peers would wait in the gather forever);
     4. `probe_gather()` (the tiny frame's RCCL gather + rank 0's check); agreed.
-    Any failure on any rank sends every rank to the host gather, with the reasons.  (A rank
-    whose ncclCommInitRank fails while the others succeed leaves them blocked inside RCCL
-    itself; such asymmetric init failures are outside what a blocking init can recover.)
+    Any failure on any rank sends every rank to the host gather, with the reasons.  The
+    communicator is created non-blocking and polled against a deadline (rvcp_rccl_init,
+    rvcp_rccl_set_timeout), and so is every gather wait: when one rank's init fails at once,
+    its peers' inits end with RVCP_E_TIMEOUT instead of waiting inside RCCL, and the all-gather
+    of step 2 sees every rank's outcome.
     Returns ("rccl", None) or ("host", reason)."""
     ids, why = None, None
     try:
@@ -378,6 +390,66 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
     return fif, grid, batch
 
 
+class CallSchedule:
+    """The bench's call schedule: `n` frames as calls of `batch` frames
+    (the last one shorter) dealt round-robin to `fif` contexts; a context holds one call at a
+    time (rvcp.h), so call c waits, before its enqueue, for the call its context ran `fif`
+    calls earlier.  Frame f of the whole run (warm-up frames first) renders with the time seed
+    TIME0 + f.  `run(n)` returns the stats of every call it made, each exactly once, in
+    completion order; `slot_time[i][j]` is the seed of the frame in context i's slot j and
+    `done_t` the (host time, frames) of each completed call of the last run.
+
+    enqueue(i, pushes, nb) starts a call of nb frames on context i; finish(i, nb) waits for it
+    and returns its stats.  Pure host logic: tests/test_bench_cpu.py drives it with a stub."""
+
+    def __init__(self, fif, batch, enqueue, finish, push_of, clock=time.perf_counter):
+        assert fif >= 1 and batch >= 1
+        self.fif, self.batch = fif, batch
+        self._enqueue, self._finish, self._push_of, self._clock = enqueue, finish, push_of, clock
+        self.pending = [0] * fif            # frames of the call in flight on each context
+        self.frames_run = 0                 # frames enqueued so far (the next frame's index)
+        self.slot_time = [[None] * batch for _ in range(fif)]
+        self.done_t = []
+
+    def calls(self, n):
+        """n frames as calls of `batch` frames (the last one shorter)."""
+        return [self.batch] * (n // self.batch) + ([n % self.batch] if n % self.batch else [])
+
+    def _finish_ctx(self, i):
+        nb, self.pending[i] = self.pending[i], 0
+        st = self._finish(i, nb)
+        self.done_t.append((self._clock(), nb))
+        return st
+
+    def run(self, n):
+        """Render n frames; returns the stats of each call (all of them, drained)."""
+        self.done_t = []
+        stats = []
+        for c, nb in enumerate(self.calls(n)):
+            i = c % self.fif
+            if self.pending[i]:
+                stats.append(self._finish_ctx(i))
+            ts = [TIME0 + float(self.frames_run + j) for j in range(nb)]
+            self.frames_run += nb
+            self.slot_time[i][:nb] = ts
+            self._enqueue(i, [self._push_of(t) for t in ts], nb)
+            self.pending[i] = nb
+        stats += [self._finish_ctx(i) for i in range(self.fif) if self.pending[i]]
+        return stats
+
+
+def report_failure(rank, world, wl, stage, err):
+    """A rank's library error during the run (e.g. RVCP_E_TIMEOUT from a gather whose peer never
+    came): one labelled JSON line on stdout (rank 0: the line the driver reads; other ranks: the
+    same record), naming the rank and the stage, before the non-zero exit."""
+    rec = {"metric": metric_name(wl, world), "value": None, "unit": "Msamples/s",
+           "n_gpus": world, "higher_is_better": True,
+           "error": {"rank": rank, "stage": stage, "code": getattr(err, "code", None),
+                     "message": str(err)}}
+    print(json.dumps(rec), flush=True, file=sys.stdout if rank == 0 else sys.stderr)
+    return rec
+
+
 def free_port():
     """A TCP port on 127.0.0.1 that is free right now (for the ranks' rendezvous)."""
     import socket
@@ -409,7 +481,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "spheres", "c3m2", "c3rot", "c3gen"],
+    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "c6", "spheres", "c3m2", "c3rot", "c3gen"],
                     help="default: c3 at N=1 (headline), c4 at N>1 (BASELINE's 8-GPU config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -430,6 +502,11 @@ def main():
                     help="rvcp_config_t.grid_waves_per_simd: the path kernel's persistent grid "
                          "per frame in waves per SIMD (0 = every resident slot; -1 = auto, "
                          "chosen with the frames in flight)")
+    ap.add_argument("--comm-timeout-ms", type=int, default=60000,
+                    help="N>1: deadline of the RCCL communicator's creation and of each gather "
+                         "wait (rvcp_rccl_set_timeout); past it the rank aborts its communicator "
+                         "-- at creation every rank then takes the labelled host gather, during "
+                         "the run the command exits non-zero with a line naming rank and stage")
     ap.add_argument("--launch-pass", type=int, default=10,
                     help="frames (at most --steps) of the post-timing one-frame-in-flight pass "
                          "that measures the path kernel's isolated launch time "
@@ -469,7 +546,11 @@ def main():
         # control plane only (barriers, the max-over-ranks time, the RCCL ids, agreement on
         # the gather mode); the frame itself moves over RCCL inside librvcp
         # (rvcp_gather_frame_async)
-        dist.init_process_group("gloo")
+        # (a bounded control plane too: a rank that died leaves its peers' gloo calls waiting
+        # this long at most, torch.distributed.run ending them sooner)
+        import datetime
+        dist.init_process_group("gloo", timeout=datetime.timedelta(
+            seconds=max(300, 3 * args.comm_timeout_ms // 1000)))
 
     wname = args.workload or ("c3" if world == 1 else "c4")
     wl = workload(wname, world)
@@ -566,34 +647,26 @@ def main():
                     if not torch.equal(ref, p_frame):
                         raise RuntimeError("probe frame differs from the 1-rank render")
             torch.cuda.synchronize()
+        def init_comm(i, uid):
+            # non-blocking creation polled against the deadline: a peer that never joins
+            # gives RVCP_E_TIMEOUT here (communicator aborted), not a rank blocked in RCCL
+            rts[i].rccl_set_timeout(args.comm_timeout_ms)
+            rts[i].rccl_init(uid, world, rank)
         gather_mode, gather_error = negotiate_gather(
-            dist, rank, fif, rvcp_amd.rccl_unique_id,
-            lambda i, uid: rts[i].rccl_init(uid, world, rank), probe_render, probe_gather)
+            dist, rank, fif, rvcp_amd.rccl_unique_id, init_comm, probe_render, probe_gather)
     host_gather = world > 1 and gather_mode != "rccl"
     torch.cuda.synchronize()
-    pending = [0] * fif                 # frames in flight on each context
-    gather_ms = []
     # Every frame has its own time seed, as the reference re-stamps `time` in the push
     # constant of every frame it submits (vulkan.rs:418-421): frame f (warm-up frames first,
     # then the timed ones, the same numbering on every rank) renders with time TIME0 + f, so
-    # no two frames of the run share an RNG stream.  slot_time[i][j]: the seed of the frame in
-    # context i's output slot j.
-    n_frames_run = [0]
-    slot_time = [[None] * batch for _ in range(fif)]
-    done_t = []                         # (host time a call's frames were complete, frames)
+    # no two frames of the run share an RNG stream.
+    gather_ms = []
 
-    def next_pushes(i, nb):
-        ts_ = [TIME0 + float(n_frames_run[0] + j) for j in range(nb)]
-        n_frames_run[0] += nb
-        slot_time[i][:nb] = ts_
-        return [sc.push_constant(t) for t in ts_]
-
-    def enqueue(i, nb):
+    def enqueue(i, pushes, nb):
         """Enqueue nb frames (one call) on context i's own stream (stream 0 = its stream)."""
         r, shard_buf, gat_flat = rts[i], shard_bufs[i], gat_flats[i]
         out = frames[i] if world == 1 else shard_buf
         k, n = (0, 1) if world == 1 else (rank, world)
-        pushes = next_pushes(i, nb)
         if batch == 1:
             r.render_shard_async(pushes[0], W, H, k, n, out.data_ptr())
         else:
@@ -607,10 +680,9 @@ def main():
                                  gat_flat.data_ptr() if rank == 0 else 0,
                                  frames[i][j].data_ptr() if rank == 0 else 0)
 
-    def finish(i):
-        """Wait for context i's frames; return their stats (one entry per call)."""
+    def finish(i, nb):
+        """Wait for context i's call of nb frames; return its stats."""
         st = rts[i].sync_stats()
-        nb, pending[i] = pending[i], 0
         if world > 1 and not host_gather:
             gather_ms.append(rts[i].gather_wait()[0])
         if host_gather:    # gloo gather through host memory (rehearsal / no usable RCCL)
@@ -621,23 +693,9 @@ def main():
                     rts[i].assemble_frame_async(gat_flats[i].data_ptr(), slot, W, H, world,
                                                 frames[i][j].data_ptr())
                     torch.cuda.synchronize()
-        done_t.append((time.perf_counter(), nb))
         return st
 
-    def step(c, nb):
-        """Call c (nb frames): returns the stats of the call it waited for (or None)."""
-        i = c % fif
-        st = finish(i) if pending[i] else None
-        enqueue(i, nb)
-        pending[i] = nb
-        return st
-
-    def drain():
-        return [finish(i) for i in range(fif) if pending[i]]
-
-    def calls(n):
-        """n frames as calls of `batch` frames (the last one shorter)."""
-        return [batch] * (n // batch) + ([n % batch] if n % batch else [])
+    sched = CallSchedule(fif, batch, enqueue, finish, lambda t: sc.push_constant(t))
 
     # Warm-up: at least one full batch on every context, so that each context's surface list,
     # accumulator and camera buffers have their full size before timing (growing one inside the
@@ -645,42 +703,46 @@ def main():
     # context's frames)
     warm = max(args.warmup, fif * batch)
     warm = -(-warm // batch) * batch
-    for c, nb in enumerate(calls(warm)):
-        step(c, nb)
-    drain()
-    gather_ms.clear()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stats = []
-    t0 = time.perf_counter()
-    done_t.clear()
-    done_t.append((t0, 0))
-    for c, nb in enumerate(calls(args.steps)):
-        st = step(c, nb)
-        if st is not None:
-            stats.append(st)
-    stats += drain()
-    # (a copy: the post-timing passes below render into the same buffers)
-    frame = frames[0][0].clone() if rank == 0 else None
-    frame_time = slot_time[0][0]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    stage = ["warm-up frames"]
+    try:
+        sched.run(warm)
+        gather_ms.clear()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        stage[0] = "timed frames"
+        t0 = time.perf_counter()
+        stats = sched.run(args.steps)
+        # (a copy: the post-timing passes below render into the same buffers)
+        frame = frames[0][0].clone() if rank == 0 else None
+        frame_time = sched.slot_time[0][0]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    except rvcp_amd.abi.RvcpError as e:
+        # a gather that timed out (a peer rank missing or failed: RVCP_E_TIMEOUT, the
+        # communicator aborted) or any other library error: a labelled line and a non-zero exit
+        # instead of a hang; torch.distributed.run then ends the other ranks
+        report_failure(rank, world, wl, stage[0], e)
+        raise SystemExit(3)
     kernel_ms = [float(st["kernel_ms"]) for st in stats]
     main_ms = [float(st["main_kernel_ms"]) for st in stats]
     trav = sum(int(st["traversals"]) for st in stats)
     trav_exec = sum(int(st["traversals_executed"]) for st in stats)
     variant = int(stats[-1]["kernel_variant"])
-    assert sum(int(st["samples"]) for st in stats) == args.steps * W * rows * spp
+    # every timed frame rendered exactly once (CallSchedule; tests/test_bench_cpu.py sweeps
+    # steps x batch x frames in flight against a stub)
+    assert sum(int(st["samples"]) for st in stats) == args.steps * W * rows * spp, \
+        (len(stats), [int(st["samples"]) for st in stats], args.steps, batch, fif)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    done_t = [(t0, 0)] + sched.done_t
     intervals = [(b[0] - a[0]) * 1000.0 / b[1] for a, b in zip(done_t, done_t[1:]) if b[1]]
     samples_total = W * H * spp * args.steps
     value = samples_total / elapsed / 1e6

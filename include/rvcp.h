@@ -262,6 +262,9 @@ typedef struct rvcp_ctx rvcp_ctx_t;
 #define RVCP_E_UNSUPPORTED  (-4)
 #define RVCP_E_NOMEM        (-5)   /* host or device allocation failed */
 #define RVCP_E_INTERNAL     (-6)   /* unexpected internal error (caught at the ABI boundary) */
+#define RVCP_E_TIMEOUT      (-7)   /* a collective did not complete within the deadline
+                                    * (rvcp_rccl_set_timeout): a peer rank is missing or failed;
+                                    * the context's own communicator has been aborted */
 
 /* ---------------------------------------------------------------------------------------
  * Entry points
@@ -368,7 +371,9 @@ int rvcp_render_frames_async(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes
                              uint32_t shard_index, uint32_t shard_count,
                              void *d_rgba8, void *d_linear_rgb, void *stream);
 
-/* Wait for the last async render of ctx and fetch its statistics. */
+/* Wait for the last async render of ctx and fetch its statistics.  It waits for the render
+ * only: a gather enqueued behind it (rvcp_gather_frame_async) needs rvcp_gather_wait before
+ * rank 0's assembled frame may be read. */
 int rvcp_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats);
 
 /* The asynchronous pair of SURVEY.md §8(b) (the reference's per-image fences,
@@ -409,10 +414,20 @@ int rvcp_assemble_frame_async(rvcp_ctx_t *ctx, const void *d_gathered, uint32_t 
  * out-of-band channel (MPI, a TCP store, torch.distributed's broadcast). */
 int rvcp_rccl_unique_id(uint8_t out_id[RVCP_RCCL_ID_BYTES]);
 
-/* Every rank, collectively: create ctx's communicator (ncclCommInitRank on ctx's device).
- * Blocks until all `world` ranks have joined.  Destroyed with the context. */
+/* Every rank, collectively: create ctx's communicator (non-blocking ncclCommInitRankConfig on
+ * ctx's device, polled with ncclCommGetAsyncError).  Returns once all `world` ranks have
+ * joined, or RVCP_E_TIMEOUT when they have not within the context's deadline (the half-made
+ * communicator is aborted with ncclCommAbort; the context stays usable and may try again).
+ * Destroyed with the context.  The reference has no counterpart (single device); its own
+ * recover-not-hang path is the swapchain's OutOfDate -> recreate (src/ray_tracer/vulkan.rs:
+ * 355-364). */
 int rvcp_rccl_init(rvcp_ctx_t *ctx, const uint8_t id[RVCP_RCCL_ID_BYTES], uint32_t world,
                    uint32_t rank);
+
+/* Deadline of rvcp_rccl_init and rvcp_gather_wait (and of the wait for a pending gather in
+ * rvcp_destroy), in milliseconds; 0 = wait forever.  Default 60000.  It must exceed the
+ * render time of the frames a gather waits behind. */
+int rvcp_rccl_set_timeout(rvcp_ctx_t *ctx, uint32_t timeout_ms);
 
 /* Use the caller's existing communicator (an ncclComm_t over ctx's device, rank `rank` of
  * `world`) instead; the caller keeps ownership. */
@@ -434,7 +449,13 @@ int rvcp_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, uint32_t
 /* Wait for ctx's last rvcp_gather_frame_async and report its device time (ncclGather plus, on
  * rank 0, the assembly) in *gather_ms and, if frame_ms is not NULL, the time from the start of
  * the preceding render to the end of the gather in *frame_ms (HIP events on the gather's
- * stream).  RVCP_E_INVALID when no gather was enqueued since the last call. */
+ * stream).  RVCP_E_INVALID when no gather was enqueued since the last call.  The wait polls
+ * against the context's deadline (rvcp_rccl_set_timeout): when the gather has not finished by
+ * then -- a peer rank never entered it -- or RCCL reports an asynchronous error, the
+ * context's communicator is aborted (ncclCommAbort; its kernels exit) and RVCP_E_TIMEOUT
+ * (resp. RVCP_E_HIP) is returned; rvcp_rccl_init may then build a new one.
+ * rvcp_sync_stats / rvcp_wait wait for the render only: rank 0's assembled frame (d_frame)
+ * is complete after this call, not after theirs. */
 int rvcp_gather_wait(rvcp_ctx_t *ctx, float *gather_ms, float *frame_ms);
 
 #ifdef __cplusplus

@@ -43,7 +43,7 @@ DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop
 
 # Error codes
 RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E_NOMEM, \
-    RVCP_E_INTERNAL = 0, -1, -2, -3, -4, -5, -6
+    RVCP_E_INTERNAL, RVCP_E_TIMEOUT = 0, -1, -2, -3, -4, -5, -6, -7
 RCCL_ID_BYTES = 128
 
 EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "rvcp_create",
@@ -51,7 +51,7 @@ EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "r
             "rvcp_sync_stats", "rvcp_shard_rows", "rvcp_assemble_frame_async",
             "rvcp_upload_scene_file", "rvcp_mandelbrot", "rvcp_render_async", "rvcp_wait",
             "rvcp_rccl_unique_id", "rvcp_rccl_init", "rvcp_rccl_attach", "rvcp_gather_frame_async",
-            "rvcp_gather_wait", "rvcp_render_frames_async"]
+            "rvcp_gather_wait", "rvcp_render_frames_async", "rvcp_rccl_set_timeout"]
 
 
 # Integrator mode 2 (ray_tracer.comp ray_trace): its own #defines (ray_tracer.comp:5-13).
@@ -138,6 +138,7 @@ def load():
     L.rvcp_rccl_unique_id.argtypes = [P]
     L.rvcp_rccl_init.argtypes = [P, P, u32, u32]
     L.rvcp_rccl_attach.argtypes = [P, P, u32, u32]
+    L.rvcp_rccl_set_timeout.argtypes = [P, u32]
     L.rvcp_gather_frame_async.argtypes = [P, P, u32, u32, P, P, P]
     L.rvcp_gather_wait.argtypes = [P, P, P]
     for name in ("rvcp_config_default", "rvcp_config_default_for", "rvcp_create", "rvcp_destroy", "rvcp_upload_scene",
@@ -145,7 +146,7 @@ def load():
                  "rvcp_assemble_frame_async", "rvcp_upload_scene_file", "rvcp_mandelbrot",
                  "rvcp_render_async", "rvcp_wait", "rvcp_rccl_unique_id", "rvcp_rccl_init",
                  "rvcp_rccl_attach", "rvcp_gather_frame_async", "rvcp_gather_wait",
-                 "rvcp_render_frames_async"):
+                 "rvcp_render_frames_async", "rvcp_rccl_set_timeout"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -14,11 +14,13 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <exception>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rvcp.h"
@@ -37,6 +39,12 @@ using namespace rvcp;
 #else
 #define RVCP_KNOB(name) ((const char *)nullptr)
 #endif
+
+// rvcp_rccl_init / rvcp_gather_wait give up after this long unless rvcp_rccl_set_timeout says
+// otherwise: far above a frame (C5 brute force, the slowest workload, 6.5 s) and far below
+// "forever", which is what a blocking ncclCommInitRank or an unbounded event wait gives when a
+// peer never arrives
+constexpr uint32_t kDefaultCommTimeoutMs = 60000;
 
 struct rvcp_ctx {
     rvcp_config_t cfg{};
@@ -120,6 +128,8 @@ struct rvcp_ctx {
     ncclComm_t comm = nullptr;
     bool comm_owned = false;
     uint32_t comm_world = 0, comm_rank = 0;
+    // deadline of rvcp_rccl_init and rvcp_gather_wait (rvcp_rccl_set_timeout; 0 = none)
+    uint32_t comm_timeout_ms = kDefaultCommTimeoutMs;
 
     // last launch
     bool pending = false;
@@ -151,6 +161,12 @@ int fail(rvcp_ctx *ctx, int code, const std::string &msg)
 struct RcclApi {
     ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
     ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    // non-blocking creation, abort and the communicator's asynchronous state: what makes a
+    // missing or failed peer a timeout instead of a hang (rccl.h: ncclCommInitRankConfig,
+    // ncclCommAbort, ncclCommGetAsyncError; present in every RCCL >= 2.14)
+    ncclResult_t (*comm_init_rank_config)(ncclComm_t *, int, ncclUniqueId, int, ncclConfig_t *) = nullptr;
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+    ncclResult_t (*get_async_error)(ncclComm_t, ncclResult_t *) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*gather)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t,
                            hipStream_t) = nullptr;
@@ -172,12 +188,18 @@ const RcclApi &rccl_api()
         }
         api.get_unique_id = (decltype(api.get_unique_id))dlsym(h, "ncclGetUniqueId");
         api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        api.comm_init_rank_config = (decltype(api.comm_init_rank_config))dlsym(h, "ncclCommInitRankConfig");
+        api.comm_abort = (decltype(api.comm_abort))dlsym(h, "ncclCommAbort");
+        api.get_async_error = (decltype(api.get_async_error))dlsym(h, "ncclCommGetAsyncError");
         api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
         api.gather = (decltype(api.gather))dlsym(h, "ncclGather");
         api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
-        api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.gather &&
+        api.ok = api.get_unique_id && api.comm_init_rank && api.comm_init_rank_config &&
+                 api.comm_abort && api.get_async_error && api.comm_destroy && api.gather &&
                  api.error_string;
-        if (!api.ok) api.why = "librccl.so.1 lacks ncclGather / ncclCommInitRank";
+        if (!api.ok)
+            api.why = "librccl.so.1 lacks ncclGather / ncclCommInitRankConfig / ncclCommAbort / "
+                      "ncclCommGetAsyncError";
     });
     return api;
 }
@@ -262,6 +284,10 @@ void free_scene(rvcp_ctx *ctx)
 }
 
 }  // namespace
+
+using Clock = std::chrono::steady_clock;
+static void abort_comm(rvcp_ctx_t *ctx);
+static int wait_gather_done(rvcp_ctx_t *ctx);
 
 extern "C" {
 
@@ -455,7 +481,11 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     (void)hipSetDevice(ctx->device);
     // a frame still in flight (possibly on the caller's stream) reads the buffers freed below
     if (ctx->pending && ctx->ev1) (void)hipEventSynchronize(ctx->ev1);
-    if (ctx->gather_pending && ctx->evg1) (void)hipEventSynchronize(ctx->evg1);
+    // (a gather still pending is waited for with the deadline: a peer that never came must not
+    // hang the destroy; on expiry the communicator is aborted)
+    if (ctx->gather_pending && ctx->evg1 && wait_gather_done(ctx) == RVCP_OK)
+        ctx->gather_pending = false;
+    if (ctx->gather_pending) abort_comm(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm && ctx->comm_owned) (void)rccl_api().comm_destroy(ctx->comm);
     ctx->comm = nullptr;
@@ -1202,6 +1232,43 @@ static int impl_rccl_unique_id(uint8_t *out_id)
     return RVCP_OK;
 }
 
+static Clock::time_point comm_deadline(const rvcp_ctx_t *ctx)
+{
+    return ctx->comm_timeout_ms ? Clock::now() + std::chrono::milliseconds(ctx->comm_timeout_ms)
+                                : Clock::time_point::max();
+}
+
+// Abort ctx's communicator (ours) after a deadline or an asynchronous error: ncclCommAbort
+// raises RCCL's abort flag, which its kernels poll in every wait loop, so a gather stuck on a
+// peer that never comes finishes and the streams drain; the context stays usable for
+// single-GPU renders.  A caller's communicator (rvcp_rccl_attach) is the caller's to abort.
+static void abort_comm(rvcp_ctx_t *ctx)
+{
+    if (ctx->comm && ctx->comm_owned) (void)rccl_api().comm_abort(ctx->comm);
+    if (ctx->comm_owned) ctx->comm = nullptr;
+}
+
+// Wait until a non-blocking communicator has finished its last call (ncclInProgress ->
+// ncclSuccess), bounded by `deadline`.  RVCP_E_TIMEOUT on expiry, RVCP_E_HIP on an RCCL error.
+static int wait_comm_ready(rvcp_ctx_t *ctx, ncclComm_t comm, Clock::time_point deadline,
+                    const char *what)
+{
+    const RcclApi &R = rccl_api();
+    for (unsigned spin = 0;; spin++) {
+        ncclResult_t st = ncclInProgress;
+        const ncclResult_t r = R.get_async_error(comm, &st);
+        if (r != ncclSuccess)
+            return fail(ctx, RVCP_E_HIP, std::string(what) + ": ncclCommGetAsyncError: " + R.error_string(r));
+        if (st == ncclSuccess) return RVCP_OK;
+        if (st != ncclInProgress)
+            return fail(ctx, RVCP_E_HIP, std::string(what) + ": " + R.error_string(st));
+        if (Clock::now() >= deadline)
+            return fail(ctx, RVCP_E_TIMEOUT, std::string(what) + ": no progress within " +
+                        std::to_string(ctx->comm_timeout_ms) + " ms (a peer rank missing or failed)");
+        std::this_thread::sleep_for(std::chrono::microseconds(spin < 100 ? 20 : 1000));
+    }
+}
+
 static int impl_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, uint32_t rank)
 {
     if (!ctx) return RVCP_E_INVALID;
@@ -1213,13 +1280,35 @@ static int impl_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, ui
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
+    // non-blocking: the call returns at once (ncclInProgress) and the rendezvous is polled
+    // against the deadline, so a rank whose peers never join gets RVCP_E_TIMEOUT instead of
+    // blocking forever (a library older than this header reads only the fields it knows:
+    // `size` tells it how many there are)
+    ncclConfig_t conf = NCCL_CONFIG_INITIALIZER;
+    conf.blocking = 0;
+    const Clock::time_point deadline = comm_deadline(ctx);
     ncclComm_t comm = nullptr;
-    const ncclResult_t r = R.comm_init_rank(&comm, (int)world, uid, (int)rank);
-    if (r != ncclSuccess) return fail(ctx, RVCP_E_HIP, std::string("ncclCommInitRank: ") + R.error_string(r));
+    const ncclResult_t r = R.comm_init_rank_config(&comm, (int)world, uid, (int)rank, &conf);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        if (comm) (void)R.comm_abort(comm);
+        return fail(ctx, RVCP_E_HIP, std::string("ncclCommInitRankConfig: ") + R.error_string(r));
+    }
+    const int rc = wait_comm_ready(ctx, comm, deadline, "ncclCommInitRankConfig");
+    if (rc != RVCP_OK) {
+        (void)R.comm_abort(comm);
+        return rc;
+    }
     ctx->comm = comm;
     ctx->comm_owned = true;
     ctx->comm_world = world;
     ctx->comm_rank = rank;
+    return RVCP_OK;
+}
+
+static int impl_rccl_set_timeout(rvcp_ctx_t *ctx, uint32_t timeout_ms)
+{
+    if (!ctx) return RVCP_E_INVALID;
+    ctx->comm_timeout_ms = timeout_ms;
     return RVCP_OK;
 }
 
@@ -1266,7 +1355,17 @@ static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, u
     HIP_TRY(ctx, hipEventRecord(ctx->evg0, s));
     const ncclResult_t r = rccl_api().gather(d_shard_rgba8, root ? d_gathered : nullptr,
                                              (size_t)slot * width, ncclUint32, 0, ctx->comm, s);
-    if (r != ncclSuccess) return fail(ctx, RVCP_E_HIP, std::string("ncclGather: ") + rccl_api().error_string(r));
+    if (r != ncclSuccess && r != ncclInProgress)
+        return fail(ctx, RVCP_E_HIP, std::string("ncclGather: ") + rccl_api().error_string(r));
+    if (r == ncclInProgress && ctx->comm_owned) {
+        // a non-blocking communicator may still be connecting to its peers (first gather):
+        // the enqueue completes once it has, bounded by the deadline
+        const int rc = wait_comm_ready(ctx, ctx->comm, comm_deadline(ctx), "ncclGather");
+        if (rc != RVCP_OK) {
+            abort_comm(ctx);
+            return rc;
+        }
+    }
     if (root && rvcp_launch_assemble((const uint32_t *)d_gathered, slot, width, height, N,
                                      (uint32_t *)d_frame, s) != 0)
         return fail(ctx, RVCP_E_HIP, "assemble launch failed");
@@ -1276,12 +1375,50 @@ static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, u
     return RVCP_OK;
 }
 
+// Poll the gather's end event against the deadline (a hipEventSynchronize would block forever
+// when a peer never enters the collective); on expiry, or when RCCL reports an asynchronous
+// error, abort the communicator so that the stuck kernel exits and the streams drain.
+static int wait_gather_done(rvcp_ctx_t *ctx)
+{
+    const Clock::time_point deadline = comm_deadline(ctx);
+    const RcclApi &R = rccl_api();
+    for (unsigned spin = 0;; spin++) {
+        const hipError_t q = hipEventQuery(ctx->evg1);
+        if (q == hipSuccess) return RVCP_OK;
+        if (q != hipErrorNotReady)
+            return fail(ctx, RVCP_E_HIP, std::string("gather: ") + hipGetErrorString(q));
+        if (ctx->comm && (spin & 63) == 63) {
+            ncclResult_t st = ncclSuccess;
+            if (R.get_async_error(ctx->comm, &st) == ncclSuccess && st != ncclSuccess &&
+                st != ncclInProgress) {
+                const std::string msg = std::string("ncclGather: ") + R.error_string(st);
+                abort_comm(ctx);
+                return fail(ctx, RVCP_E_HIP, msg);
+            }
+        }
+        if (Clock::now() >= deadline) {
+            abort_comm(ctx);
+            // the aborted kernels exit; give the stream a bounded moment to drain so that the
+            // context's buffers are no longer read when the caller frees or reuses them
+            const Clock::time_point drain = Clock::now() + std::chrono::seconds(5);
+            while (hipEventQuery(ctx->evg1) == hipErrorNotReady && Clock::now() < drain)
+                std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            if (hipEventQuery(ctx->evg1) == hipSuccess) ctx->gather_pending = false;
+            return fail(ctx, RVCP_E_TIMEOUT, "gather not complete within " +
+                        std::to_string(ctx->comm_timeout_ms) +
+                        " ms (a peer rank missing or failed); communicator aborted");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(spin < 2000 ? 5 : 200));
+    }
+}
+
 static int impl_gather_wait(rvcp_ctx_t *ctx, float *gather_ms, float *frame_ms)
 {
     if (!ctx) return RVCP_E_INVALID;
     if (!ctx->gather_pending) return fail(ctx, RVCP_E_INVALID, "no gather in flight");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipEventSynchronize(ctx->evg1));
+    const int rc = wait_gather_done(ctx);
+    if (rc != RVCP_OK) return rc;
     ctx->gather_pending = false;
     float ms = 0.0f;
     if (gather_ms) {
@@ -1403,6 +1540,11 @@ int rvcp_rccl_unique_id(uint8_t *out_id)
 int rvcp_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, uint32_t rank)
 {
     return barrier(ctx, [&] { return impl_rccl_init(ctx, id, world, rank); });
+}
+
+int rvcp_rccl_set_timeout(rvcp_ctx_t *ctx, uint32_t timeout_ms)
+{
+    return barrier(ctx, [&] { return impl_rccl_set_timeout(ctx, timeout_ms); });
 }
 
 int rvcp_rccl_attach(rvcp_ctx_t *ctx, void *nccl_comm, uint32_t world, uint32_t rank)

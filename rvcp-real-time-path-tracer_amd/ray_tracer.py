@@ -197,6 +197,11 @@ class RayTracer:
         buf = (ctypes.c_uint8 * abi.RCCL_ID_BYTES).from_buffer_copy(unique_id)
         self._check(self._lib.rvcp_rccl_init(self._ctx, ctypes.cast(buf, ctypes.c_void_p), world, rank))
 
+    def rccl_set_timeout(self, timeout_ms: int):
+        """rvcp_rccl_set_timeout: deadline of rccl_init / gather_wait in ms (0 = none); past it
+        they raise RvcpError with code RVCP_E_TIMEOUT and the communicator is aborted."""
+        self._check(self._lib.rvcp_rccl_set_timeout(self._ctx, int(timeout_ms)))
+
     def gather_frame_async(self, d_shard: int, width: int, height: int, d_gathered: int = 0,
                            d_frame: int = 0, stream: int = 0):
         """rvcp_gather_frame_async: RCCL gather of the shards to rank 0 + device assembly

@@ -20,6 +20,8 @@ def test_workloads_match_baseline_configs():
         assert (wl["W"], wl["H"], wl["spp"]) == (side, side, spp)
         assert f"{side}" in text and f"SPP={spp}" in text
     assert bench.workload("c5", 1)["extra_tris"] == 100000
+    c6 = bench.workload("c6", 1)                   # the reference's own scene-size limit
+    assert (c6["W"], c6["spp"], 32 + c6["extra_tris"], 68 + 3 * c6["extra_tris"]) == (1024, 30, 342, 998)
     assert bench.workload("c4", 8)["scaling"] == "strong"
     assert bench.workload("c4", 8)["W"] == 2048                 # fixed frame at any N
     assert bench.workload("c3", 1)["workload"] == "cornell_1024sq_spp30"
@@ -88,13 +90,16 @@ def _negotiate_worker(rank, world, port, outdir):
     """One rank of bench.py's N>1 control flow (negotiate_gather) over gloo, with the RCCL
     calls replaced by stand-ins that fail on chosen ranks."""
     import torch.distributed as dist
+    import rvcp_amd
+    RVCP_E_TIMEOUT, RvcpError = rvcp_amd.abi.RVCP_E_TIMEOUT, rvcp_amd.abi.RvcpError
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     results = {}
     try:
         for case, bad_rank, stage in [("ok", -1, ""), ("id", 3, "id"), ("init", 5, "init"),
                                       ("render", 6, "render"), ("probe", 7, "probe"),
-                                      ("init_all", -2, "init")]:
+                                      ("init_all", -2, "init"), ("init_timeout", 4, "init_t"),
+                                      ("probe_timeout", 2, "probe_t")]:
             inited = []
             gathered = []
 
@@ -109,6 +114,14 @@ def _negotiate_worker(rank, world, port, outdir):
             def init_comm(i, uid):
                 if fails("init"):
                     raise RuntimeError("ncclCommInitRank: unhandled system error")
+                if stage == "init_t":
+                    # the asymmetric case a blocking init could not survive: rank 4 fails at
+                    # once, its peers' non-blocking inits run into the deadline
+                    # (rvcp_rccl_init -> RVCP_E_TIMEOUT, communicator aborted)
+                    if rank == bad_rank:
+                        raise RuntimeError("ncclCommInitRankConfig: invalid usage")
+                    raise RvcpError(RVCP_E_TIMEOUT, "ncclCommInitRankConfig: no progress within "
+                                    "60000 ms (a peer rank missing or failed)")
                 assert uid == bytes([0]) * 128          # every rank joins rank 0's ids
                 inited.append(i)
 
@@ -120,6 +133,9 @@ def _negotiate_worker(rank, world, port, outdir):
                 gathered.append(True)
                 if fails("probe"):
                     raise RuntimeError("ncclGather: internal error")
+                if stage == "probe_t" and rank != bad_rank:
+                    # rank 2 never enters the gather: every other rank's wait hits the deadline
+                    raise RvcpError(RVCP_E_TIMEOUT, "gather not complete within 60000 ms")
 
             mode, why = bench.negotiate_gather(dist, rank, 2, make_id, init_comm, probe_render,
                                                probe_gather)
@@ -154,6 +170,14 @@ def test_negotiate_gather_world8_injected_failures(tmp_path):
             assert mode == "host" and bad in why, (r, case, why)
         mode, why, _, _ = res[r]["init_all"]
         assert mode == "host" and all(f"rank {k}" in why for k in range(8))
+        # an injected deadline: every rank agrees on the host gather, the failing rank and the
+        # timed-out ones are all named, and nobody was left inside a collective
+        mode, why, _, _ = res[r]["init_timeout"]
+        assert mode == "host" and "rank 4" in why and "invalid usage" in why
+        assert all(f"rank {k}" in why for k in range(8)) and "error -7" in why
+        mode, why, _, gathered = res[r]["probe_timeout"]
+        assert mode == "host" and "error -7" in why and "rank 2" not in why
+        assert gathered == [True]
         # a render failure on one rank keeps EVERY rank out of the collective gather (its
         # peers would otherwise wait in it forever)
         assert res[r]["render"][3] == [] and res[r]["ok"][3] == [True]
@@ -213,3 +237,70 @@ def test_self_launch_fails_with_a_rank(tmp_path):
     """A failing rank makes the whole command fail (non-zero exit status)."""
     r = _self_launch(tmp_path, {"STUB_FAIL_RANK": "1"})
     assert r.returncode != 0
+
+
+class _StubTracer:
+    """Stand-in for a RayTracer context: one call in flight at a time, stats of the last call."""
+
+    def __init__(self, log, i):
+        self.log, self.i, self.inflight = log, i, None
+
+    def enqueue(self, pushes, nb):
+        assert self.inflight is None, "a context holds one call at a time (rvcp.h)"
+        assert len(pushes) == nb
+        self.inflight = list(pushes)
+        self.log.extend(pushes)
+
+    def finish(self, nb):
+        assert self.inflight is not None and len(self.inflight) == nb
+        st = {"samples": nb * 7, "frames": self.inflight}
+        self.inflight = None
+        return st
+
+
+def test_call_schedule_accounts_every_frame_once():
+    """bench.CallSchedule (the warm-up and timed calls of bench.py) over
+    steps x frames per launch x frames in flight: every frame is enqueued exactly once with its
+    own time seed, every call's stats come back exactly once (so `sum(samples)` is exact), no
+    context ever holds two calls, and the seeds continue from warm-up into the timed run."""
+    for fif in (1, 2, 3, 4):
+        for batch in (1, 2, 3, 4, 5, 7, 8, 16, 22, 32):
+            for steps in list(range(1, 41)) + [63, 64, 65, 100, 129]:
+                log = []
+                tr = [_StubTracer(log, i) for i in range(fif)]
+                sched = bench.CallSchedule(fif, batch, lambda i, p, nb: tr[i].enqueue(p, nb),
+                                           lambda i, nb: tr[i].finish(nb), lambda t: t)
+                warm = -(-max(3, fif * batch) // batch) * batch
+                w_stats = sched.run(warm)
+                assert sum(s["samples"] for s in w_stats) == warm * 7
+                assert all(t.inflight is None for t in tr) and sched.pending == [0] * fif
+                stats = sched.run(steps)
+                assert sum(s["samples"] for s in stats) == steps * 7, (fif, batch, steps)
+                assert len(stats) == len(sched.calls(steps)) == len(sched.done_t)
+                assert sum(nb for _, nb in sched.done_t) == steps
+                want = [bench.TIME0 + f for f in range(warm + steps)]
+                assert log == want                       # every seed once, in order
+                got = sorted(t for s in stats for t in s["frames"])
+                assert got == want[warm:]                # each timed call's stats exactly once
+                assert all(t.inflight is None for t in tr)
+                # slot 0 of context 0 holds the first frame of the last call made on it
+                c0 = [c for c in range(len(sched.calls(steps))) if c % fif == 0][-1]
+                assert sched.slot_time[0][0] == bench.TIME0 + warm + sum(sched.calls(steps)[:c0])
+
+
+def test_report_failure_names_rank_and_stage(capsys):
+    """A library error during the run (a gather's RVCP_E_TIMEOUT) becomes one labelled JSON line
+    naming the rank, the stage and the code (rank 0 on stdout, the driver's line)."""
+    import rvcp_amd
+    RVCP_E_TIMEOUT, RvcpError = rvcp_amd.abi.RVCP_E_TIMEOUT, rvcp_amd.abi.RvcpError
+    wl = bench.workload("c4", 8)
+    err = RvcpError(RVCP_E_TIMEOUT, "gather not complete within 60000 ms")
+    rec = bench.report_failure(0, 8, wl, "timed frames", err)
+    line = capsys.readouterr().out.strip()
+    assert json.loads(line) == rec
+    assert rec["value"] is None and rec["n_gpus"] == 8
+    assert rec["error"] == {"rank": 0, "stage": "timed frames", "code": -7,
+                            "message": "rvcp error -7: gather not complete within 60000 ms"}
+    bench.report_failure(3, 8, wl, "warm-up frames", err)
+    cap = capsys.readouterr()
+    assert cap.out == "" and json.loads(cap.err)["error"]["rank"] == 3

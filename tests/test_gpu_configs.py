@@ -14,6 +14,11 @@ traversal count equal.  Coverage per config (BASELINE.json `configs`):
   C5 Cornell + 100k triangles   64^2 SPP=1 whole frame on the default LDS-tiled schedule (5),
                                  on schedule 4 and on the opt-in BVH; at 1024^2 SPP=30 two
                                  256-pixel row segments (tiled and BVH)
+  C6 Cornell + 310 triangles    (bench --workload c6: 342 faces / 998 vertices, the largest
+                                 unshared-vertex scene the reference's 1000-entry buffers hold,
+                                 ray_tracer_games101_branch.comp:18-19) 128^2 SPP=30 whole frame
+                                 on every brute-force schedule, and the 1024^2 SPP=30 frame's
+                                 rows at every stripe offset (y mod 8) and shard of 8
 """
 import numpy as np
 import pytest
@@ -143,6 +148,46 @@ def test_c5_full_size_segments(c5_scene, kw):
     g = _gpu(c5_scene, cfg, 1024, 1024)
     for rect in C5_RECTS:
         _assert_rect(g, _oracle(c5_scene, rvcp_amd.abi.make_config(spp=30), 1024, 1024, rect=rect), rect)
+
+
+# ---------------------------------------------------------------- C6: the reference's limit --
+@pytest.fixture(scope="module")
+def c6_scene(cornell):
+    import bench
+    sc = rvcp_amd.scene.with_random_triangles(cornell, bench.C6_EXTRA_TRIS)
+    assert len(sc.mesh.aligned_faces()) == 342 and len(sc.mesh.aligned_vertices()) == 998
+    return sc
+
+
+@pytest.fixture(scope="module")
+def c6_small_oracle(c6_scene):
+    cfg = rvcp_amd.abi.make_config(spp=30)
+    return cfg, _oracle(c6_scene, cfg, 128, 128)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(kernel_variant=3), dict(kernel_variant=4),
+                                dict(kernel_variant=5), dict(kernel_variant=6),
+                                dict(kernel_variant=10), dict(accel=1)],
+                         ids=["default", "scalar3", "tiled4", "tiled5", "scalar6", "tiledpool10", "bvh"])
+def test_c6_small_bitexact(c6_scene, c6_small_oracle, kw):
+    """128^2 SPP=30 of the c6 scene (342 faces), whole frame, every brute-force schedule and
+    the BVH, against the oracle: linear bits, RGBA8 and the traversal count."""
+    cfg, orc = c6_small_oracle
+    _assert_frame(_gpu(c6_scene, rvcp_amd.abi.make_config(spp=30, **kw), 128, 128), orc)
+
+
+C6_ROWS = sorted({8 * (13 * i % 128) + i % 8 for i in range(24)} | {0, 1023})
+
+
+def test_c6_full_size_rows(c6_scene):
+    """The bench's c6 frame at its own size (1024^2 SPP=30, the default schedule): rows at
+    every stripe offset and every shard of 8, against the oracle."""
+    assert {y % 8 for y in C6_ROWS} == set(range(8))
+    assert {(y // 8) % 8 for y in C6_ROWS} == set(range(8))
+    cfg = rvcp_amd.abi.make_config(spp=30)
+    g = _gpu(c6_scene, cfg, 1024, 1024)
+    for y in C6_ROWS:
+        _assert_rect(g, _oracle(c6_scene, cfg, 1024, 1024, rect=(0, y, 1024, 1)), (0, y, 1024, 1))
 
 
 # ---------------------------------------------------------------- UNORM8 rules -------------
