@@ -47,9 +47,11 @@ Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the path-tr
     a short pass after the timed region (with frames in flight a launch's event time includes
     the other frame's work); the rocprofv3 summary of the same command is committed under
     profiles/ and must agree;
-  * `valu_issue_*_pmc`: VALU wave-instructions per SIMD-cycle from the committed SQ counter
-    passes (tools/pmc_valu.py), against the guide's 0.5 (2 cycles per wave64 instruction) and
-    against the measured ceiling (tools/valu_rate.hip);
+  * `valu_issue_frac_pmc_guide`: VALU wave-instructions per SIMD-cycle from the committed SQ
+    counter passes (tools/pmc_valu.py) over the guide's 0.5 (2 cycles per wave64 instruction);
+    `valu_issue_frac_wall`: that pass's instructions per frame over the issue slots of
+    `ms_per_step` at `shader_clock_ghz`, the clock THIS run's path kernel measured on itself
+    (per-wave s_memtime / s_memrealtime stamps);
   * `traffic`: the kernel's measured HBM bytes per launch (rocprofv3 PMC, tools/pmc_traffic.py);
     `hbm_algorithmic`: SURVEY.md §8(d)'s HBM-read figure (36 algorithmic bytes per triangle
     test), which exceeds the HBM peak because the scene is served on-chip.
@@ -78,11 +80,10 @@ FLOP_PER_SPHERE_TEST = 25      # ray_tracer.comp:300-321
 REFERENCE_MSAMPLES = {"c3": 94.4, "c2": 75.2}
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (spec)
 # VALU issue: 1,024 SIMDs (256 CUs x 4) issuing one wave64 instruction per 2 cycles
-# (MI355X_MICROARCH.md) at the shader clock measured under this load, 2.29 GHz (in-kernel
-# s_memtime / s_memrealtime stamps of the C3 path kernel)
+# (MI355X_MICROARCH.md) at the shader clock this run measured (the path kernel's own per-wave
+# s_memtime / s_memrealtime stamps, rvcp_stats_t.shader_clock_ghz)
 N_SIMDS = 1024
 VALU_ISSUE_PER_CLK = 0.5
-SHADER_CLOCK_GHZ = 2.29
 FLOP_PER_TEST = 52
 C6_EXTRA_TRIS = 310            # Cornell + 310 = 342 faces, 998 vertices (workload c6)
 # the time seed of frame 0 (the tests' fixed seed); frame f renders with
@@ -507,6 +508,11 @@ def main():
                          "wait (rvcp_rccl_set_timeout); past it the rank aborts its communicator "
                          "-- at creation every rank then takes the labelled host gather, during "
                          "the run the command exits non-zero with a line naming rank and stage")
+    ap.add_argument("--interactive-pass", type=int, default=20,
+                    help="N=1: frames of the post-timing pass in the reference's own loop shape "
+                         "(one frame per launch, 2 in flight, each frame's push made just before "
+                         "its submission: ray_tracer.rs:80-98, vulkan.rs:367-369) -> "
+                         "config.interactive_ms_per_step (0 = skip)")
     ap.add_argument("--launch-pass", type=int, default=10,
                     help="frames (at most --steps) of the post-timing one-frame-in-flight pass "
                          "that measures the path kernel's isolated launch time "
@@ -748,11 +754,34 @@ def main():
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed * 1000.0 / args.steps
 
+    # The reference's own loop shape (after the timed region): one frame per submission, the
+    # push constant of each frame stamped just before it is submitted (ray_tracer.rs:80-98),
+    # two frames in flight behind per-image fences (vulkan.rs:367-369) -- no batches, nothing
+    # enqueued ahead.  Its ms per frame is config.interactive_ms_per_step beside ms_per_step.
+    interactive_ms = None
+    if args.interactive_pass > 0 and world == 1:
+        rts_i = [rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0)) for _ in range(2)]
+        for r in rts_i:
+            r.upload_scene(sc)
+        bufs_i = [torch.zeros((H, W), dtype=torch.int32, device=dev) for _ in range(2)]
+        sch_i = CallSchedule(
+            2, 1, lambda i, pushes, nb: rts_i[i].render_shard_async(pushes[0], W, H, 0, 1,
+                                                                   bufs_i[i].data_ptr()),
+            lambda i, nb: rts_i[i].sync_stats(), lambda t: sc.push_constant(t))
+        sch_i.run(4)
+        torch.cuda.synchronize()
+        ti = time.perf_counter()
+        sch_i.run(args.interactive_pass)
+        torch.cuda.synchronize()
+        interactive_ms = (time.perf_counter() - ti) * 1000.0 / args.interactive_pass
+        for r in rts_i:
+            r.close()
+
     # Isolated launch time (after the timed region): the path kernel with ONE frame in flight,
     # so its HIP-event time is its own (roofline.per_launch), on the full resident grid -- the
     # launch a one-frame-at-a-time caller makes (a grid left partly free for the next frame,
     # grid_waves_per_simd, only pays off with frames beside it)
-    iso_ms, latency_ms = [], []
+    iso_ms, latency_ms, iso_clk = [], [], []
     if args.launch_pass > 0:
         rt_iso = rt if grid_waves == 0 else rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0))
         if rt_iso is not rt:
@@ -761,7 +790,9 @@ def main():
             tl = time.perf_counter()
             rt_iso.render_shard_async(sc.push_constant(TIME0 + float(f)), W, H, rank, world,
                                       (frames[0] if world == 1 else shard_bufs[0]).data_ptr())
-            iso_ms.append(float(rt_iso.sync_stats()["main_kernel_ms"]))
+            st_iso = rt_iso.sync_stats()
+            iso_ms.append(float(st_iso["main_kernel_ms"]))
+            iso_clk.append(float(st_iso["shader_clock_ghz"]))
             latency_ms.append((time.perf_counter() - tl) * 1000.0)
         if rt_iso is not rt:
             rt_iso.close()
@@ -786,12 +817,17 @@ def main():
     algo_gbs = bytes_per_launch / wall_s / 1e9
     kname = rvcp_amd.abi.KERNEL_NAMES.get(variant, "?")
     traffic, traffic_src = load_traffic(wl["workload"], kname)
-    valu_busy, valu_issue_frac, valu_insts, valu_src = load_valu_busy(wl["workload"], kname,
-                                                                      want_insts=True)
+    valu_busy, _, valu_insts, valu_src = load_valu_busy(wl["workload"], kname, want_insts=True)
+    # the shader clock of THIS run: the path kernel's own per-wave s_memtime / s_memrealtime
+    # stamps (rvcp_stats_t.shader_clock_ghz), averaged over the timed calls by kernel time
+    clk = [(float(st["shader_clock_ghz"]), float(st["main_kernel_ms"])) for st in stats]
+    clk_w = sum(w for c, w in clk if c > 0)
+    clock_ghz = (sum(c * w for c, w in clk if c > 0) / clk_w) if clk_w > 0 else None
     # the committed PMC pass's VALU instructions per frame (one frame per launch there) over
-    # the issue slots of one timed frame: how close the wall clock is to the issue floor
-    valu_wall = (None if not valu_insts or world != 1 else
-                 valu_insts / (ms_per_step * 1e-3 * SHADER_CLOCK_GHZ * 1e9 * N_SIMDS * VALU_ISSUE_PER_CLK))
+    # the issue slots of one timed frame at this run's clock: how close the wall clock is to the
+    # issue floor (the guide's 0.5 wave-instructions per SIMD-cycle)
+    valu_wall = (None if not valu_insts or world != 1 or not clock_ghz else
+                 valu_insts / (ms_per_step * 1e-3 * clock_ghz * 1e9 * N_SIMDS * VALU_ISSUE_PER_CLK))
     bvh = args.accel == "bvh"
     iso_s = (float(np.mean(iso_ms)) / 1000.0) if iso_ms else None
 
@@ -906,6 +942,12 @@ def main():
                        # rvcp_render of this rank's frame; ms_per_step is the pipelined rate)
                        "frame_latency_ms_alone": (round(float(np.median(latency_ms)), 4)
                                                   if latency_ms else None),
+                       # the reference's loop shape: one frame per launch, 2 in flight, a push
+                       # per frame made just before its submission (ray_tracer.rs:80-98,
+                       # vulkan.rs:367-369); ms_per_step is the batched pipeline's rate
+                       "interactive_ms_per_step": (None if interactive_ms is None else
+                                                   round(interactive_ms, 4)),
+                       "interactive_frames": args.interactive_pass if interactive_ms else 0,
                        "gpu_max_hw_queues": hw_queues,
                        "gather": ("none" if world == 1 else
                                   "gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
@@ -954,13 +996,20 @@ def main():
                          if world == 1 else None,
                          "executed_traversal_frac": round(trav_exec / max(trav, 1), 4),
                          "valu_issue_frac_pmc_guide": valu_busy,
-                         "valu_issue_frac_pmc_measured_ceiling": valu_issue_frac,
                          "valu_insts_per_frame_pmc": None if not valu_insts else round(valu_insts),
+                         "shader_clock_ghz": None if clock_ghz is None else round(clock_ghz, 4),
+                         "shader_clock_ghz_isolated": (round(float(np.mean(iso_clk)), 4)
+                                                       if iso_clk and min(iso_clk) > 0 else None),
+                         "shader_clock_definition": (
+                             "this run's path-kernel waves: sum of s_memtime ticks / sum of "
+                             "s_memrealtime ticks x 100 MHz, start to end of each wave (timed "
+                             "calls, weighted by kernel time; _isolated: the one-frame pass)"),
                          "valu_issue_frac_wall": None if valu_wall is None else round(valu_wall, 4),
                          "valu_issue_frac_wall_definition": (
                              "PMC SQ_INSTS_VALU of the dominant kernel per frame (" + str(valu_src) +
-                             f") / (ms_per_step x {SHADER_CLOCK_GHZ} GHz x {N_SIMDS} SIMDs x "
-                             f"{VALU_ISSUE_PER_CLK} wave-instructions per SIMD-cycle)")},
+                             f") / (ms_per_step x shader_clock_ghz x {N_SIMDS} SIMDs x "
+                             f"{VALU_ISSUE_PER_CLK} wave-instructions per SIMD-cycle: the guide's "
+                             "issue rate)")},
             "cpu_baseline": None,
         }
         if world > 1:

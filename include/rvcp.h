@@ -226,6 +226,10 @@ typedef struct rvcp_stats {
     double main_kernel_ms;            /* device time of the dominant (path-tracing) kernel
                                          alone, HIP events on the launch stream; kernel_ms
                                          also covers the primary pre-pass and counter reset */
+    double shader_clock_ghz;          /* the shader clock that kernel ran at: its waves'
+                                         s_memtime ticks over their s_memrealtime (100 MHz)
+                                         ticks, start to end, summed; 0 when not measured
+                                         (schedules 1 / 2, trivial frames) */
 } rvcp_stats_t;
 
 #define RVCP_VARIANT_SPECIALIZED 16

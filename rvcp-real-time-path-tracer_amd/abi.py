@@ -24,8 +24,8 @@ CONFIG_DTYPE = np.dtype([("device", "<i4"), ("integrator", "<i4"), ("spp", "<u4"
 STATS_DTYPE = np.dtype([("kernel_ms", "<f8"), ("traversals", "<u8"),
                         ("traversals_executed", "<u8"), ("samples", "<u8"), ("faces", "<u4"),
                         ("kernel_variant", "<i4"), ("wave_iterations", "<u8"),
-                        ("main_kernel_ms", "<f8")])
-assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 56
+                        ("main_kernel_ms", "<f8"), ("shader_clock_ghz", "<f8")])
+assert CONFIG_DTYPE.itemsize == 64 and STATS_DTYPE.itemsize == 64
 # rvcp_stats_t.kernel_variant -> the dominant kernel's name as rocprofv3 reports it
 KERNEL_NAMES = {1: "games101_kernel", 2: "games101_dual_kernel", 3: "games101_path_kernel<5>",
                 4: "games101_tiled_kernel", 5: "games101_tiled_single_kernel",

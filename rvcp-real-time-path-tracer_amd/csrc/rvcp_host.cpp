@@ -45,6 +45,9 @@ using namespace rvcp;
 // "forever", which is what a blocking ncclCommInitRank or an unbounded event wait gives when a
 // peer never arrives
 constexpr uint32_t kDefaultCommTimeoutMs = 60000;
+// d_counters: executed traversals, queue head, wave iterations, surface-list length, and the
+// path kernel's clock stamps (shader-clock ticks, 100-MHz ticks; clock_stamp); padded to 8
+constexpr int kCounterWords = 8;
 
 struct rvcp_ctx {
     rvcp_config_t cfg{};
@@ -405,7 +408,7 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
     // the gamma-free store of ray_tracer.comp:820-822 and mandelbrot.comp:32-33
     for (int k = 1; k < 256; k++) T[k] = (float)G[k];
     if ((rc = dev_upload<float>(ctx, &ctx->d_unorm, T, 257)) != RVCP_OK) return bail(rc);
-    if (hipMalloc((void **)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMalloc((void **)&ctx->d_counters, kCounterWords * sizeof(unsigned long long)) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "hipMalloc counters"));
 
     int cus = 0;
@@ -807,7 +810,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     ctx->last_spec = false;
     // a gather of this context's previous frame may still read the caller's shard buffer
     if (ctx->gather_on_gstream) HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->evg1, 0));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(unsigned long long), s));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, kCounterWords * sizeof(unsigned long long), s));
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, s));
     if (A.n_pixels > 0) {
         int rc;
@@ -991,8 +994,11 @@ static int impl_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         std::memset(stats, 0, sizeof(*stats));
         float ms = 0.0f;
         HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-        unsigned long long c[4] = {0, 0, 0, 0};
+        unsigned long long c[kCounterWords] = {};
         HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+        // the path kernel's per-wave clock stamps (clock_stamp): shader-clock ticks over
+        // 100-MHz ticks, summed over its waves
+        stats->shader_clock_ghz = c[5] ? 0.1 * (double)c[4] / (double)c[5] : 0.0;
         stats->kernel_ms = ms;
         float ms_main = 0.0f;
         HIP_TRY(ctx, hipEventElapsedTime(&ms_main, ctx->evm, ctx->ev1));
@@ -1087,6 +1093,7 @@ static int render_multi(rvcp_ctx_t *ctx, const rvcp_push_constant_t *push, uint3
         total.wave_iterations += st.wave_iterations;
         total.faces = st.faces;
         total.kernel_variant = st.kernel_variant;
+        if (k == 0) total.shader_clock_ghz = st.shader_clock_ghz;
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         const uint32_t stripes = (H + 7) / 8;
         const uint32_t full = H / 8;                       // stripes with 8 rows

@@ -1104,6 +1104,22 @@ __device__ __forceinline__ void flush_wave_counters(unsigned long long *__restri
         atomicAdd(&counters[2], (unsigned long long)iters);
     }
 }
+// The shader clock the kernel ran at, measured in the product kernel itself (bench.py's
+// roofline.clock): every wave of a path kernel stamps s_memtime (shader-clock ticks) and
+// s_memrealtime (100 MHz) when it starts and when it ends, and lane 0 accumulates
+// (sum of the end stamps - sum of the start stamps) in counters[4] / counters[5] with vector
+// atomics (unsigned wrap-around makes the two halves of the difference separable, so no stamp
+// is held across the kernel: no register cost).  The host reports counters[4] / counters[5] *
+// 0.1 GHz (rvcp_stats_t::shader_clock_ghz), the wave-time-weighted mean clock.
+__device__ __forceinline__ void clock_stamp(unsigned long long *__restrict__ counters,
+                                            uint32_t lane, bool end) {
+    const unsigned long long c = __builtin_amdgcn_s_memtime();
+    const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        atomicAdd(&counters[4], end ? c : 0ull - c);
+        atomicAdd(&counters[5], end ? r : 0ull - r);
+    }
+}
 __device__ __forceinline__ void flush_counters(unsigned long long *__restrict__ counters,
                                                uint32_t lane, uint32_t trav, uint32_t iters) {
     unsigned long long t64 = trav;
@@ -1604,6 +1620,7 @@ __device__ __forceinline__ void path_body(
     const uint32_t lane = lane_id();
     // this wave's index in the block, made wave-uniform (an SGPR) for the LDS row bases
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    clock_stamp(counters, lane, false);
     // the per-wave timeline (FrameArgs::timeline) exists in the debug build only (RVCP_TIMELINE,
     // also passed to its specialised modules): its clocks held across the kernel cost the
     // product kernel SGPRs, spilled into VGPR lanes read back inside the loop
@@ -2256,6 +2273,7 @@ __device__ __forceinline__ void path_body(
 #endif
     }
     flush_wave_counters(counters, lane, trav_wave, iters);
+    clock_stamp(counters, lane, true);
 #ifdef RVCP_TIMELINE
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * BLK + threadIdx.x) / kWave;
@@ -2529,6 +2547,7 @@ __device__ __forceinline__ void legacy_body(
 {
     uint8_t *tab = coop_tab[threadIdx.x / kWave];
     const uint32_t lane = lane_id();
+    clock_stamp(counters, lane, false);
     Queue q = queue_init(A);
     const float sppf = (float)A.spp;
     const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
@@ -2767,6 +2786,7 @@ __device__ __forceinline__ void legacy_body(
 #endif
     }
     flush_counters(counters, lane, trav, iters);
+    clock_stamp(counters, lane, true);
 #ifdef RVCP_TIMELINE
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;

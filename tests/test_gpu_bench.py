@@ -60,6 +60,18 @@ def test_bench_line(tmp_path, workload, side, spp, steps):
     pl = rl["per_launch"]
     assert pl["frames"] >= 1 and 0 < pl["frac"] <= 1
     assert pl["kernel_ms_min"] <= pl["kernel_ms"]
+    # the clock is this run's (the path kernel's own stamps), not a
+    # constant; no "ceiling" field that the wall clock exceeds; the reference's loop shape
+    assert "valu_issue_frac_pmc_measured_ceiling" not in rl
+    assert 1.0 < rl["shader_clock_ghz"] < 3.0 and 1.0 < rl["shader_clock_ghz_isolated"] < 3.0
+    if rl["valu_insts_per_frame_pmc"]:
+        want = rl["valu_insts_per_frame_pmc"] / (d["ms_per_step"] * 1e-3 * rl["shader_clock_ghz"]
+                                                 * 1e9 * 1024 * 0.5)
+        assert rl["valu_issue_frac_wall"] == pytest.approx(want, rel=1e-3)
+    assert c["interactive_ms_per_step"] > 0 and c["interactive_frames"] == 20
+    # one frame per launch cannot beat the batched pipeline by much, nor lose by more than the
+    # tail it leaves (C2's frames are mostly tail)
+    assert 0.8 * d["ms_per_step"] < c["interactive_ms_per_step"] < 6.0 * d["ms_per_step"]
     # every frame has its own seed (123.0 + frame index); the saved frame is the oracle's
     # render of its seed
     assert c["saved_frame_time"] >= 123.0

@@ -35,6 +35,7 @@ int main(void) {
   S(rvcp_stats_t); F(rvcp_stats_t, kernel_ms); F(rvcp_stats_t, traversals);
   F(rvcp_stats_t, traversals_executed); F(rvcp_stats_t, samples); F(rvcp_stats_t, faces);
   F(rvcp_stats_t, wave_iterations); F(rvcp_stats_t, main_kernel_ms);
+  F(rvcp_stats_t, shader_clock_ghz);
   S(rvcp_lengths_t);
   S(rvcp_mandelbrot_push_t); F(rvcp_mandelbrot_push_t, position); F(rvcp_mandelbrot_push_t, scale);
   return 0;

@@ -110,6 +110,9 @@ for s in $STEPS; do
         selfl8) run selfl8 500 env RVCP_BENCH_REHEARSAL=1 python bench.py --gpus 8 --steps 10 --warmup 2 ;;
         c5tests) run c5tests 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "c5 or multi_tile or odd_remainder or variants or bitexact_cornell" ;;
         pooltests) run pooltests 600 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        rccltest) run pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl_timeout.py tests/test_gpu_batch.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
+        c6test) run pytest_c6 900 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 600 --timeout-method thread -k c6 ;;
+        benchc6) run bench_c6 300 python bench.py --workload c6 --steps 20 --warmup 3 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
