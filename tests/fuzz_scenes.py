@@ -5,7 +5,10 @@ The specialised scan drops products with exact-zero triangle components and skip
 reciprocal's class check where an interval/grain analysis proves the denominator zero or
 normal.  Those proofs depend on the triangles' magnitudes and lowest set bits, so the scenes
 here span them: a room of axis-aligned quads (many exact zeros, coarse grains) at a scale of
-2^-20 .. 2^38, plus a mix of off-axis triangles with random bits, slivers, point- and
+2^-20 .. 2^22, for a third of the seeds translated (with its camera) by up to 2^38 -- so that
+coordinates span 2^-20 .. 2^38 while the distances a path covers stay below the 2^24 that
+rvcp_config_t.ray_t_max allows (the shader's miss test writes t_max + 1, :287) -- plus a mix
+of off-axis triangles with random bits, slivers, point- and
 line-degenerate triangles, coplanar overlapping and duplicated triangles, tiny and huge
 triangles relative to the room, and cameras inside the geometry.  Each scene stays within the
 specialisation's range (|v0| <= 2^40, |e| <= 2^41: jit_scene_in_range), has at most 64 faces
@@ -31,8 +34,16 @@ def _normal(p0, p1, p2):
 def fuzz_scene(seed):
     """(scene, config kwargs, description) for fuzz case `seed`."""
     rng = np.random.default_rng(0x5EC0 + seed)
-    e = int(rng.integers(-20, 39)) if seed >= 4 else [-20, 38, 0, 37][seed]
+    e = int(rng.integers(-20, 23)) if seed >= 4 else [-20, 22, 0, 20][seed]
     s = np.float32(2.0 ** e)
+    # a translation of the whole scene: none, or 2^20 .. 2^38 per axis (seeds 1 and 3 at 2^38)
+    e_off = 38 if seed in (1, 3) else (int(rng.integers(20, 39)) if rng.random() < 0.34 else None)
+    off = (np.zeros(3, np.float32) if e_off is None else
+           (rng.choice([-1.0, 1.0], 3) * 2.0 ** e_off * rng.uniform(1, 1.9, 3)).astype(np.float32))
+    if e_off is not None and e < e_off - 16:
+        # the room at least 2^7 ulps of the offset across (else it collapses to a point)
+        e = e_off - 16
+        s = np.float32(2.0 ** e)
     tris, mats = [], []
 
     def add(p0, p1, p2, mat):
@@ -108,7 +119,7 @@ def fuzz_scene(seed):
     # every vertex within 30 rooms of the origin: |v0| <= 2^40 and |e| <= 2^41 at 2^38, the
     # specialisation's range (jit_scene_in_range), so every case takes the specialised scan
     lim = np.float32(30) * g
-    tris = [np.clip(p, -lim, lim).astype(np.float32) for p in tris]
+    tris = [(np.clip(p, -lim, lim) + off).astype(np.float32) for p in tris]
 
     V = rvcp_amd.scene.VERTEX_DTYPE
     F = rvcp_amd.scene.FACE_DTYPE
@@ -130,16 +141,19 @@ def fuzz_scene(seed):
     look = rng.uniform(-4, 4, 3).astype(np.float32) * g
     if np.allclose(look, pos):
         look = pos + np.float32([0, 0, 1]) * g
-    cam = rvcp_amd.Camera.new(pos, look, float(np.float32(0.1) * g), float(np.float32(1e5) * s),
+    t_cap = 16777214.0                      # below 2^24 (rvcp_config_t.ray_t_max)
+    pos, look = (pos + off).astype(np.float32), (look + off).astype(np.float32)
+    cam = rvcp_amd.Camera.new(pos, look, float(np.float32(0.1) * g),
+                              min(float(np.float32(1e5) * s), t_cap),
                               float(rng.uniform(35, 80)), 1.0, 1.0)
     mesh = rvcp_amd.scene.ArrayMesh(verts, faces)
     sc = rvcp_amd.Scene(cam, materials, [], mesh)
 
     t_min = float(np.float32(rng.choice([1e-2, 1e-3, 0.3])) * g)
-    kw = dict(spp=2, ray_t_min=t_min, ray_t_max=float(np.float32(1e4) * s),
+    kw = dict(spp=2, ray_t_min=t_min, ray_t_max=min(float(np.float32(1e4) * s), t_cap),
               eps=float(rng.choice([1e-3 * float(g), 1e-2 * float(g), 1e-3])),
               max_bounces=int(rng.choice([3, 15])), lum_id_std140_quirk=int(rng.random() < 0.7))
-    desc = (f"seed {seed}: scale 2^{e}, {len(tris)} faces, camera {'inside' if inside else 'outside'}"
+    desc = (f"seed {seed}: scale 2^{e}, offset 2^{e_off}, {len(tris)} faces, camera {'inside' if inside else 'outside'}"
             f", t_min {t_min:.3g}, eps {kw['eps']:.3g}, kinds {sorted(set(kinds))}")
     return sc, kw, desc
 

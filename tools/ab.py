@@ -8,7 +8,8 @@ arguments of the runner.  Cases run interleaved, pass after pass, each under its
 limit; one line per (pass, case), then the median per case.
 
 Runners:
-  bench     python bench.py --no-cpu-baseline --launch-pass 0 --steps 40 --warmup 5 ARGS
+  bench     python bench.py --no-cpu-baseline --launch-pass 0 --interactive-pass 0 --steps 40
+            --warmup 5 ARGS
             (ms_per_step, the driver's figure: frames in flight and batches as the bench
             picks them unless ARGS fix them; --field picks another key of the line, e.g.
             config.frame_latency_ms_alone with ARGS --launch-pass 40)
@@ -32,10 +33,21 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RUNNERS = {
     "bench": [sys.executable, "bench.py", "--no-cpu-baseline", "--launch-pass", "0",
-              "--steps", "40", "--warmup", "5"],
+              "--interactive-pass", "0", "--steps", "40", "--warmup", "5"],
     "frames": [sys.executable, "tools/frames.py", "--frames", "20"],
     "share": [sys.executable, "-u", "tools/rank_share.py"],
 }
+
+
+def stale_macros(env):
+    """-D macros a case passes to hipRTC (RVCP_JIT_FLAGS) that no kernel source names any more:
+    re-running such a case would build the same module under another label."""
+    import re
+    names = re.findall(r"-D\s*([A-Za-z_][A-Za-z0-9_]*)", env.get("RVCP_JIT_FLAGS", ""))
+    csrc = os.path.join(ROOT, "rvcp-real-time-path-tracer_amd", "csrc")
+    text = "".join(open(os.path.join(csrc, f)).read() for f in os.listdir(csrc)
+                   if f.endswith((".hip", ".h", ".cpp")))
+    return [n for n in names if n not in text]
 
 
 def parse_case(text):
@@ -84,6 +96,11 @@ def main():
     if not texts:
         ap.error("no cases")
     cases = [parse_case(c) for c in texts]
+    for label, env, _ in cases:
+        stale = stale_macros(env)
+        if stale:
+            sys.exit(f"case {label}: {', '.join(stale)} no longer exist in the kernel sources -- a "
+                     "historical case file, not re-runnable (it would measure noise as an effect)")
     got = {label: [] for label, _, _ in cases}
     for p in range(1, a.passes + 1):
         for label, env, args in cases:

@@ -57,26 +57,27 @@ for s in $STEPS; do
         benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 --no-cpu-baseline ;;
         # the headline command under rocprofv3: default frames in flight, and one frame in flight
         # (per-launch durations that do not overlap -- roofline.per_launch)
-        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
-        # every launch timed (no warm-up, no launch pass): tools/trace_busy.py's busy time per frame
-        profbusy) run profbusy 600 rocprofv3 --kernel-trace --stats -d "$OUT/profbusy_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 0 --launch-pass 0 --no-cpu-baseline && python3 tools/trace_busy.py "$OUT/profbusy_$TAG/run_kernel_trace.csv" --frames 20 --skip 2 >> "$OUT/${TAG}_profbusy.log" ;;
-        prof1) run prof1 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof1_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --interactive-pass 0 ;;
+        # every launch timed (no warm-up, no launch pass): tools/trace_busy.py's busy time per frame,
+# skipping the warm-up launches the bench reports (config.warmup_frames / frames_per_launch)
+        profbusy) run profbusy 600 rocprofv3 --kernel-trace --stats -d "$OUT/profbusy_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 && python3 tools/trace_busy.py "$OUT/profbusy_$TAG/run_kernel_trace.csv" --frames 20 --skip "$(python3 -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['config']; print(-(-d['warmup_frames'] // d['frames_per_launch']))" "$OUT/${TAG}_profbusy.log")" >> "$OUT/${TAG}_profbusy.log" ;;
+        prof1) run prof1 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof1_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
         # PMC passes, one counter group per run (one frame in flight and one frame per launch, so
         # each dispatch is one frame of its own)
-        pmcf) run pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        pmcw) run pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        sqpmc) run sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        sqpmc2) run sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        c5pmcf) run c5pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5pmcf_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        c5pmcw) run c5pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5pmcw_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        c5sqpmc) run c5sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c5sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        c5sqpmc2) run c5sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d "$OUT/c5sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        bvhsqpmc) run bvhsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/bvhsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        bvhsqpmc2) run bvhsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/bvhsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        m2sqpmc) run m2sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/m2sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        m2sqpmc2) run m2sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/m2sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        spsqpmc) run spsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/spsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
-        spsqpmc2) run spsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/spsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        pmcf) run pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        pmcw) run pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        sqpmc) run sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        sqpmc2) run sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        c5pmcf) run c5pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5pmcf_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        c5pmcw) run c5pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5pmcw_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        c5sqpmc) run c5sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c5sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        c5sqpmc2) run c5sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d "$OUT/c5sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --steps 1 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        bvhsqpmc) run bvhsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/bvhsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        bvhsqpmc2) run bvhsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/bvhsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c5 --accel bvh --steps 2 --warmup 1 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        m2sqpmc) run m2sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/m2sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        m2sqpmc2) run m2sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/m2sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c3m2 --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        spsqpmc) run spsqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/spsqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        spsqpmc2) run spsqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/spsqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload spheres --steps 10 --warmup 2 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
         # the chip's VALU issue ceiling and its in-kernel clock; the C3 kernel's in-kernel clock
         valu) run valu_rate 180 tools/build/valu_rate ;;
         valupmc) run valupmc 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/valupmc_$TAG" -o run --output-format csv -- tools/build/valu_rate ;;
@@ -90,7 +91,7 @@ for s in $STEPS; do
         # schedules 4 / 10 on meshes (tools/ab.py, one frame at a time)
         c5pool) run c5pool 900 python tools/ab.py --runner frames "s4=::--variant 4 --tris 2000 --size 1024 --spp 8 --frames 6" "s10=::--variant 10 --tris 2000 --size 1024 --spp 8 --frames 6" ;;
         spec) run pytest_spec 900 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_pipeline.py tests/test_gpu_batch.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
-        sqpmc3) run sqpmc3 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVE_CYCLES -d "$OUT/sqpmc3_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames-in-flight 1 --batch 1 ;;
+        sqpmc3) run sqpmc3 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVE_CYCLES -d "$OUT/sqpmc3_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
         sqrtchk) run sqrt_check 300 tools/build/sqrt_check ;;
         bvhtest) run pytest_bvh 600 python -u -m pytest tests/test_gpu_bvh.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         m2test) run pytest_m2 600 python -u -m pytest tests/test_gpu_legacy.py tests/test_gpu_specialize.py tests/test_gpu_batch.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
@@ -110,6 +111,7 @@ for s in $STEPS; do
         selfl8) run selfl8 500 env RVCP_BENCH_REHEARSAL=1 python bench.py --gpus 8 --steps 10 --warmup 2 ;;
         c5tests) run c5tests 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "c5 or multi_tile or odd_remainder or variants or bitexact_cornell" ;;
         pooltests) run pooltests 600 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        fuzz) run pytest_fuzz 600 python -u -m pytest tests/test_gpu_spec_fuzz.py -m gpu -x -q --timeout 200 --timeout-method thread ;;
         rccltest) run pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl_timeout.py tests/test_gpu_batch.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
         c6test) run pytest_c6 900 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 600 --timeout-method thread -k c6 ;;
         benchc6) run bench_c6 300 python bench.py --workload c6 --steps 20 --warmup 3 ;;
