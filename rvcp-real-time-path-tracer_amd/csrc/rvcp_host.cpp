@@ -45,9 +45,7 @@ using namespace rvcp;
 // "forever", which is what a blocking ncclCommInitRank or an unbounded event wait gives when a
 // peer never arrives
 constexpr uint32_t kDefaultCommTimeoutMs = 60000;
-// d_counters: executed traversals, queue head, wave iterations, surface-list length, and the
-// path kernel's clock stamps (shader-clock ticks, 100-MHz ticks; clock_stamp); padded to 8
-constexpr int kCounterWords = 8;
+
 
 struct rvcp_ctx {
     rvcp_config_t cfg{};
@@ -258,6 +256,22 @@ void camera_constants(const rvcp_push_constant_t &pc, uint32_t W, uint32_t H, Fr
     A.t_near = pc.camera.t_near;
     A.t_far = pc.camera.t_far;
     A.time = pc.time;
+}
+
+// The primary ray's range is [t_near, t_far] x t_coef (sample_ray, :226-233), and a miss is
+// written as t_max + 1 (:287) and detected as t > t_max (:424): once t_max reaches 2^24 the +1
+// is lost and the shader takes a miss for a hit on uninitialised data.  The kernels detect a
+// miss by the absent face instead, so such a frame would differ from the reference's; it is
+// refused, as rvcp_config_t.ray_t_max >= 2^24 is for the secondary rays.  t_coef is at most
+// |corner of the image plane - eye| / t_near = sqrt(1 + tan^2(fov / 2) (1 + (W / H)^2))
+// (u, v, forward orthogonal); a 1e-3 margin covers the float rounding of the shader's t_coef.
+bool primary_t_range_ok(const rvcp_push_constant_t &pc, uint32_t W, uint32_t H)
+{
+    const double tf = pc.camera.t_far;
+    const double t = std::tan((double)pc.camera.vertical_fov / 2.0 * 3.1415926 / 180.0);
+    const double a = (double)W / (double)H;
+    const double tc = std::sqrt(1.0 + t * t * (1.0 + a * a));
+    return std::fabs(tf) * tc * (1.0 + 1e-3) < 16777216.0;
 }
 
 template <typename T>
@@ -699,6 +713,10 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     if (n_frames > 1 && !ctx->subs.empty())
         return fail(ctx, RVCP_E_UNSUPPORTED, "frame batches drive one GPU (n_gpus = 1)");
     if (!ctx->has_scene) return fail(ctx, RVCP_E_NO_SCENE, "render before rvcp_upload_scene");
+    for (uint32_t k = 0; k < n_frames; k++)
+        if (!primary_t_range_ok(pushes[k], width, height))
+            return fail(ctx, RVCP_E_INVALID, "camera t_far x t_coef must stay below 2^24 (the "
+                        "shader's miss test t_max + 1, :287, :424)");
     // one frame in flight per context: its surface list, counters and events are the frame's
     if (ctx->pending)
         return fail(ctx, RVCP_E_INVALID, "a frame is in flight on this context (rvcp_wait first)");
@@ -998,7 +1016,8 @@ static int impl_sync_stats(rvcp_ctx_t *ctx, rvcp_stats_t *stats)
         HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
         // the path kernel's per-wave clock stamps (clock_stamp): shader-clock ticks over
         // 100-MHz ticks, summed over its waves
-        stats->shader_clock_ghz = c[5] ? 0.1 * (double)c[4] / (double)c[5] : 0.0;
+        stats->shader_clock_ghz = c[kClockWord + 1]
+            ? 0.1 * (double)c[kClockWord] / (double)c[kClockWord + 1] : 0.0;
         stats->kernel_ms = ms;
         float ms_main = 0.0f;
         HIP_TRY(ctx, hipEventElapsedTime(&ms_main, ctx->evm, ctx->ev1));

@@ -56,6 +56,11 @@ constexpr uint32_t kChunkWindow = 10000;    // 100 us
 // unused: a non-tiled pool measured slower)
 constexpr int kDefaultVariant = 3;
 constexpr int kMaxVariant = 10;
+// d_counters (u64 words): executed traversals, queue head, wave iterations, surface-list
+// length, and at kClockWord (a cache line of its own) the path kernel's clock stamps
+// (shader-clock ticks, 100-MHz ticks; clock_stamp in rvcp_kernels.hip)
+constexpr int kCounterWords = 32;
+constexpr int kClockWord = 16;
 constexpr int kTiledPoolVariant = 10;
 constexpr int variant_block(int v) { return v == kTiledPoolVariant ? kTiledPoolWaves * kWave : kBlock; }
 constexpr uint64_t kWideMinSamples = 8ull << 20;   // auto: variant 6 from 8 Msamples per frame

@@ -1105,19 +1105,21 @@ __device__ __forceinline__ void flush_wave_counters(unsigned long long *__restri
     }
 }
 // The shader clock the kernel ran at, measured in the product kernel itself (bench.py's
-// roofline.clock): every wave of a path kernel stamps s_memtime (shader-clock ticks) and
-// s_memrealtime (100 MHz) when it starts and when it ends, and lane 0 accumulates
-// (sum of the end stamps - sum of the start stamps) in counters[4] / counters[5] with vector
-// atomics (unsigned wrap-around makes the two halves of the difference separable, so no stamp
-// is held across the kernel: no register cost).  The host reports counters[4] / counters[5] *
-// 0.1 GHz (rvcp_stats_t::shader_clock_ghz), the wave-time-weighted mean clock.
+// roofline.shader_clock_ghz): the first wave of every workgroup of a path kernel stamps
+// s_memtime (shader-clock ticks) and s_memrealtime (100 MHz) when it starts and when it ends,
+// and lane 0 accumulates (sum of the end stamps - sum of the start stamps) in
+// counters[kClockWord] / [kClockWord + 1] with vector atomics (unsigned wrap-around makes the
+// two halves of the difference separable, so no stamp is held across the kernel: no register
+// cost; a cache line of their own, away from the queue head's atomics).  The host reports their
+// quotient x 0.1 GHz (rvcp_stats_t::shader_clock_ghz), the wave-time-weighted mean clock.
 __device__ __forceinline__ void clock_stamp(unsigned long long *__restrict__ counters,
-                                            uint32_t lane, bool end) {
+                                            uint32_t lane, bool first_wave, bool end) {
+    if (!first_wave) return;
     const unsigned long long c = __builtin_amdgcn_s_memtime();
     const unsigned long long r = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
-        atomicAdd(&counters[4], end ? c : 0ull - c);
-        atomicAdd(&counters[5], end ? r : 0ull - r);
+        atomicAdd(&counters[kClockWord], end ? c : 0ull - c);
+        atomicAdd(&counters[kClockWord + 1], end ? r : 0ull - r);
     }
 }
 __device__ __forceinline__ void flush_counters(unsigned long long *__restrict__ counters,
@@ -1620,7 +1622,7 @@ __device__ __forceinline__ void path_body(
     const uint32_t lane = lane_id();
     // this wave's index in the block, made wave-uniform (an SGPR) for the LDS row bases
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    clock_stamp(counters, lane, false);
+    clock_stamp(counters, lane, wv == 0, false);
     // the per-wave timeline (FrameArgs::timeline) exists in the debug build only (RVCP_TIMELINE,
     // also passed to its specialised modules): its clocks held across the kernel cost the
     // product kernel SGPRs, spilled into VGPR lanes read back inside the loop
@@ -2273,7 +2275,7 @@ __device__ __forceinline__ void path_body(
 #endif
     }
     flush_wave_counters(counters, lane, trav_wave, iters);
-    clock_stamp(counters, lane, true);
+    clock_stamp(counters, lane, wv == 0, true);
 #ifdef RVCP_TIMELINE
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * BLK + threadIdx.x) / kWave;
@@ -2547,7 +2549,8 @@ __device__ __forceinline__ void legacy_body(
 {
     uint8_t *tab = coop_tab[threadIdx.x / kWave];
     const uint32_t lane = lane_id();
-    clock_stamp(counters, lane, false);
+    const bool first_wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave) == 0;
+    clock_stamp(counters, lane, first_wave, false);
     Queue q = queue_init(A);
     const float sppf = (float)A.spp;
     const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
@@ -2786,7 +2789,7 @@ __device__ __forceinline__ void legacy_body(
 #endif
     }
     flush_counters(counters, lane, trav, iters);
-    clock_stamp(counters, lane, true);
+    clock_stamp(counters, lane, first_wave, true);
 #ifdef RVCP_TIMELINE
     if (A.timeline && lane == 0) {
         const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) / kWave;

@@ -143,8 +143,9 @@ def fuzz_scene(seed):
         look = pos + np.float32([0, 0, 1]) * g
     t_cap = 16777214.0                      # below 2^24 (rvcp_config_t.ray_t_max)
     pos, look = (pos + off).astype(np.float32), (look + off).astype(np.float32)
+    # (the primary ray's t_far x t_coef stays below 2^24 too: t_coef < 4 at these fields of view)
     cam = rvcp_amd.Camera.new(pos, look, float(np.float32(0.1) * g),
-                              min(float(np.float32(1e5) * s), t_cap),
+                              min(float(np.float32(1e5) * s), 2.0 ** 22),
                               float(rng.uniform(35, 80)), 1.0, 1.0)
     mesh = rvcp_amd.scene.ArrayMesh(verts, faces)
     sc = rvcp_amd.Scene(cam, materials, [], mesh)

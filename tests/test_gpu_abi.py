@@ -222,3 +222,29 @@ def test_grid_waves_per_simd_keeps_the_frame(cornell, integrator, spp):
     for img, trav in outs[1:]:
         assert np.array_equal(img, outs[0][0])
         assert trav == outs[0][1]
+
+
+def test_primary_t_range_below_2_24_is_enforced(cornell):
+    """The shader writes a miss as t_max + 1 and tests t > t_max (:287, :424): at a primary-ray
+    t_max (camera t_far x t_coef) of 2^24 or more the +1 is lost and the reference takes a miss
+    for a hit.  Such a camera is refused (RVCP_E_INVALID) like rvcp_config_t.ray_t_max >= 2^24;
+    the largest accepted t_far renders the oracle's frame (found by tests/test_gpu_spec_fuzz.py)."""
+    import oracle as O
+    from conftest import scene_arrays
+    cam = cornell.camera
+    with rvcp_amd.RayTracer(spp=1) as rt:
+        for t_far, ok in [(2.0 ** 24, False), (1.5e7, False), (float("inf"), False),
+                          (float("nan"), False), (1.0e7, True)]:
+            sc = rvcp_amd.Scene(rvcp_amd.Camera.new(cam.position, cam.position + cam.forward,
+                                                    cam.t_near, t_far, cam.vertical_fov, 1.0, 1.0),
+                                cornell.materials, [], cornell.mesh)
+            rt.upload_scene(sc)
+            if not ok:
+                with pytest.raises(rvcp_amd.abi.RvcpError) as e:
+                    rt.render(64, 48, 123.0)
+                assert e.value.code == rvcp_amd.abi.RVCP_E_INVALID and "2^24" in str(e.value)
+            else:
+                rgba = rt.render(64, 48, 123.0)
+                _, o_rgba, _ = O.render(scene_arrays(sc), sc.push_constant(123.0),
+                                        rvcp_amd.abi.make_config(spp=1), 64, 48)
+                assert np.array_equal(rgba, o_rgba)

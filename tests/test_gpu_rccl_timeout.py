@@ -19,12 +19,14 @@ import time
 import numpy as np
 import rvcp_amd
 from rvcp_amd import abi
+print("STAGE start", flush=True)
 sc = rvcp_amd.Scene.default()
 rt = rvcp_amd.RayTracer(spp=2)
 rt.upload_scene(sc)
 before = rt.render(40, 24, 123.0)
 rt.rccl_set_timeout(TIMEOUT_MS)
 uid = rvcp_amd.rccl_unique_id()
+print("STAGE init", flush=True)
 t0 = time.perf_counter()
 try:
     rt.rccl_init(uid, 2, 0)               # world 2, and rank 1 never comes
@@ -32,6 +34,7 @@ try:
 except abi.RvcpError as e:
     print("RESULT", e.code, round(time.perf_counter() - t0, 3), str(e), flush=True)
 # the context outlives the aborted communicator: it still renders, bit-identically
+print("STAGE render", flush=True)
 after = rt.render(40, 24, 123.0)
 print("SAME", bool(np.array_equal(before, after)), flush=True)
 # a gather without a communicator is refused, not attempted
@@ -41,16 +44,23 @@ try:
 except abi.RvcpError as e:
     print("WAIT", e.code, flush=True)
 # and a world-1 communicator can still be made on the same context afterwards
+print("STAGE reinit", flush=True)
 rt.rccl_init(rvcp_amd.rccl_unique_id(), 1, 0)
 print("REINIT ok", flush=True)
+print("STAGE close", flush=True)
 rt.close()
 print("DONE", flush=True)
 '''
 
 
 def _run(code, limit):
-    return subprocess.run([sys.executable, "-u", "-c", code], cwd=ROOT, capture_output=True,
-                          text=True, timeout=limit)
+    try:
+        return subprocess.run([sys.executable, "-u", "-c", code], cwd=ROOT, capture_output=True,
+                              text=True, timeout=limit)
+    except subprocess.TimeoutExpired as e:
+        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
+        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
+        raise AssertionError(f"child hung after {limit} s; stdout:\n{out[-3000:]}\nstderr:\n{err[-3000:]}")
 
 
 @pytest.mark.gpu
