@@ -869,7 +869,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
             A.chunk_window = kChunkWindow;
             if (const char *c = RVCP_KNOB("RVCP_DEBUG_CHUNK")) {   // fixed grab (experiments)
                 const int v = std::atoi(c);
-                if (v >= 1 && v <= 4096) A.dyn_chunk = A.chunk_min = (uint32_t)v;
+                if (v >= 1 && v <= (int)kDynChunk) A.dyn_chunk = A.chunk_min = (uint32_t)v;   // <= 64: mode 2 prefills a grab into 64 LDS slots
             }
             if (const char *c = RVCP_KNOB("RVCP_DEBUG_CHUNK_WINDOW")) {
                 const int v = std::atoi(c);

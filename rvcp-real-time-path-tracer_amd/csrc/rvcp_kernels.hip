@@ -844,6 +844,11 @@ __device__ __forceinline__ void start_batch_pixel(const FrameArgs &A, uint32_t p
     ridx = 0.0f;
     primary_ray(C, u_, v_, o, d, tmin, tmax);
 }
+__device__ __forceinline__ void start_any(const FrameArgs &A, uint32_t pix, float &seed,
+                                          float &ridx, f3 &o, f3 &d, float &tmin, float &tmax) {
+    if (A.batch_cams) start_batch_pixel(A, pix, seed, ridx, o, d, tmin, tmax);
+    else start_pixel(A, pix, seed, ridx, o, d, tmin, tmax);
+}
 // Output index of queue pixel `pix` (frame f's outputs start f * frame_stride pixels in).
 __device__ __forceinline__ uint32_t batch_out(const FrameArgs &A, uint32_t pix) {
     if (!A.batch_cams) return pix;
@@ -1089,6 +1094,88 @@ __device__ __forceinline__ void queue_take(Queue &q, uint64_t need, uint32_t lan
         const bool mine = ((need >> lane) & 1ull) && r < avail;
         const uint64_t given = __ballot(mine);
         if (mine) { pix = q.next + r; got = true; }
+        q.next += __builtin_popcountll(given);
+        q.taken += __builtin_popcountll(given);
+        need &= ~given;
+    }
+}
+
+// Mode 2's pixel starts (srand's three sines, sample_ray's root and divisions: ~150 VALU per
+// pixel, main :486-491), computed for a whole grab at once, one pixel per lane, into this wave's
+// 64 LDS slots, instead of per pixel when a lane takes it -- in the persistent kernel a few lanes
+// take a pixel in most iterations, so the start ran at a few lanes per instruction.  A slot holds
+// (d, seed) and (o, t_min) + t_max; a lane taking pixel p reads slot p - base.  Each pixel's
+// start is the same arithmetic as before, so the frames are unchanged.
+#ifndef RVCP_LEGACY_PREFILL
+#define RVCP_LEGACY_PREFILL 1
+#endif
+struct StartSlot {
+    float4 ds;      // d.xyz, seed
+    float4 ot;      // o.xyz, t_min
+    float tmax;
+};
+__device__ __forceinline__ void start_any(const FrameArgs &A, uint32_t pix, float &seed,
+                                          float &ridx, f3 &o, f3 &d, float &tmin, float &tmax);
+__device__ __forceinline__ void prefill_starts(const FrameArgs &A, uint32_t base, uint32_t n,
+                                               uint32_t lane, StartSlot *slots) {
+    if (lane < n) {
+        float seed, ridx, tmin, tmax;
+        f3 o, d;
+        start_any(A, base + lane, seed, ridx, o, d, tmin, tmax);
+        slots[lane].ds = make_float4(d.x, d.y, d.z, seed);
+        slots[lane].ot = make_float4(o.x, o.y, o.z, tmin);
+        slots[lane].tmax = tmax;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// queue_take for mode 2 with prefilled starts: a lane that gets pixel `pix` also gets its start
+// (read from its slot before the next grab refills the slots).
+__device__ __forceinline__ void queue_take_started(Queue &q, uint64_t need, uint32_t lane,
+                                                   const FrameArgs &A,
+                                                   unsigned long long *__restrict__ counters,
+                                                   StartSlot *slots, uint32_t &base, bool &got,
+                                                   uint32_t &pix, float &seed, float &ridx, f3 &o,
+                                                   f3 &d, float &tmin, float &tmax) {
+    got = false;
+    while (need != 0ull) {
+        if (q.next >= q.end) {
+            if (q.exhausted) break;
+            const int leader = (int)__builtin_ctzll(need);
+            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - q.t0 + 1ull;
+            const uint64_t want = (uint64_t)q.taken * A.chunk_window / dt;
+            uint32_t c = want > A.dyn_chunk ? A.dyn_chunk : (uint32_t)want;
+            c = __builtin_amdgcn_readfirstlane(c < A.chunk_min ? A.chunk_min : c);
+            uint32_t b = 0;
+            if (lane == (uint32_t)leader) b = atomicAdd((unsigned int *)&counters[1], c);
+            b = __builtin_amdgcn_readfirstlane(__shfl(b, leader)) + A.static_chunks;
+            if (b >= A.n_pixels) { q.exhausted = true; break; }
+            q.next = b;
+            q.end = b + c < A.n_pixels ? b + c : A.n_pixels;
+            base = b;
+            prefill_starts(A, base, q.end - base, lane, slots);
+        }
+        const uint32_t avail = q.end - q.next;
+        const uint32_t r = rank_in(need);
+        const bool mine = ((need >> lane) & 1ull) && r < avail;
+        const uint64_t given = __ballot(mine);
+        if (mine) {
+            pix = q.next + r;
+            got = true;
+            const StartSlot &S = slots[pix - base];
+            const float4 ds = S.ds, ot = S.ot;
+            d = mk(ds.x, ds.y, ds.z);
+            seed = ds.w;
+            o = mk(ot.x, ot.y, ot.z);
+            tmin = ot.w;
+            tmax = S.tmax;
+            ridx = 0.0f;
+        }
+        // the slots a later grab overwrites have been read (wave-ordered LDS accesses)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         q.next += __builtin_popcountll(given);
         q.taken += __builtin_popcountll(given);
         need &= ~given;
@@ -2545,13 +2632,18 @@ __device__ __forceinline__ void legacy_body(
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    uint8_t (*coop_tab)[kWave])
+    uint8_t (*coop_tab)[kWave], StartSlot (*start_slots)[kWave])
 {
     uint8_t *tab = coop_tab[threadIdx.x / kWave];
     const uint32_t lane = lane_id();
     const bool first_wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave) == 0;
     clock_stamp(counters, lane, first_wave, false);
     Queue q = queue_init(A);
+#if RVCP_LEGACY_PREFILL
+    StartSlot *slots = start_slots[threadIdx.x / kWave];
+    uint32_t q_base = q.next;                       // the static chunk, prefilled here
+    prefill_starts(A, q_base, q.end - q.next, lane, slots);
+#endif
     const float sppf = (float)A.spp;
     const float inv_spp = rcp_ieee(sppf);     // divs_y's shared reciprocal
     const float inv_rr = rcp_ieee(A.rr);
@@ -2608,11 +2700,17 @@ __device__ __forceinline__ void legacy_body(
             {   // take new pixels from the frame queue (wave-uniform control flow)
                 bool got;
                 uint32_t np = pix;
+#if RVCP_LEGACY_PREFILL
+                queue_take_started(q, __ballot(need_pixel && !done), lane, A, counters, slots,
+                                   q_base, got, np, seed, ridx, ro, rd, rtmin, rtmax);
+#else
                 queue_take(q, __ballot(need_pixel && !done), lane, A, counters, got, np);
+#endif
                 if (got) {
                     pix = np;
-                    if (A.batch_cams) start_batch_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
-                    else start_pixel(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
+#if !RVCP_LEGACY_PREFILL
+                    start_any(A, pix, seed, ridx, ro, rd, rtmin, rtmax);
+#endif
                     primary = true;
                     need_pixel = false;
                     k = 0;
@@ -2817,7 +2915,9 @@ __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void legacy_kernel(
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
 {
     __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
-    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
+    __shared__ StartSlot start_slots[kBlock / kWave][kWave];
+    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab,
+                start_slots);
 }
 #else
 // mode 2 with the scene-specialised triangle scan (rvcp_jit.cpp, RVCP_JIT_LEGACY)
@@ -2831,6 +2931,7 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters)
 {
     __shared__ uint8_t coop_tab[kBlock / kWave][kWave];
+    __shared__ StartSlot start_slots[kBlock / kWave][kWave];
 #ifdef RVCP_LEGACY_LDS_SCENE
     // scenes of at most 64 spheres, materials and faces (rvcp_jit.cpp, lds_fits): the per-lane
     // gathers of the hit record, the spheres and the scatter's material read LDS copies
@@ -2852,9 +2953,11 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
     }
     // (the sphere loop's wave-uniform records read from global memory by scalar loads instead,
     // beside the LDS copies for the per-lane gathers: 0.2855 vs 0.2814 ms, profiles/r04i_ab_m2c.log)
-    legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab);
+    legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab,
+                start_slots);
 #else
-    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab);
+    legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab,
+                start_slots);
 #endif
 }
 #endif
