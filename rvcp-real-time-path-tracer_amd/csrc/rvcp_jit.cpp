@@ -282,10 +282,18 @@ struct RangeMask {
 // value that does not depend on the running nearest hit, temporaries named <prefix>r<k>, then
 // the range mask, which reads the nearest hit as the previous commit left it) and its
 // acceptance (`accept`: the update); false when it can never accept.
+//
+// `inner` (the dual scan's shadow slot, emit_scan): the arithmetic is split at the range mask.
+// `decl` gets what t and the mask need (s, s1 = d x e2, den, s2 = s x e1, dot(s2, e2), f, t,
+// mask), `*inner` the rest (n1, n2, b1, b2, the compares) -- code the caller places inside a
+// wave-uniform `if (RVCP_SPEC_ANY(mask))`, so its temporaries go to `inner_seen` and never to
+// `seen` (a later test must not name a value a skipped block did not compute).  The same
+// operations on the same values as the unsplit order, so the same results.
 bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, uint32_t index,
                    const char *r, std::map<std::string, std::string> &seen,
                    std::map<std::string, RangeMask> &prev, bool *reused = nullptr,
-                   bool defer = false)
+                   bool defer = false, std::string *inner = nullptr,
+                   std::map<std::string, std::string> *inner_seen = nullptr)
 {
     Gen g;
     g.seen = &seen;
@@ -310,8 +318,11 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
         return false;
     }
     g.cross(s, e1, s2);                                                        // :251
-    const Val n1 = g.dot(s1, s);
-    const Val n2 = g.dot(s2, d);
+    Val n1, n2;
+    if (!inner) {
+        n1 = g.dot(s1, s);
+        n2 = g.dot(s2, d);
+    }
     const Val tt = g.dot(s2, e2);
     // the reciprocal of the signed denominator (its sign stays inside: v_rcp's symmetry is
     // not relied on); without the class check when the denominator is zero or a normal number
@@ -322,6 +333,16 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     // t = f * dot(s2, e2) (:255); a vanished dot leaves t = +-0 or NaN, rejected by
     // t >= t_min > 0 in both forms
     const std::string t = tt.kind == Val::kZero ? std::string("0.0f") : g.text(g.mul(f, tt));
+    size_t split_at = std::string::npos;
+    if (inner) {
+        // the rest after the mask: into *inner, its temporaries into inner_seen (a copy of the
+        // values visible here plus its own)
+        split_at = g.out.size();
+        *inner_seen = seen;
+        g.seen = inner_seen;
+        n1 = g.dot(s1, s);
+        n2 = g.dot(s2, d);
+    }
     std::string cond;
     auto add = [&](const std::string &c) { cond += (cond.empty() ? "" : " & ") + c; };
     std::string b1, b2;
@@ -332,7 +353,12 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
     if (!b1.empty() && !b2.empty()) add("(" + b1 + " + " + b2 + " <= 1.0f)");
     else if (!b1.empty()) add("(" + b1 + " <= 1.0f)");
     else if (!b2.empty()) add("(" + b2 + " <= 1.0f)");
-    decl += g.out;
+    if (inner) {
+        decl += g.out.substr(0, split_at);
+        *inner += g.out.substr(split_at);
+    } else {
+        decl += g.out;
+    }
     RangeMask &pm = prev[R];
     if (reused) *reused = !pm.name.empty() && pm.t == t;
     if (pm.name.empty() || pm.t != t) {
@@ -348,7 +374,7 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
         // the next test of this ray has the same t: keep the flag, apply both together
         const std::string c = g.prefix + "c";
         accept += "        " + c + " = " + cond + ";\n";
-        decl += "    bool " + c + ";\n";
+        (inner ? *inner : decl) += "    bool " + c + ";\n";
         pm.pending.emplace_back(c, index);
         return true;
     }
@@ -406,20 +432,79 @@ void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *c
     }
     std::map<std::string, std::string> seen;
     std::map<std::string, RangeMask> prev;
-    for (uint32_t u = 0; u < N; u++) {
+    // this ray's next emitted test after u, and whether it shares u's range mask
+    auto next_used = [&](uint32_t u) {
+        uint32_t v = u + (uint32_t)n_rays;
+        while (v < N && !used[v]) v += (uint32_t)n_rays;
+        return v;
+    };
+    auto defers = [&](uint32_t u) {
+        const uint32_t v = next_used(u);
+        return used[u] && v < N && reused[v];
+    };
+    // The single-ray scan (and the dual scan's path slot B): one test per commit region, or
+    // a run of tests sharing one range mask (an axis-aligned quad) in one region.
+    auto emit_plain = [&](uint32_t u) {
         std::string decl, accept;
         const std::string R(rays[u % (uint32_t)n_rays]);
-        uint32_t v = u + (uint32_t)n_rays;                  // this ray's next emitted test
-        while (v < N && !used[v]) v += (uint32_t)n_rays;
-        const bool defer = used[u] && v < N && reused[v];   // same region as its quad partner
+        const bool defer = defers(u);
         emit_triangle(decl, accept, tri[u / (uint32_t)n_rays], u / (uint32_t)n_rays, R.c_str(),
                       seen, prev, nullptr, defer);
         out += decl;
-        if (!used[u]) continue;
+        if (!used[u]) return;
         out += "    {\n" + accept + "    }\n";
-        if (defer) continue;
+        if (defer) return;
         out += R == "A" ? "    RVCP_SPEC_COMMIT1(btA);\n"
                         : "    RVCP_SPEC_COMMIT(bt" + R + ", best" + R + ");\n";
+    };
+    if (n_rays == 1) {
+        for (uint32_t u = 0; u < N; u++) emit_plain(u);
+        return;
+    }
+    // The dual scan: per triangle (run), the shadow slot A, then the path slot B.  Slot A's
+    // tests are emitted as runs of tests sharing one range mask, each split at the mask: the
+    // first test's t and mask, then `if (RVCP_SPEC_ANY(mask)) { the rest of the run }`.  A
+    // wave whose shadow rays all have t outside [t_min, btA] skips the barycentric half of the
+    // run -- every one of them would reject it (the mask is part of every acceptance), so the
+    // result is unchanged.  Shadow rays all end on a luminous face, which the scan tests first
+    // in the Cornell box (faces 0, 1), so btA is that short distance for most of the scan and
+    // the walls, floor and ceiling behind it are out of range for the whole wave.
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t uA = 2 * i;
+        if (!used[uA]) {                  // den identically zero: omitted for both rays
+            emit_plain(uA);
+            emit_plain(uA + 1);
+            i += 1;
+            continue;
+        }
+        std::vector<uint32_t> run = {uA};
+        while (defers(run.back())) run.push_back(next_used(run.back()));
+        // slot A: the run's first test split at its mask, the rest inside the skippable block
+        std::map<std::string, std::string> inner_seen;
+        std::string head, body, accept;
+        for (size_t k = 0; k < run.size(); k++) {
+            const uint32_t u = run[k];
+            const bool defer = k + 1 < run.size();
+            std::string decl, inner, acc;
+            if (k == 0) {
+                emit_triangle(decl, acc, tri[u / 2], u / 2, "A", seen, prev, nullptr, defer,
+                              &inner, &inner_seen);
+                head += decl;
+                body += inner;
+            } else {
+                emit_triangle(decl, acc, tri[u / 2], u / 2, "A", inner_seen, prev, nullptr, defer);
+                body += decl;
+            }
+            accept += acc;
+        }
+        const std::string &mask = prev["A"].name;
+        out += head;
+        out += "    if (RVCP_SPEC_ANY(" + mask + ")) {\n" + body + "    {\n" + accept + "    }\n    }\n";
+        out += "    RVCP_SPEC_COMMIT1(btA);\n";
+        // slot B: the same triangles, as before
+        for (uint32_t u : run) emit_plain(u + 1);
+        // (triangles of the run's span that slot A omitted are omitted for B too)
+        i = run.back() / 2 + 1;
     }
 }
 

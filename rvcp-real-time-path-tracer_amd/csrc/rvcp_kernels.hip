@@ -318,6 +318,14 @@ __device__ __forceinline__ bool dir_fast_ok(f3 d) {
 // the dual scan's shadow ray: its t only (spec_scan2 keeps no face index for slot A)
 #define RVCP_SPEC_COMMIT1(t) do { asm volatile("" : "+v"(t)); \
                                   __builtin_amdgcn_sched_barrier(0); } while (0)
+// RVCP_SPEC_ANY(mask): does any lane of the wave pass a shadow-slot run's range mask (the
+// generator's skippable blocks, rvcp_jit.cpp emit_scan)?  RVCP_SPEC_NO_SKIP (A/B only) runs
+// every block.
+#ifdef RVCP_SPEC_NO_SKIP
+#define RVCP_SPEC_ANY(q) ((void)(q), true)
+#else
+#define RVCP_SPEC_ANY(q) (__builtin_amdgcn_ballot_w64(q) != 0ull)
+#endif
 // The reciprocal of the specialised tests: rcp_scan, with its rare IEEE branch inline.  (A
 // branch-free variant that only flags non-normal reciprocals and re-runs the wave's scan with
 // the generic loop when a live ray was flagged is bit-exact too but measured 1.9x slower --
@@ -2279,6 +2287,9 @@ __device__ __forceinline__ void path_body(
                 // A): a nearest t other than t_max is a hit; t_max itself (a miss, or a hit at
                 // exactly t_max -- neither occurs in a closed room) is settled by the generic
                 // scan of the wave's shadow rays, which finds the same nearest hit
+                // a lane without a shadow ray takes no part in the shadow slot's skippable
+                // blocks: its mask is false whatever its stale ray (btA below t_min)
+                if (!hasA) btA = -1.0f;
                 spec_scan2(a_o, a_d, b_o, b_d, A.t_min, btA, btB, bestB);
             } else
 #endif

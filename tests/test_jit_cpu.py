@@ -53,6 +53,7 @@ static inline bool dir_grain_ok(f3 d) {       // the kernel's guard (rvcp_kernel
     return true;
 }
 #define RVCP_SPEC_COMMIT(t, i) ((void)0)
+#define RVCP_SPEC_ANY(q) (q)          // one lane: the block runs iff this ray's mask holds
 #define RVCP_SPEC_COMMIT1(t) ((void)0)
 """
 DRIVER = r"""
