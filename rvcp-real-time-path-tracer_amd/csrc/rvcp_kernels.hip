@@ -1677,6 +1677,25 @@ __device__ __forceinline__ void scan_generic2(const TriRecord *__restrict__ tri,
     for (uint32_t i = 0; i < n; ++i) {
         const TriRecord T = tri[i];
         float tA, tB;
+#ifndef RVCP_SPEC_NO_SKIP
+        if (!SINGLE) {
+            // the shadow slot as the specialised scan runs it (rvcp_jit.cpp emit_scan): t and its
+            // range mask first, the barycentric half only when some lane of the wave is in range
+            // (every other lane would reject on the mask); the same operations on the same values
+            const f3 s = mk(a_o.x - T.v0[0], a_o.y - T.v0[1], a_o.z - T.v0[2]);
+            const f3 e1 = ld3(T.e1);
+            const f3 s1 = cross(a_d, ld3(T.e2));
+            const f3 s2 = cross(s, e1);
+            const float f = FAST ? rcp_scan_fast(dot(s1, e1)) : rcp_scan(dot(s1, e1));
+            const float t = f * dot(s2, ld3(T.e2));
+            const bool q = (t >= tmin) & (t <= btA);
+            if (__builtin_amdgcn_ballot_w64(q) != 0ull) {
+                const float b1 = f * dot(s1, s);
+                const float b2 = f * dot(s2, a_d);
+                if ((b1 >= 0.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f) & q) btA = t;
+            }
+        } else
+#endif
         if (tri_accept<FAST>(T, a_o, a_d, tmin, btA, tA)) {
             btA = tA;
             if (SINGLE) bestA = (int)i;
@@ -2294,7 +2313,9 @@ __device__ __forceinline__ void path_body(
             } else
 #endif
             {
-            // the generic loop keeps no face index for the shadow ray either (as spec_scan2)
+            // the generic loop keeps no face index for the shadow ray either (as spec_scan2),
+            // and a lane without a shadow ray takes no part in its skips (btA below t_min)
+            if (!SINGLE && !hasA) btA = -1.0f;
             if (A.rcp_fast && !__any((hasA && !dir_fast_ok(a_d)) || (hasB && !dir_fast_ok(b_d))))
                 scan_generic2<true, SINGLE>(tri, A.n_faces, a_o, a_d, b_o, b_d, A.t_min, btA, bestA, btB, bestB);
             else
