@@ -415,7 +415,7 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
 // tests between them form one region, so the compiler can merge the two acceptances of a ray
 // (both write the same t) into one select of bt.
 void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *const *rays,
-               int n_rays)
+               int n_rays, bool skip_b = false)
 {
     const uint32_t N = n * (uint32_t)n_rays;
     std::vector<char> used(N), reused(N);
@@ -469,6 +469,31 @@ void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *c
     // result is unchanged.  Shadow rays all end on a luminous face, which the scan tests first
     // in the Cornell box (faces 0, 1), so btA is that short distance for most of the scan and
     // the walls, floor and ceiling behind it are out of range for the whole wave.
+    // a run of one ray's tests, split at the first test's mask into a skippable block
+    auto emit_split_run = [&](const std::vector<uint32_t> &run, const char *R) {
+        std::map<std::string, std::string> inner_seen;
+        std::string head, body, accept;
+        for (size_t k = 0; k < run.size(); k++) {
+            const uint32_t u = run[k];
+            const bool defer = k + 1 < run.size();
+            std::string decl, inner, acc;
+            if (k == 0) {
+                emit_triangle(decl, acc, tri[u / 2], u / 2, R, seen, prev, nullptr, defer,
+                              &inner, &inner_seen);
+                head += decl;
+                body += inner;
+            } else {
+                emit_triangle(decl, acc, tri[u / 2], u / 2, R, inner_seen, prev, nullptr, defer);
+                body += decl;
+            }
+            accept += acc;
+        }
+        const std::string &mask = prev[R].name;
+        const std::string r(R);
+        out += head;
+        out += "    if (RVCP_SPEC_ANY(" + mask + ")) {\n" + body + "    {\n" + accept + "    }\n    }\n";
+        out += r == "A" ? "    RVCP_SPEC_COMMIT1(btA);\n" : "    RVCP_SPEC_COMMIT(bt" + r + ", best" + r + ");\n";
+    };
     for (uint32_t i = 0; i < n;) {
         const uint32_t uA = 2 * i;
         if (!used[uA]) {                  // den identically zero: omitted for both rays
@@ -479,30 +504,17 @@ void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *c
         }
         std::vector<uint32_t> run = {uA};
         while (defers(run.back())) run.push_back(next_used(run.back()));
-        // slot A: the run's first test split at its mask, the rest inside the skippable block
-        std::map<std::string, std::string> inner_seen;
-        std::string head, body, accept;
-        for (size_t k = 0; k < run.size(); k++) {
-            const uint32_t u = run[k];
-            const bool defer = k + 1 < run.size();
-            std::string decl, inner, acc;
-            if (k == 0) {
-                emit_triangle(decl, acc, tri[u / 2], u / 2, "A", seen, prev, nullptr, defer,
-                              &inner, &inner_seen);
-                head += decl;
-                body += inner;
-            } else {
-                emit_triangle(decl, acc, tri[u / 2], u / 2, "A", inner_seen, prev, nullptr, defer);
-                body += decl;
-            }
-            accept += acc;
+        emit_split_run(run, "A");
+        // slot B: the same triangles, as before (or split too: skip_b, an experiment knob --
+        // path rays rarely leave a whole wave out of range, and the split costs slot B the
+        // sharing of values across tests)
+        if (skip_b) {
+            std::vector<uint32_t> runB;
+            for (uint32_t u : run) runB.push_back(u + 1);
+            emit_split_run(runB, "B");
+        } else {
+            for (uint32_t u : run) emit_plain(u + 1);
         }
-        const std::string &mask = prev["A"].name;
-        out += head;
-        out += "    if (RVCP_SPEC_ANY(" + mask + ")) {\n" + body + "    {\n" + accept + "    }\n    }\n";
-        out += "    RVCP_SPEC_COMMIT1(btA);\n";
-        // slot B: the same triangles, as before
-        for (uint32_t u : run) emit_plain(u + 1);
         // (triangles of the run's span that slot A omitted are omitted for B too)
         i = run.back() / 2 + 1;
     }
@@ -607,7 +619,7 @@ bool jit_scene_in_range(const TriRecord *tri, uint32_t n)
     return true;
 }
 
-std::string jit_scan_source(const TriRecord *tri, uint32_t n)
+std::string jit_scan_source(const TriRecord *tri, uint32_t n, bool skip_b)
 {
     // RVCP_F32(bits): the triangle's float by its bit pattern; RVCP_SPEC_COMMIT(t, i): the
     // test's result is final here (on the GPU an empty asm on the two registers plus a
@@ -622,7 +634,7 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n)
     out += "}\n";
     out += "__device__ __forceinline__ void spec_scan2(f3 oA, f3 dA, f3 oB, f3 dB, float tmin, "
            "float &btA, float &btB, int &bestB) {\n";
-    emit_scan(out, tri, n, two, 2);
+    emit_scan(out, tri, n, two, 2, skip_b);
     out += "}\n";
     return out;
 }
@@ -662,6 +674,18 @@ std::vector<std::string> jit_extra_flags()
     }
 #endif
     return extra;
+}
+
+// Experiment knob (debug build only, like jit_extra_flags): split the dual scan's path slot B
+// into skippable runs as well (RVCP_DEBUG_SPEC_SKIP_B=1).
+bool jit_skip_b()
+{
+#ifdef RVCP_DEBUG_KNOBS
+    const char *e = std::getenv("RVCP_DEBUG_SPEC_SKIP_B");
+    return e && *e == '1';
+#else
+    return false;
+#endif
 }
 
 namespace {
@@ -763,7 +787,7 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
 #endif
     std::string key_flags;
     for (const std::string &x : jit_extra_flags()) key_flags += " " + x;
-    const std::string scan = jit_scan_source(tri, n) +
+    const std::string scan = jit_scan_source(tri, n, jit_skip_b()) +
         (legacy ? "// +legacy " + std::to_string(legacy_waves) + (lds_scene ? " lds" : "") + "\n"
                 : std::string()) +
         (key_flags.empty() ? std::string() : "// +flags" + key_flags + "\n");
@@ -857,12 +881,12 @@ extern "C" int rvcp_internal_jit_compile_check(const void *tri_records, uint32_t
 
 // The generated scan source for n triangle records (for inspection): writes at most cap bytes
 // including the terminator and returns the full length.
-extern "C" size_t rvcp_internal_jit_scan_source(const void *tri_records, uint32_t n, char *out,
-                                                size_t cap)
+extern "C" size_t rvcp_internal_jit_scan_source_opt(const void *tri_records, uint32_t n,
+                                                    int skip_b, char *out, size_t cap)
 {
     try {
-        const std::string s =
-            rvcp::jit_scan_source(static_cast<const rvcp::TriRecord *>(tri_records), n);
+        const std::string s = rvcp::jit_scan_source(
+            static_cast<const rvcp::TriRecord *>(tri_records), n, skip_b != 0);
         if (out && cap) {
             std::strncpy(out, s.c_str(), cap - 1);
             out[cap - 1] = '\0';
@@ -871,4 +895,10 @@ extern "C" size_t rvcp_internal_jit_scan_source(const void *tri_records, uint32_
     } catch (...) {
         return 0;
     }
+}
+
+extern "C" size_t rvcp_internal_jit_scan_source(const void *tri_records, uint32_t n, char *out,
+                                                size_t cap)
+{
+    return rvcp_internal_jit_scan_source_opt(tri_records, n, 0, out, cap);
 }

@@ -97,20 +97,20 @@ def _tri_records(positions):
     return rec
 
 
-def _scan_source(rec):
+def _scan_source(rec, skip_b=False):
     L = rvcp_amd.abi.load()
-    fn = L.rvcp_internal_jit_scan_source
+    fn = L.rvcp_internal_jit_scan_source_opt
     fn.restype = ctypes.c_size_t
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
-    n = fn(rec.ctypes.data, len(rec), None, 0)
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    n = fn(rec.ctypes.data, len(rec), int(skip_b), None, 0)
     buf = ctypes.create_string_buffer(n + 1)
-    fn(rec.ctypes.data, len(rec), buf, n + 1)
+    fn(rec.ctypes.data, len(rec), int(skip_b), buf, n + 1)
     return buf.value.decode()
 
 
-def _build(tmp_path, rec, name):
+def _build(tmp_path, rec, name, skip_b=False):
     src = tmp_path / f"{name}.cpp"
-    src.write_text(PRELUDE + _scan_source(rec) + DRIVER)
+    src.write_text(PRELUDE + _scan_source(rec, skip_b) + DRIVER)
     so = tmp_path / f"{name}.so"
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                     "-mfma", "-fno-fast-math", "-o", str(so), str(src)], check=True)
@@ -486,3 +486,22 @@ def test_generated_scan_fuzz_scenes_bitexact(tmp_path, seed):
     rays = np.concatenate([_adversarial_rays(pos, rng, 300), _grain_edge_rays(pos, rng, 150)])
     _check(lib, pos, rays, tmin=kw["ray_t_min"], tmax=kw["ray_t_max"])
     assert lib.fast_rcp_violations() == 0, desc
+
+
+def test_generated_scan_skippable_runs_bitexact(tmp_path):
+    """The dual scan's skippable runs (round 5): slot A always, slot B with the experiment knob
+    (RVCP_DEBUG_SPEC_SKIP_B).  Every run is split at its first test's range mask; on one lane the
+    block runs iff that lane's mask holds, so this checks that the split keeps every value and
+    every acceptance: Cornell and two fuzz scenes, adversarial rays, both slots against the oracle."""
+    from fuzz_scenes import fuzz_scene, positions
+    import re
+    cases = [("cornell", _cornell_positions())] + [(f"fuzz{k}", positions(fuzz_scene(k)[0])) for k in (2, 13)]
+    for name, pos in cases:
+        rec = _tri_records(pos)
+        for skip_b in (False, True):
+            src = _scan_source(rec, skip_b)
+            runs_a = len(re.findall(r"RVCP_SPEC_ANY\(t\d+A_q\)", src))
+            runs_b = len(re.findall(r"RVCP_SPEC_ANY\(t\d+B_q\)", src))
+            assert runs_a > 0 and (runs_b > 0) == skip_b, (name, skip_b, runs_a, runs_b)
+            lib = _build(tmp_path, rec, f"{name}_{int(skip_b)}", skip_b)
+            _check(lib, pos, _adversarial_rays(pos, np.random.default_rng(5), 300))
