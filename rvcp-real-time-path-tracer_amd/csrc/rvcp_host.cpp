@@ -15,7 +15,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <exception>
 #include <mutex>
 #include <new>
@@ -1258,6 +1260,13 @@ static int impl_rccl_unique_id(uint8_t *out_id)
     return RVCP_OK;
 }
 
+// debug build only (tools/rccl_timeout_diag.py): stage stamps of the communicator paths on stderr
+static void rccl_trace(const char *what, long v = 0)
+{
+    static const bool on = RVCP_KNOB("RVCP_DEBUG_RCCL_TRACE") != nullptr;
+    if (on) std::fprintf(stderr, "rvcp rccl: %s %ld\n", what, v);
+}
+
 static Clock::time_point comm_deadline(const rvcp_ctx_t *ctx)
 {
     return ctx->comm_timeout_ms ? Clock::now() + std::chrono::milliseconds(ctx->comm_timeout_ms)
@@ -1267,17 +1276,23 @@ static Clock::time_point comm_deadline(const rvcp_ctx_t *ctx)
 // Abort ctx's communicator (ours) after a deadline or an asynchronous error: ncclCommAbort
 // raises RCCL's abort flag, which its kernels poll in every wait loop, so a gather stuck on a
 // peer that never comes finishes and the streams drain; the context stays usable for
-// single-GPU renders.  A caller's communicator (rvcp_rccl_attach) is the caller's to abort.
+// single-GPU renders.  The abort itself runs on a detached thread: it also joins RCCL's own
+// threads, and a wait for a peer that never comes must not become a wait inside the abort.  A
+// caller's communicator (rvcp_rccl_attach) is the caller's to abort.
 static void abort_comm(rvcp_ctx_t *ctx)
 {
-    if (ctx->comm && ctx->comm_owned) (void)rccl_api().comm_abort(ctx->comm);
+    if (ctx->comm && ctx->comm_owned) {
+        const ncclComm_t c = ctx->comm;
+        rccl_trace("abort: detached ncclCommAbort");
+        std::thread([c] { (void)rccl_api().comm_abort(c); }).detach();
+    }
     if (ctx->comm_owned) ctx->comm = nullptr;
 }
 
 // Wait until a non-blocking communicator has finished its last call (ncclInProgress ->
 // ncclSuccess), bounded by `deadline`.  RVCP_E_TIMEOUT on expiry, RVCP_E_HIP on an RCCL error.
 static int wait_comm_ready(rvcp_ctx_t *ctx, ncclComm_t comm, Clock::time_point deadline,
-                    const char *what)
+                           const char *what)
 {
     const RcclApi &R = rccl_api();
     for (unsigned spin = 0;; spin++) {
@@ -1295,6 +1310,21 @@ static int wait_comm_ready(rvcp_ctx_t *ctx, ncclComm_t comm, Clock::time_point d
     }
 }
 
+// The communicator's creation runs on a worker thread: ncclCommInitRankConfig (blocking = 0)
+// and the poll of ncclCommGetAsyncError until the rendezvous completes.  The caller waits for
+// the worker with the deadline, so rvcp_rccl_init returns in time whatever RCCL does inside
+// (with its peer absent, the non-blocking call and its abort together did not return within the
+// 120 s limit of tests/test_gpu_rccl_timeout.py on this image's RCCL 2.27.7 when both ran on the
+// caller's thread); a worker left behind aborts its half-made communicator when it gets control
+// back (detached: the process never waits for it).
+struct CommJob {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclResult_t result = ncclSuccess;
+    ncclComm_t comm = nullptr;
+};
+
 static int impl_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, uint32_t rank)
 {
     if (!ctx) return RVCP_E_INVALID;
@@ -1306,25 +1336,63 @@ static int impl_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, ui
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
-    // non-blocking: the call returns at once (ncclInProgress) and the rendezvous is polled
-    // against the deadline, so a rank whose peers never join gets RVCP_E_TIMEOUT instead of
-    // blocking forever (a library older than this header reads only the fields it knows:
-    // `size` tells it how many there are)
-    ncclConfig_t conf = NCCL_CONFIG_INITIALIZER;
-    conf.blocking = 0;
     const Clock::time_point deadline = comm_deadline(ctx);
-    ncclComm_t comm = nullptr;
-    const ncclResult_t r = R.comm_init_rank_config(&comm, (int)world, uid, (int)rank, &conf);
-    if (r != ncclSuccess && r != ncclInProgress) {
-        if (comm) (void)R.comm_abort(comm);
-        return fail(ctx, RVCP_E_HIP, std::string("ncclCommInitRankConfig: ") + R.error_string(r));
+    auto job = std::make_shared<CommJob>();
+    const int dev = ctx->device;
+    std::thread([job, uid, world, rank, dev]() mutable {
+        const RcclApi &R = rccl_api();
+        (void)hipSetDevice(dev);
+        // non-blocking: a library older than this header reads only the fields it knows (`size`
+        // tells it how many there are)
+        ncclConfig_t conf = NCCL_CONFIG_INITIALIZER;
+        conf.blocking = 0;
+        ncclComm_t comm = nullptr;
+        rccl_trace("init worker: calling ncclCommInitRankConfig, world", (long)world);
+        ncclResult_t r = R.comm_init_rank_config(&comm, (int)world, uid, (int)rank, &conf);
+        rccl_trace("init worker: returned", (long)r);
+        for (unsigned spin = 0; r == ncclSuccess || r == ncclInProgress; spin++) {
+            ncclResult_t st = ncclInProgress;
+            if (!comm || R.get_async_error(comm, &st) != ncclSuccess) { r = ncclInternalError; break; }
+            if (st != ncclInProgress) { r = st; break; }
+            {
+                std::lock_guard<std::mutex> g(job->m);
+                if (job->abandoned) break;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(spin < 100 ? 20 : 1000));
+        }
+        bool keep;
+        {
+            std::lock_guard<std::mutex> g(job->m);
+            keep = !job->abandoned && r == ncclSuccess;
+            job->result = r;
+            if (keep) job->comm = comm;
+            job->done = true;
+        }
+        job->cv.notify_all();
+        if (!keep && comm) {
+            rccl_trace("init worker: ncclCommAbort");
+            (void)R.comm_abort(comm);
+            rccl_trace("init worker: ncclCommAbort returned");
+        }
+    }).detach();
+    std::unique_lock<std::mutex> lk(job->m);
+    bool finished;
+    if (ctx->comm_timeout_ms == 0) {
+        job->cv.wait(lk, [&] { return job->done; });
+        finished = true;
+    } else {
+        finished = job->cv.wait_until(lk, deadline, [&] { return job->done; });
     }
-    const int rc = wait_comm_ready(ctx, comm, deadline, "ncclCommInitRankConfig");
-    if (rc != RVCP_OK) {
-        (void)R.comm_abort(comm);
-        return rc;
+    if (!finished) {
+        job->abandoned = true;
+        rccl_trace("init: deadline, worker abandoned");
+        return fail(ctx, RVCP_E_TIMEOUT, "ncclCommInitRankConfig: no rendezvous within " +
+                    std::to_string(ctx->comm_timeout_ms) + " ms (a peer rank missing or failed); "
+                    "the half-made communicator is aborted");
     }
-    ctx->comm = comm;
+    if (job->result != ncclSuccess)
+        return fail(ctx, RVCP_E_HIP, std::string("ncclCommInitRankConfig: ") + R.error_string(job->result));
+    ctx->comm = job->comm;
     ctx->comm_owned = true;
     ctx->comm_world = world;
     ctx->comm_rank = rank;

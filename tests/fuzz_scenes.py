@@ -138,15 +138,16 @@ def fuzz_scene(seed):
     # the camera: inside the room (often inside the clutter) or outside the open front
     inside = rng.random() < 0.5
     pos = (rng.uniform(-6, 6, 3).astype(np.float32) * g if inside
-           else np.float32([0, 0, -24]) * g + rng.uniform(-2, 2, 3).astype(np.float32) * g)
+           else np.float32([0, 0, -12]) * g + rng.uniform(-2, 2, 3).astype(np.float32) * g)
     look = rng.uniform(-4, 4, 3).astype(np.float32) * g
     if np.allclose(look, pos):
         look = pos + np.float32([0, 0, 1]) * g
     t_cap = 16777214.0                      # below 2^24 (rvcp_config_t.ray_t_max)
     pos, look = (pos + off).astype(np.float32), (look + off).astype(np.float32)
-    # (the primary ray's t_far x t_coef stays below 2^24 too: t_coef < 4 at these fields of view)
+    # (the primary ray's t_far x t_coef stays below 2^24 too: t_coef < 1.7 at these fields of
+    # view, rvcp_host.cpp primary_t_range_ok; 2^23 still reaches across a 2^22 room)
     cam = rvcp_amd.Camera.new(pos, look, float(np.float32(0.1) * g),
-                              min(float(np.float32(1e5) * s), 2.0 ** 22),
+                              min(float(np.float32(1e5) * s), 2.0 ** 23),
                               float(rng.uniform(35, 80)), 1.0, 1.0)
     mesh = rvcp_amd.scene.ArrayMesh(verts, faces)
     sc = rvcp_amd.Scene(cam, materials, [], mesh)

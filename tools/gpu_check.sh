@@ -113,7 +113,7 @@ for s in $STEPS; do
         pooltests) run pooltests 600 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         fuzz) run pytest_fuzz 600 python -u -m pytest tests/test_gpu_spec_fuzz.py -m gpu -x -q --timeout 200 --timeout-method thread ;;
         spec2) run pytest_spec2 600 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not c5" ;;
-        rccldiag) run rccl_diag 120 env NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP,ENV python -u tools/rccl_timeout_diag.py 3000 ;;
+        rccldiag) run rccl_diag 90 env RVCP_LIB=$DBG RVCP_DEBUG_RCCL_TRACE=1 NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP,ENV python -u tools/rccl_timeout_diag.py 3000 ;;
         abitest) run pytest_abi 300 python -u -m pytest tests/test_gpu_abi.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         rccltest) run pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl_timeout.py tests/test_gpu_batch.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
         c6test) run pytest_c6 900 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 600 --timeout-method thread -k c6 ;;

@@ -1,9 +1,11 @@
 """Diagnostic (GPU box): rvcp_rccl_init(world = 2, rank = 0) with no peer, each stage stamped,
 to see where a non-blocking RCCL init / abort spends its time.  Run with NCCL_DEBUG=INFO."""
+import os
 import sys
 import time
 
-import rvcp_amd
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import rvcp_amd  # noqa: E402
 
 t00 = time.perf_counter()
 
