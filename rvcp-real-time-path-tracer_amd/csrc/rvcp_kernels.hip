@@ -1209,6 +1209,9 @@ __device__ __forceinline__ void flush_wave_counters(unsigned long long *__restri
 // quotient x 0.1 GHz (rvcp_stats_t::shader_clock_ghz), the wave-time-weighted mean clock.
 __device__ __forceinline__ void clock_stamp(unsigned long long *__restrict__ counters,
                                             uint32_t lane, bool first_wave, bool end) {
+#ifdef RVCP_NO_CLOCK_STAMP
+    return;         // A/B only (tools/ab_cases/stamp.txt)
+#endif
     if (!first_wave) return;
     const unsigned long long c = __builtin_amdgcn_s_memtime();
     const unsigned long long r = __builtin_amdgcn_s_memrealtime();
