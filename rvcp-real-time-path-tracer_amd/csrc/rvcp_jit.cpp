@@ -258,11 +258,16 @@ struct Gen {
     }
     // dot = fma(z, z', fma(y, y', x*x')), cross_i = fma(a_j, b_k, -(a_k*b_j)): DESIGN.md §3.1
     Val dot(const Val *a, const Val *b) { return fma(a[2], b[2], fma(a[1], b[1], mul(a[0], b[0]))); }
+    // component k of a x b; a component of a whose partners in b are both zero is not read
+    // (it may be a placeholder zero: the terms it would enter are dropped anyway)
+    Val cross_at(const Val *a, const Val *b, int k)
+    {
+        const int i = (k + 1) % 3, j = (k + 2) % 3;
+        return fma(a[i], b[j], neg(mul(a[j], b[i])));
+    }
     void cross(const Val *a, const Val *b, Val *r)
     {
-        r[0] = fma(a[1], b[2], neg(mul(a[2], b[1])));
-        r[1] = fma(a[2], b[0], neg(mul(a[0], b[2])));
-        r[2] = fma(a[0], b[1], neg(mul(a[1], b[0])));
+        for (int k = 0; k < 3; k++) r[k] = cross_at(a, b, k);
     }
 };
 
@@ -293,7 +298,7 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
                    const char *r, std::map<std::string, std::string> &seen,
                    std::map<std::string, RangeMask> &prev, bool *reused = nullptr,
                    bool defer = false, std::string *inner = nullptr,
-                   std::map<std::string, std::string> *inner_seen = nullptr)
+                   std::map<std::string, std::string> *inner_seen = nullptr, bool eager = false)
 {
     Gen g;
     g.seen = &seen;
@@ -309,21 +314,60 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
         e1[k] = lit_or_zero(T.e1[k]);
         e2[k] = lit_or_zero(T.e2[k]);
     }
-    Val s[3] = {g.sub(o[0], v0[0]), g.sub(o[1], v0[1]), g.sub(o[2], v0[2])};   // :249
-    Val s1[3], s2[3];
-    g.cross(d, e2, s1);                                                        // :250
-    const Val den = g.dot(s1, e1);                                             // :254
+    Val s[3], s1[3], s2[3];
+    Val n1, n2, den, tt;
+    // `inner`: s, s1 = d x e2 and s2 = s x e1 component by component, as t and the mask need
+    // them (den reads the components of s1 where e1 is non-zero, dot(s2, e2) those of s2 where
+    // e2 is), so that the ones only n1 and n2 read are computed after the split, inside the
+    // skippable block -- the same operations on the same operands in either order
+    bool have_s[3] = {}, have_s1[3] = {}, have_s2[3] = {};
+    auto S = [&](int k) {
+        if (!have_s[k]) { s[k] = g.sub(o[k], v0[k]); have_s[k] = true; }
+        return s[k];
+    };
+    auto S1 = [&](int k) {
+        if (!have_s1[k]) { s1[k] = g.cross_at(d, e2, k); have_s1[k] = true; }
+        return s1[k];
+    };
+    auto S2 = [&](int k) {
+        if (!have_s2[k]) {
+            const int i = (k + 1) % 3, j = (k + 2) % 3;
+            Val a[3];
+            if (e1[j].kind != Val::kZero) a[i] = S(i);
+            if (e1[i].kind != Val::kZero) a[j] = S(j);
+            s2[k] = g.cross_at(a, e1, k);
+            have_s2[k] = true;
+        }
+        return s2[k];
+    };
+    const bool lazy = inner && !eager;      // eager: the round-5 (r05h) order, an A/B knob
+    if (lazy) {
+        Val s1p[3];
+        for (int k = 0; k < 3; k++) s1p[k] = e1[k].kind != Val::kZero ? S1(k) : zero();
+        den = g.dot(s1p, e1);                                                  // :254
+    } else {
+        for (int k = 0; k < 3; k++) S(k);                                      // :249
+        g.cross(d, e2, s1);                                                    // :250
+        have_s1[0] = have_s1[1] = have_s1[2] = true;
+        den = g.dot(s1, e1);                                                   // :254
+    }
     if (den.kind == Val::kZero) {
         decl += g.out;          // its temporaries may be named by a later test (`seen`)
         return false;
     }
-    g.cross(s, e1, s2);                                                        // :251
-    Val n1, n2;
-    if (!inner) {
-        n1 = g.dot(s1, s);
-        n2 = g.dot(s2, d);
+    if (lazy) {
+        Val s2p[3];
+        for (int k = 0; k < 3; k++) s2p[k] = e2[k].kind != Val::kZero ? S2(k) : zero();
+        tt = g.dot(s2p, e2);
+    } else {
+        g.cross(s, e1, s2);                                                    // :251
+        have_s2[0] = have_s2[1] = have_s2[2] = true;
+        if (!inner) {
+            n1 = g.dot(s1, s);
+            n2 = g.dot(s2, d);
+        }
+        tt = g.dot(s2, e2);
     }
-    const Val tt = g.dot(s2, e2);
     // the reciprocal of the signed denominator (its sign stays inside: v_rcp's symmetry is
     // not relied on); without the class check when the denominator is zero or a normal number
     // whose reciprocal is normal (grain >= -126, mag <= 126: see Val)
@@ -340,8 +384,12 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
         split_at = g.out.size();
         *inner_seen = seen;
         g.seen = inner_seen;
-        n1 = g.dot(s1, s);
-        n2 = g.dot(s2, d);
+        Val s1f[3], sf[3], s2f[3];
+        for (int k = 0; k < 3; k++) s1f[k] = S1(k);
+        for (int k = 0; k < 3; k++) sf[k] = s1f[k].kind != Val::kZero ? S(k) : zero();
+        n1 = g.dot(s1f, sf);
+        for (int k = 0; k < 3; k++) s2f[k] = S2(k);
+        n2 = g.dot(s2f, d);
     }
     std::string cond;
     auto add = [&](const std::string &c) { cond += (cond.empty() ? "" : " & ") + c; };
@@ -415,8 +463,9 @@ bool emit_triangle(std::string &decl, std::string &accept, const TriRecord &T, u
 // tests between them form one region, so the compiler can merge the two acceptances of a ray
 // (both write the same t) into one select of bt.
 void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *const *rays,
-               int n_rays, bool skip_b = false)
+               int n_rays, unsigned opts = 0)
 {
+    const bool skip_b = (opts & kScanSkipB) != 0, eager = (opts & kScanEagerSplit) != 0;
     const uint32_t N = n * (uint32_t)n_rays;
     std::vector<char> used(N), reused(N);
     {   // dry run: which tests are emitted and which reuse their ray's previous range mask
@@ -479,7 +528,7 @@ void emit_scan(std::string &out, const TriRecord *tri, uint32_t n, const char *c
             std::string decl, inner, acc;
             if (k == 0) {
                 emit_triangle(decl, acc, tri[u / 2], u / 2, R, seen, prev, nullptr, defer,
-                              &inner, &inner_seen);
+                              &inner, &inner_seen, eager);
                 head += decl;
                 body += inner;
             } else {
@@ -619,7 +668,7 @@ bool jit_scene_in_range(const TriRecord *tri, uint32_t n)
     return true;
 }
 
-std::string jit_scan_source(const TriRecord *tri, uint32_t n, bool skip_b)
+std::string jit_scan_source(const TriRecord *tri, uint32_t n, unsigned opts)
 {
     // RVCP_F32(bits): the triangle's float by its bit pattern; RVCP_SPEC_COMMIT(t, i): the
     // test's result is final here (on the GPU an empty asm on the two registers plus a
@@ -634,7 +683,7 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n, bool skip_b)
     out += "}\n";
     out += "__device__ __forceinline__ void spec_scan2(f3 oA, f3 dA, f3 oB, f3 dB, float tmin, "
            "float &btA, float &btB, int &bestB) {\n";
-    emit_scan(out, tri, n, two, 2, skip_b);
+    emit_scan(out, tri, n, two, 2, opts);
     out += "}\n";
     return out;
 }
@@ -676,16 +725,19 @@ std::vector<std::string> jit_extra_flags()
     return extra;
 }
 
-// Experiment knob (debug build only, like jit_extra_flags): split the dual scan's path slot B
-// into skippable runs as well (RVCP_DEBUG_SPEC_SKIP_B=1).
-bool jit_skip_b()
+// Experiment knobs (debug build only, like jit_extra_flags): split the dual scan's path slot B
+// into skippable runs as well (RVCP_DEBUG_SPEC_SKIP_B=1); compute the shadow slot's s1 and s2
+// whole before its split, as round 5's first form did (RVCP_DEBUG_SPEC_EAGER=1).
+unsigned jit_scan_opts()
 {
+    unsigned opts = 0;
 #ifdef RVCP_DEBUG_KNOBS
     const char *e = std::getenv("RVCP_DEBUG_SPEC_SKIP_B");
-    return e && *e == '1';
-#else
-    return false;
+    if (e && *e == '1') opts |= kScanSkipB;
+    e = std::getenv("RVCP_DEBUG_SPEC_EAGER");
+    if (e && *e == '1') opts |= kScanEagerSplit;
 #endif
+    return opts;
 }
 
 namespace {
@@ -787,7 +839,7 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
 #endif
     std::string key_flags;
     for (const std::string &x : jit_extra_flags()) key_flags += " " + x;
-    const std::string scan = jit_scan_source(tri, n, jit_skip_b()) +
+    const std::string scan = jit_scan_source(tri, n, jit_scan_opts()) +
         (legacy ? "// +legacy " + std::to_string(legacy_waves) + (lds_scene ? " lds" : "") + "\n"
                 : std::string()) +
         (key_flags.empty() ? std::string() : "// +flags" + key_flags + "\n");
@@ -882,11 +934,11 @@ extern "C" int rvcp_internal_jit_compile_check(const void *tri_records, uint32_t
 // The generated scan source for n triangle records (for inspection): writes at most cap bytes
 // including the terminator and returns the full length.
 extern "C" size_t rvcp_internal_jit_scan_source_opt(const void *tri_records, uint32_t n,
-                                                    int skip_b, char *out, size_t cap)
+                                                    int opts, char *out, size_t cap)
 {
     try {
         const std::string s = rvcp::jit_scan_source(
-            static_cast<const rvcp::TriRecord *>(tri_records), n, skip_b != 0);
+            static_cast<const rvcp::TriRecord *>(tri_records), n, (unsigned)opts);
         if (out && cap) {
             std::strncpy(out, s.c_str(), cap - 1);
             out[cap - 1] = '\0';

@@ -33,7 +33,9 @@ bool scan_rcp_fast_scene(const TriRecord *tri, uint32_t n);
 // Extra hipRTC options (debug build only; empty in the product library).
 std::vector<std::string> jit_extra_flags();
 // The generated scan (spec_scan1 / spec_scan2) for n triangle records.
-std::string jit_scan_source(const TriRecord *tri, uint32_t n, bool skip_b = false);
+// opts: kScanSkipB | kScanEagerSplit (experiment knobs, jit_scan_opts)
+constexpr unsigned kScanSkipB = 1u, kScanEagerSplit = 2u;
+std::string jit_scan_source(const TriRecord *tri, uint32_t n, unsigned opts = 0);
 // Compile rvcp_kernels.hip with the given scan for gfx950 (hipRTC); 0 or -1 with err set.
 // `legacy` also builds the mode-2 kernel (RVCP_JIT_LEGACY).
 // `lds_scene`: the mode-2 kernel copies the scene into LDS (RVCP_LEGACY_LDS_SCENE).

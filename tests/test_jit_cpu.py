@@ -97,20 +97,20 @@ def _tri_records(positions):
     return rec
 
 
-def _scan_source(rec, skip_b=False):
+def _scan_source(rec, opts=0):
     L = rvcp_amd.abi.load()
     fn = L.rvcp_internal_jit_scan_source_opt
     fn.restype = ctypes.c_size_t
     fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
-    n = fn(rec.ctypes.data, len(rec), int(skip_b), None, 0)
+    n = fn(rec.ctypes.data, len(rec), int(opts), None, 0)
     buf = ctypes.create_string_buffer(n + 1)
-    fn(rec.ctypes.data, len(rec), int(skip_b), buf, n + 1)
+    fn(rec.ctypes.data, len(rec), int(opts), buf, n + 1)
     return buf.value.decode()
 
 
-def _build(tmp_path, rec, name, skip_b=False):
+def _build(tmp_path, rec, name, opts=0):
     src = tmp_path / f"{name}.cpp"
-    src.write_text(PRELUDE + _scan_source(rec, skip_b) + DRIVER)
+    src.write_text(PRELUDE + _scan_source(rec, opts) + DRIVER)
     so = tmp_path / f"{name}.so"
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                     "-mfma", "-fno-fast-math", "-o", str(so), str(src)], check=True)
@@ -498,10 +498,29 @@ def test_generated_scan_skippable_runs_bitexact(tmp_path):
     cases = [("cornell", _cornell_positions())] + [(f"fuzz{k}", positions(fuzz_scene(k)[0])) for k in (2, 13)]
     for name, pos in cases:
         rec = _tri_records(pos)
-        for skip_b in (False, True):
-            src = _scan_source(rec, skip_b)
+        head_ops = {}
+        for opts in (0, 1, 2):              # default; + slot B split; eager shadow split (r05h)
+            skip_b = bool(opts & 1)
+            src = _scan_source(rec, opts)
             runs_a = len(re.findall(r"RVCP_SPEC_ANY\(t\d+A_q\)", src))
             runs_b = len(re.findall(r"RVCP_SPEC_ANY\(t\d+B_q\)", src))
-            assert runs_a > 0 and (runs_b > 0) == skip_b, (name, skip_b, runs_a, runs_b)
-            lib = _build(tmp_path, rec, f"{name}_{int(skip_b)}", skip_b)
+            assert runs_a > 0 and (runs_b > 0) == skip_b, (name, opts, runs_a, runs_b)
+            head_ops[opts] = _unskippable_ops(src)
+            lib = _build(tmp_path, rec, f"{name}_{opts}", opts)
             _check(lib, pos, _adversarial_rays(pos, np.random.default_rng(5), 300))
+        # the default computes s1 / s2 components only n1 and n2 read inside the skippable block
+        assert head_ops[0] < head_ops[2], (name, head_ops)
+
+
+def _unskippable_ops(src):
+    """Arithmetic statements of the dual scan outside its skippable blocks."""
+    body = src[src.index("spec_scan2"):]
+    n, inside = 0, False
+    for line in body.splitlines():
+        if "RVCP_SPEC_ANY(" in line:
+            inside = True
+        elif line.startswith("    RVCP_SPEC_COMMIT"):
+            inside = False
+        elif line.strip().startswith("const float") and not inside:
+            n += 1
+    return n
