@@ -42,6 +42,14 @@ using namespace rvcp;
 #define RVCP_KNOB(name) ((const char *)nullptr)
 #endif
 
+// The specialised pre-pass (rvcp_spec_primary_kernel) with the specialised path kernels; the
+// debug build's RVCP_DEBUG_GENERIC_PREPASS=1 keeps the built-in one (A/B)
+static bool jit_spec_prepass()
+{
+    const char *e = RVCP_KNOB("RVCP_DEBUG_GENERIC_PREPASS");
+    return !(e && *e == '1');
+}
+
 // rvcp_rccl_init / rvcp_gather_wait give up after this long unless rvcp_rccl_set_timeout says
 // otherwise: far above a frame (C5 brute force, the slowest workload, 6.5 s) and far below
 // "forever", which is what a blocking ncclCommInitRank or an unbounded event wait gives when a
@@ -942,7 +950,9 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                                                  spec ? (void *)(A.variant == 6 ? jk->path6 : jk->path5)
                                                       : nullptr,
                                                  cams && frame_px <= kPrepassBatchMaxPixels
-                                                     ? ctx->d_cams : nullptr);
+                                                     ? ctx->d_cams : nullptr,
+                                                 spec && jit_spec_prepass() ? (void *)jk->primary
+                                                                            : nullptr);
                 }
                 if (spec) ctx->last_spec = true;
             } else {

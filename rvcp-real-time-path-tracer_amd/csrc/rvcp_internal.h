@@ -286,7 +286,8 @@ int rvcp_launch_games101(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri
                          uint32_t grid_blocks, void *stream);
 // args[0 .. n_frames): one FrameArgs per frame of the batch (pix_base = k x frame_stride);
 // one pre-pass per frame into one surface list, one path kernel, one tone map over
-// n_frames x frame_stride pixels (n_pixels when n_frames == 1)
+// n_frames x frame_stride pixels (n_pixels when n_frames == 1).  spec_path_fn / spec_pre_fn:
+// the scene-specialised path kernel and pre-pass (rvcp_jit.cpp), or null for the built-in ones
 int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_frames, uint32_t frame_stride,
                             const rvcp::TriRecord *tri,
                             const void *faces, const void *verts, const rvcp::MatRecord *mats,
@@ -295,7 +296,7 @@ int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_frames, uint
                             rvcp::SurfRecord *surf, const rvcp::FaceShade *shade,
                             const rvcp::Bvh4Node *bvh_nodes, const rvcp::TriRecord *bvh_tris,
                             uint32_t grid_blocks, void *stream, void *main_event,
-                            void *spec_path_fn, const float *cams);
+                            void *spec_path_fn, const float *cams, void *spec_pre_fn = nullptr);
 // Integrator RVCP_INTEGRATOR_LEGACY (ray_tracer.comp): materials / spheres are the raw
 // rvcp_material_t / rvcp_sphere_t arrays, unorm_t the UNORM8 threshold table.
 int rvcp_launch_legacy(const rvcp::FrameArgs *args, const rvcp::TriRecord *tri,

@@ -865,6 +865,10 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         err = "specialised kernels missing from the module";
         return nullptr;
     }
+    if (hipModuleGetFunction(&k->primary, k->module, "rvcp_spec_primary_kernel") != hipSuccess) {
+        err = "specialised pre-pass kernel missing from the module";
+        return nullptr;
+    }
     if (legacy && hipModuleGetFunction(&k->legacy, k->module, "rvcp_spec_legacy_kernel") != hipSuccess) {
         err = "specialised mode-2 kernel missing from the module";
         return nullptr;

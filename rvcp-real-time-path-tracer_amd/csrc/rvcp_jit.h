@@ -18,6 +18,7 @@ struct JitKernels {
     hipFunction_t path5 = nullptr;     // schedule 3 (5 waves per SIMD)
     hipFunction_t path6 = nullptr;     // schedule 6 (6 waves per SIMD)
     hipFunction_t legacy = nullptr;    // integrator mode 2 (modules compiled with `legacy`)
+    hipFunction_t primary = nullptr;   // the schedule-3/6 pre-pass with the specialised scan
     int blocks_per_cu5 = 0, blocks_per_cu6 = 0, blocks_per_cu_legacy = 0;
     ~JitKernels();
 };

@@ -323,6 +323,8 @@ __device__ __forceinline__ bool dir_fast_ok(f3 d) {
 // every block.
 #ifdef RVCP_SPEC_NO_SKIP
 #define RVCP_SPEC_ANY(q) ((void)(q), true)
+#elif defined(RVCP_SPEC_ISA_SKIP_ALL)      // tools/spec_isa.py only: the code a wave runs when
+#define RVCP_SPEC_ANY(q) ((void)(q), false) // every block is skipped (never a product build)
 #else
 #define RVCP_SPEC_ANY(q) (__builtin_amdgcn_ballot_w64(q) != 0ull)
 #endif
@@ -1555,6 +1557,7 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
     flush_counters(counters, lane, trav, iters);
 }
 
+#endif  // RVCP_JIT
 // ======================================================================================
 // Variant 3, kernel 1: primary pre-pass, one pixel per lane.  Traces every primary ray once
 // (all lanes busy, no divergence), finishes miss / light pixels in closed form (their samples
@@ -1563,8 +1566,8 @@ __global__ __launch_bounds__(kBlock) void games101_dual_kernel(
 // ======================================================================================
 constexpr uint32_t kPrimaryBlock = 256;   // one list append (global atomic) per block
 
-template <bool BVH>
-__global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
+template <bool BVH, bool SPEC>
+__device__ __forceinline__ void primary_body(
     FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
     const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
     const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
@@ -1596,7 +1599,15 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
         float bt = tmax;
         if (BVH) {
             bvh_nearest<false>(bvh_nodes, bvh_tris, A.bvh_root, nullptr, o, d, tmin, bt, best, A.bvh_n4, A.bvh_slots);
-        } else {
+        }
+#ifdef RVCP_SPEC_SCAN
+        // the scene-specialised scan (§4.7) where every primary ray of the wave is in its range
+        // (ray_in_range, t_min > 0), as the path kernels' scans
+        else if (SPEC && !__any(!(ray_in_range(o, d) && tmin > 0.0f))) {
+            spec_scan1(o, d, tmin, bt, best);
+        }
+#endif
+        else {
 #pragma unroll 2
             for (uint32_t i = 0; i < A.n_faces; ++i) {
                 float t;
@@ -1643,7 +1654,22 @@ __global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
     }
 }
 
-#endif  // RVCP_JIT
+#ifndef RVCP_JIT
+template <bool BVH>
+__global__ __launch_bounds__(kPrimaryBlock) void games101_primary_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
+    const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
+    const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
+    SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade,
+    const Bvh4Node *__restrict__ bvh_nodes, const TriRecord *__restrict__ bvh_tris,
+    const float *__restrict__ cams, uint32_t frame_stride)
+{
+    primary_body<BVH, false>(A, tri, faces, verts, mats, gamma_t, out_rgba, out_lin, counters,
+                             surf, shade, bvh_nodes, bvh_tris, cams, frame_stride);
+}
+#endif
+
 // ======================================================================================
 // Variant 3/4, kernel 2: the dual-ray machine over the surface pixels of the pre-pass.  Every
 // pixel starts with a surface event at its cached primary hit, so no iteration is spent on
@@ -2979,11 +3005,11 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
         auto cp = [](float4 *dst, const float4 *src, uint32_t n) {
             for (uint32_t e = threadIdx.x; e < n; e += kBlock) dst[e] = src[e];
         };
+        const uint32_t nm = A.n_mats < 64u ? A.n_mats : 64u;
         cp(reinterpret_cast<float4 *>(sh_tri), reinterpret_cast<const float4 *>(tri), 3u * A.n_faces);
         cp(reinterpret_cast<float4 *>(sh_shade), reinterpret_cast<const float4 *>(shade), 4u * A.n_faces);
         cp(reinterpret_cast<float4 *>(sh_sph), reinterpret_cast<const float4 *>(sph), 2u * A.n_spheres);
-        cp(reinterpret_cast<float4 *>(sh_mat), reinterpret_cast<const float4 *>(mats),
-           2u * (A.n_mats < 64u ? A.n_mats : 64u));
+        cp(reinterpret_cast<float4 *>(sh_mat), reinterpret_cast<const float4 *>(mats), 2u * nm);
         __syncthreads();
     }
     // (the sphere loop's wave-uniform records read from global memory by scalar loads instead,
@@ -3001,6 +3027,19 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
 // Scene-specialised path kernels (rvcp_jit.cpp compiles this file with hipRTC, RVCP_JIT and
 // RVCP_SPEC_SCAN set): schedules 3 and 6 with the scan unrolled over the uploaded scene
 // (DESIGN.md §4.7).  extern "C" so that the host finds them by name in the module.
+// the pre-pass with the specialised scan (rvcp_launch_games101_v3's spec_pre_fn)
+extern "C" __global__ __launch_bounds__(kPrimaryBlock) void rvcp_spec_primary_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
+    const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
+    const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
+    SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade,
+    const Bvh4Node *__restrict__ bvh_nodes, const TriRecord *__restrict__ bvh_tris,
+    const float *__restrict__ cams, uint32_t frame_stride)
+{
+    primary_body<false, true>(A, tri, faces, verts, mats, gamma_t, out_rgba, out_lin, counters,
+                              surf, shade, bvh_nodes, bvh_tris, cams, frame_stride);
+}
 extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_path_kernel5(
     FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
     const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
@@ -3085,14 +3124,31 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_f
                                        const rvcp::Bvh4Node *bvh_nodes,
                                        const rvcp::TriRecord *bvh_tris,
                                        uint32_t grid_blocks, void *stream, void *main_event,
-                                       void *spec_path_fn, const float *cams)
+                                       void *spec_path_fn, const float *cams, void *spec_pre_fn)
 {
     const uint32_t pre_blocks = (args->n_pixels + rvcp::kPrimaryBlock - 1) / rvcp::kPrimaryBlock;
     auto pre = args->accel ? rvcp::games101_primary_kernel<true> : rvcp::games101_primary_kernel<false>;
     // the frames' pre-passes append to one surface list (the path kernel reads each record's
     // pixel and seed, so the list's order is free): a batch with its cameras in device memory
     // in one launch, one frame per grid row, else one launch per frame
-    if (cams && n_frames > 1)
+    if (spec_pre_fn && !args->accel) {
+        // the specialised pre-pass (same parameters as games101_primary_kernel)
+        const bool batch = cams && n_frames > 1;
+        for (uint32_t k = 0; k < (batch ? 1u : n_frames); ++k) {
+            rvcp::FrameArgs a = args[k];
+            const void *p_faces = faces, *p_verts = verts;
+            const rvcp::Bvh4Node *p_nodes = bvh_nodes;
+            const rvcp::TriRecord *p_btris = bvh_tris;
+            const float *p_cams = batch ? cams : nullptr;
+            uint32_t p_stride = batch ? frame_stride : 0u;
+            void *params[] = {&a, &tri, &p_faces, &p_verts, &mats, &gamma_t, &out_rgba, &out_lin,
+                              &counters, &surf, &shade, &p_nodes, &p_btris, &p_cams, &p_stride};
+            if (hipModuleLaunchKernel((hipFunction_t)spec_pre_fn, pre_blocks, batch ? n_frames : 1u,
+                                      1, rvcp::kPrimaryBlock, 1, 1, 0, (hipStream_t)stream, params,
+                                      nullptr) != hipSuccess)
+                return -2;
+        }
+    } else if (cams && n_frames > 1)
         hipLaunchKernelGGL(pre, dim3(pre_blocks, n_frames), dim3(rvcp::kPrimaryBlock), 0,
                            (hipStream_t)stream, args[0], tri, (const rvcp_face_t *)faces,
                            (const rvcp_vertex_t *)verts, mats, gamma_t, out_rgba, out_lin, counters,

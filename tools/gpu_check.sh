@@ -118,6 +118,9 @@ for s in $STEPS; do
         rccltest) run pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl_timeout.py tests/test_gpu_batch.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
         c6test) run pytest_c6 900 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 600 --timeout-method thread -k c6 ;;
         benchc6) run bench_c6 300 python bench.py --workload c6 --steps 20 --warmup 3 ;;
+        c6prof1) run c6prof1 300 rocprofv3 --kernel-trace --stats -d "$OUT/c6prof1_$TAG" -o run --output-format csv -- python3 bench.py --workload c6 --steps 4 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        c6sqpmc) run c6sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/c6sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --workload c6 --steps 3 --warmup 1 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
+        c6sqpmc2) run c6sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/c6sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --workload c6 --steps 3 --warmup 1 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Compile the scene-specialised module (rvcp_jit.cpp's hipRTC build) for the Cornell box with
 hipcc instead, to read its resource usage and ISA:  python tools/spec_isa.py [--out DIR]
-Writes DIR/spec_scan.inc, DIR/spec.s and DIR/resource-usage.txt (default build/spec_isa)."""
+Writes DIR/spec_scan.inc, DIR/spec.s and DIR/resource-usage.txt (default build/spec_isa).
+--flags -DRVCP_SPEC_ISA_SKIP_ALL: the code left when every skippable block is skipped."""
 import argparse
 import ctypes
 import os
@@ -23,6 +24,7 @@ def main():
     ap.add_argument("--flags", default="")
     ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres"])
     ap.add_argument("--legacy", action="store_true", help="the mode-2 module (RVCP_JIT_LEGACY)")
+    ap.add_argument("--opts", type=int, default=0, help="generator options (rvcp_jit.h kScan*)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     sc = rvcp_amd.Scene.default() if a.scene == "cornell" else rvcp_amd.scene.sphere_scene()
@@ -32,12 +34,12 @@ def main():
     rec = np.zeros(len(p), dtype=[("v0", "<f4", 3), ("e1", "<f4", 3), ("e2", "<f4", 3), ("pad", "<f4", 3)])
     rec["v0"], rec["e1"], rec["e2"] = p[:, 0], (p[:, 1] - p[:, 0]), (p[:, 2] - p[:, 0])
     L = rvcp_amd.abi.load()
-    fn = L.rvcp_internal_jit_scan_source
+    fn = L.rvcp_internal_jit_scan_source_opt
     fn.restype = ctypes.c_size_t
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
-    n = fn(rec.ctypes.data, len(rec), None, 0)
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    n = fn(rec.ctypes.data, len(rec), a.opts, None, 0)
     buf = ctypes.create_string_buffer(n + 1)
-    fn(rec.ctypes.data, len(rec), buf, n + 1)
+    fn(rec.ctypes.data, len(rec), a.opts, buf, n + 1)
     inc = os.path.join(a.out, "spec_scan.inc")
     with open(inc, "w") as f:
         f.write(buf.value.decode())
