@@ -23,17 +23,19 @@ def main():
     ap.add_argument("--accel", type=int, default=0)
     ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres"])
     ap.add_argument("--generic", action="store_true", help="specialize = OFF (generic scan)")
+    ap.add_argument("--grid", type=int, default=0, help="rvcp_config_t.grid_waves_per_simd (0: full)")
     a = ap.parse_args()
     sc = rvcp_amd.Scene.default() if a.scene == "cornell" else rvcp_amd.scene.sphere_scene()
     if a.tris:
         sc = rvcp_amd.scene.with_random_triangles(sc, a.tris)
     with rvcp_amd.RayTracer(spp=a.spp, kernel_variant=a.variant, integrator=a.integrator,
-                            accel=a.accel, specialize=1 if a.generic else 0) as rt:
+                            accel=a.accel, specialize=1 if a.generic else 0,
+                            grid_waves_per_simd=a.grid) as rt:
         rt.upload_scene(sc)
         for _ in range(a.frames):
             rt.render(a.size, a.size, 123.0)
             st = rt.last_stats
-            print(json.dumps({"variant": a.variant, "integrator": a.integrator,
+            print(json.dumps({"variant": a.variant, "integrator": a.integrator, "grid": a.grid,
                               "traversals": int(st["traversals"]), "kernel_ms": round(float(st["kernel_ms"]), 3),
                               "executed": int(st["traversals_executed"]),
                               "wave_iterations": int(st["wave_iterations"]),
