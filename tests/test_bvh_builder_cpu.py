@@ -76,3 +76,31 @@ def test_bvh4_builder_sanitized(tmp_path):
         assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr
         assert "mismatches 0 of 200" in r.stdout, (name, r.stdout)
         assert "quantized: violations 0" in r.stdout, (name, r.stdout)
+
+
+def test_bvh4_split_clipping(checker, tmp_path):
+    """Early split clipping (round 5): the Cornell walls among many small triangles enter the
+    build as clipped pieces.  Same nearest hits as brute force (a leaf may repeat a triangle),
+    and fewer traversal steps per ray than the build without it (-DRVCP_BVH_NO_SPLIT_CLIP)."""
+    plain = str(tmp_path / "bvh4_plain")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-DRVCP_BVH_NO_SPLIT_CLIP=1",
+                    "-I", CSRC, os.path.join(ROOT, "tools", "bvh4_check.cpp"),
+                    os.path.join(CSRC, "rvcp_bvh.cpp"), "-o", plain], check=True)
+    sc = rvcp_amd.scene.with_random_triangles(rvcp_amd.Scene.default(), 20000)
+    v = sc.mesh.aligned_vertices()
+    f = sc.mesh.aligned_faces()
+    tris = v["position"][:, :3][f["vertices"]].astype(np.float32)
+    # plus a scene-spanning sliver and a big off-axis triangle: pieces of thin and tilted shapes
+    extra = np.array([[[-270, 1, -270], [270, 547, 270], [270, 548, 269]],
+                      [[-200, 50, 100], [150, 500, -250], [200, 60, 240]]], np.float32)
+    mesh = str(tmp_path / "mesh.bin")
+    np.concatenate([tris, extra]).tofile(mesh)
+
+    def steps(exe):
+        r = subprocess.run([exe, mesh, "3000"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "mismatches 0 of 3000" in r.stdout, r.stdout
+        line = [l for l in r.stdout.splitlines() if l.startswith("steps/ray")][0]
+        return float(line.split()[1])
+
+    assert steps(checker) < 0.97 * steps(plain)
