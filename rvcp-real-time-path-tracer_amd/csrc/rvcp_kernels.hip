@@ -453,6 +453,9 @@ __device__ __forceinline__ f3 slab_inv(f3 d) {
 }
 
 typedef __attribute__((address_space(3))) int32_t lds_i32;
+#ifndef RVCP_BVH_NEAREST_BREAK_REL
+#define RVCP_BVH_NEAREST_BREAK_REL 40
+#endif
 
 // 4-wide traversal (rvcp_bvh.cpp), over the byte-quantised nodes (Bvh4QNode, 64 B: four 16-B
 // loads in flight together per step).  A step tests the node's four boxes, sorts the children
@@ -510,6 +513,11 @@ __device__ __noinline__ void bvh_nearest(const Bvh4Node *__restrict__ nodes,
             }
             const bool step = alive && ref >= 0;
             if (!__any(step) || __all(parked || !alive)) break;
+#if RVCP_BVH_NEAREST_BREAK_REL > 0
+            // as bvh_pool's node phase (RVCP_BVH_NODE_BREAK_REL)
+            if (__popcll(__ballot(step)) * 64u <= (unsigned)RVCP_BVH_NEAREST_BREAK_REL * (unsigned)__popcll(__ballot(alive)) &&
+                __any(parked)) break;
+#endif
             if (step) {
                 const float4 *q = reinterpret_cast<const float4 *>(qn + ref);
                 const float4 w0 = q[0], w1 = q[1], w2 = q[2];
@@ -619,6 +627,19 @@ __device__ __forceinline__ void bvh4_step(const Bvh4QNode *__restrict__ qn, lds_
 // queue still has pixels and the call took at least kBvhCarryMinRays new rays, so each call
 // makes progress and the last iterations drain everything.
 constexpr uint32_t kBvhPoolChunk = 2;      // leaf triangles loaded together in bvh_pool
+// The node phase of the speculative while-while loop also ends once at most
+// RVCP_BVH_NODE_BREAK_REL / 64 of the lanes holding a ray can still step and some lane holds a
+// parked leaf: the parked lanes test their leaves instead of idling behind the few still
+// descending.  C5 with the BVH 69.16 -> 52.06 ms per frame at 40 / 64 (32: 53.02, 48: 52.42;
+// the absolute form, at most N stepping lanes: 54.6 ms at N = 36-40, 103 ms at 64 = if-if;
+// profiles/r05u_ab_bvhnb.log, r05v_ab_bvhnb2.log, r05w_ab_bvhnb3.log).  Leaf order does not
+// change a nearest hit (the order rule), so neither does the schedule.
+#ifndef RVCP_BVH_NODE_BREAK
+#define RVCP_BVH_NODE_BREAK 0
+#endif
+#ifndef RVCP_BVH_NODE_BREAK_REL
+#define RVCP_BVH_NODE_BREAK_REL 40
+#endif
 #ifndef RVCP_BVH_CARRY_MAX
 #define RVCP_BVH_CARRY_MAX 48
 #endif
@@ -712,6 +733,14 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
             }
             const bool step = c.has && alive && c.ref >= 0;
             if (!__any(step) || __all(!c.has || parked || !alive)) break;
+#if RVCP_BVH_NODE_BREAK > 0
+            // few lanes still stepping while the parked ones wait: test the parked leaves now
+            if (__popcll(__ballot(step)) <= (unsigned)RVCP_BVH_NODE_BREAK && __any(parked)) break;
+#elif RVCP_BVH_NODE_BREAK_REL > 0
+            // the same, relative: at most REL / 64 of the lanes holding a ray can still step
+            if (__popcll(__ballot(step)) * 64u <= (unsigned)RVCP_BVH_NODE_BREAK_REL * (unsigned)__popcll(__ballot(c.has)) &&
+                __any(parked)) break;
+#endif
             if (step) bvh4_step(qn, stk, o, inv, px, py, pz, tmin, c.bt, c.ref, c.sp, alive);
         }
         if (parked) {
