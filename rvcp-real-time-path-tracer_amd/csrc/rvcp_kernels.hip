@@ -2713,7 +2713,10 @@ __device__ __forceinline__ void legacy_hit(const FrameArgs &A, const TriRecord *
 // kLegacyDefer: the most lanes left ending a sample that sit out one trace (below).  16
 // measured best: sphere room 0.367 -> 0.345 ms, mode 2 on the C3 frame 2.237 -> 2.156 ms per
 // frame (profiles/r03v_m2_defer_sweep.log; 8, 24, 32, 40 and 64 less good).
-constexpr int kLegacyDefer = 16;
+#ifndef RVCP_LEGACY_DEFER
+#define RVCP_LEGACY_DEFER 16
+#endif
+constexpr int kLegacyDefer = RVCP_LEGACY_DEFER;
 
 }  // namespace
 
