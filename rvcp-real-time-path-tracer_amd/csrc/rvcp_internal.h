@@ -167,7 +167,14 @@ struct alignas(16) BvhNode {
     int32_t pad[2];
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
-constexpr int kBvhLeafMax = 4;
+// at most this many triangles per BVH leaf: 2 since round 5 -- with the node-phase break
+// (rvcp_kernels.hip) the 4-triangle leaves' tests cost more than the extra node steps of 2
+// (C5 BVH 52.0 -> 47.0 ms; 1: 46.5 ms for 1.8x the nodes; profiles/r06c_ab_bvhleaf.log,
+// r06d_ab_bvhleaf2.log)
+#ifndef RVCP_BVH_LEAF_MAX
+#define RVCP_BVH_LEAF_MAX 2
+#endif
+constexpr int kBvhLeafMax = RVCP_BVH_LEAF_MAX;
 constexpr uint32_t kBvhPadId = 0xFFFFFFFFu;   // padding slot of the leaf order (even leaf starts)
 constexpr int kBvhStack = 32;           // traversal stack entries per lane
 
