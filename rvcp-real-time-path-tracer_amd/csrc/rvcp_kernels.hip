@@ -630,15 +630,17 @@ constexpr uint32_t kBvhPoolChunk = 2;      // leaf triangles loaded together in 
 // The node phase of the speculative while-while loop also ends once at most
 // RVCP_BVH_NODE_BREAK_REL / 64 of the lanes holding a ray can still step and some lane holds a
 // parked leaf: the parked lanes test their leaves instead of idling behind the few still
-// descending.  C5 with the BVH 69.16 -> 52.06 ms per frame at 40 / 64 (32: 53.02, 48: 52.42;
-// the absolute form, at most N stepping lanes: 54.6 ms at N = 36-40, 103 ms at 64 = if-if;
-// profiles/r05u_ab_bvhnb.log, r05v_ab_bvhnb2.log, r05w_ab_bvhnb3.log).  Leaf order does not
-// change a nearest hit (the order rule), so neither does the schedule.
+// descending.  C5 with the BVH 69.16 -> 52.06 ms per frame at 40 / 64 with 4-triangle leaves
+// (32: 53.02, 48: 52.42; the absolute form, at most N stepping lanes: 54.6 ms at N = 36-40,
+// 103 ms at 64 = if-if; profiles/r05u_ab_bvhnb.log, r05v_ab_bvhnb2.log, r05w_ab_bvhnb3.log);
+// with 2-triangle leaves 48 / 64 is best (46.75 ms; 40: 47.03, 52: 47.36, 56: 49.38,
+// r06f_ab_bvhtune2.log, r06g_ab_bvhtune3.log).  Leaf order does not change a nearest hit (the
+// order rule), so neither does the schedule.
 #ifndef RVCP_BVH_NODE_BREAK
 #define RVCP_BVH_NODE_BREAK 0
 #endif
 #ifndef RVCP_BVH_NODE_BREAK_REL
-#define RVCP_BVH_NODE_BREAK_REL 40
+#define RVCP_BVH_NODE_BREAK_REL 48
 #endif
 #ifndef RVCP_BVH_CARRY_MAX
 #define RVCP_BVH_CARRY_MAX 48
