@@ -84,8 +84,6 @@ for s in $STEPS; do
         tlc3) tl tlc3 40 ;;
         tlreg) for k in 1 2 3 4 5; do run tlreg$k 300 bash -c "rm -f /tmp/tl_reg.bin && RVCP_LIB=$DBG RVCP_JIT_FLAGS=-DRVCP_REGION_CLOCK=$k RVCP_DEBUG_TIMELINE=/tmp/tl_reg.bin python tools/frames.py --frames 6 $TLARGS && python tools/timeline.py /tmp/tl_reg.bin --waves \$(python -c 'import os; print(os.path.getsize(\"/tmp/tl_reg.bin\") // 64 // 6)')"; done ;;
         tlc2) tl tlc2 40 --size 384 --spp 10 ;;
-        rehearse8c4) run rehearse8c4 400 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 --workload c4 --steps 5 --warmup 1 ;;
-        rehearse8c4b) run rehearse8c4b 500 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29539 bench.py --gpus 8 --workload c4 --steps 20 --warmup 4 ;;
         rehearse2) run rehearse2 300 env RVCP_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
         frames) run frames 300 python tools/frames.py --frames 20 ;;
         # schedules 4 / 10 on meshes (tools/ab.py, one frame at a time)
@@ -108,7 +106,6 @@ for s in $STEPS; do
         benchc2cpu) run bench_c2cpu 300 python bench.py --workload c2 --steps 100 --warmup 10 ;;
         # the driver's N>1 form without a launcher (bench.self_launch), one-GPU rehearsal
         selfl2) run selfl2 300 env RVCP_BENCH_REHEARSAL=1 python bench.py --gpus 2 --steps 10 --warmup 2 ;;
-        selfl8) run selfl8 500 env RVCP_BENCH_REHEARSAL=1 python bench.py --gpus 8 --steps 10 --warmup 2 ;;
         c5tests) run c5tests 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "c5 or multi_tile or odd_remainder or variants or bitexact_cornell" ;;
         pooltests) run pooltests 600 python -u -m pytest tests/test_gpu_specialize.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         fuzz) run pytest_fuzz 600 python -u -m pytest tests/test_gpu_spec_fuzz.py -m gpu -x -q --timeout 200 --timeout-method thread ;;
