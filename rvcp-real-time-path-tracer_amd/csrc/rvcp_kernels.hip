@@ -636,9 +636,6 @@ constexpr uint32_t kBvhPoolChunk = 2;      // leaf triangles loaded together in 
 // with 2-triangle leaves 48 / 64 is best (46.75 ms; 40: 47.03, 52: 47.36, 56: 49.38,
 // r06f_ab_bvhtune2.log, r06g_ab_bvhtune3.log).  Leaf order does not change a nearest hit (the
 // order rule), so neither does the schedule.
-#ifndef RVCP_BVH_NODE_BREAK
-#define RVCP_BVH_NODE_BREAK 0
-#endif
 #ifndef RVCP_BVH_NODE_BREAK_REL
 #define RVCP_BVH_NODE_BREAK_REL 48
 #endif
@@ -735,11 +732,8 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
             }
             const bool step = c.has && alive && c.ref >= 0;
             if (!__any(step) || __all(!c.has || parked || !alive)) break;
-#if RVCP_BVH_NODE_BREAK > 0
+#if RVCP_BVH_NODE_BREAK_REL > 0
             // few lanes still stepping while the parked ones wait: test the parked leaves now
-            if (__popcll(__ballot(step)) <= (unsigned)RVCP_BVH_NODE_BREAK && __any(parked)) break;
-#elif RVCP_BVH_NODE_BREAK_REL > 0
-            // the same, relative: at most REL / 64 of the lanes holding a ray can still step
             if (__popcll(__ballot(step)) * 64u <= (unsigned)RVCP_BVH_NODE_BREAK_REL * (unsigned)__popcll(__ballot(c.has)) &&
                 __any(parked)) break;
 #endif
