@@ -32,7 +32,8 @@ KERNEL_NAMES = {1: "games101_kernel", 2: "games101_dual_kernel", 3: "games101_pa
                 6: "games101_path_kernel<6>", 7: "games101_bvh_path_kernel", 8: "legacy_kernel",
                 10: "games101_tiled_pool_kernel",
                 # + RVCP_VARIANT_SPECIALIZED (16): the scene-specialised module (rvcp_jit.cpp)
-                19: "rvcp_spec_path_kernel5", 22: "rvcp_spec_path_kernel6", 24: "rvcp_spec_legacy_kernel"}
+                19: "rvcp_spec_path_kernel5", 22: "rvcp_spec_path_kernel6", 23: "rvcp_spec_bvh_path_kernel",
+                24: "rvcp_spec_legacy_kernel"}
 VARIANT_SPECIALIZED = 16
 
 # Defaults == the shader's #defines (ray_tracer_games101_branch.comp:5-13).

@@ -243,6 +243,33 @@ void early_split_clip(std::vector<Prim> &prims, const float (*pos)[3][3], const 
 
 }  // namespace
 
+uint32_t bvh_big_prefix(const float (*pos)[3][3], uint32_t n, uint32_t cap)
+{
+    if (n < 64) return 0;
+    std::vector<float> ext(n);
+    Box scene;
+    for (uint32_t i = 0; i < n; i++) {
+        Box b;
+        bool finite = true;
+        for (int v = 0; v < 3; v++)
+            for (int k = 0; k < 3; k++) finite = finite && std::isfinite(pos[i][v][k]);
+        if (!finite) return 0;
+        for (int v = 0; v < 3; v++) b.grow(pos[i][v]);
+        float e = 0.0f;
+        for (int k = 0; k < 3; k++) e = std::max(e, b.hi[k] - b.lo[k]);
+        ext[i] = e;
+        scene.grow(b);
+    }
+    std::vector<float> sorted(ext);
+    std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
+    const float dx = scene.hi[0] - scene.lo[0], dy = scene.hi[1] - scene.lo[1],
+                dz = scene.hi[2] - scene.lo[2];
+    const float thr = std::max(8.0f * sorted[n / 2], std::sqrt(dx * dx + dy * dy + dz * dz) / 16.0f);
+    uint32_t k = 0;
+    while (k < n && k < cap && ext[k] > thr) k++;
+    return k;
+}
+
 // Build over `n` faces given their three vertex positions.  Outputs the node array, the
 // leaf-ordered original face ids and the root reference; returns the tree depth.
 int bvh_build(const float (*pos)[3][3], uint32_t n, std::vector<BvhNode> &nodes,

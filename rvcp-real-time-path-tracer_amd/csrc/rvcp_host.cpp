@@ -92,6 +92,7 @@ struct rvcp_ctx {
     uint32_t bvh_n4 = 0;
     uint32_t bvh_slots = 0;
     int bvh_depth = 0;
+    uint32_t bvh_prefix = 0;    // faces [0, bvh_prefix) left out of the BVH (FrameArgs::bvh_prefix)
     float *d_gamma = nullptr;
     float *d_unorm = nullptr;
     unsigned long long *d_counters = nullptr;
@@ -607,16 +608,43 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         (rc = dev_upload<rvcp_sphere_t>(ctx, &ctx->d_spheres, spheres, n_spheres)))
         return rc;
     ctx->n_spheres = n_spheres;
+    ctx->bvh_prefix = 0;
+    std::shared_ptr<JitKernels> bvh_jit;
     if (ctx->cfg.accel == RVCP_ACCEL_BVH && n_faces > 0) {
         std::vector<float> pos((size_t)n_faces * 9);
         for (uint32_t i = 0; i < n_faces; i++)
             for (int v = 0; v < 3; v++)
                 std::memcpy(&pos[(size_t)i * 9 + 3 * v], vertices[faces[i].vertices[v]].position, 12);
+        const auto *P = reinterpret_cast<const float (*)[3][3]>(pos.data());
+        // The hybrid: when the scene starts with a run of big faces (C5: the
+        // Cornell room before 100 000 small triangles), those are tested by the specialised scan
+        // -- at full lane utilisation, no dependent loads -- and the BVH holds only the rest, so
+        // its boxes are tight and every ray enters it with the room's nearest hit as its bound.
+        // Only with a specialised module for them (games101, specialize AUTO, the JIT's range);
+        // the kernels without one test the prefix with the generic test.
+        uint32_t K = 0;
+        if (ctx->cfg.specialize == RVCP_SPECIALIZE_AUTO && ctx->cfg.integrator != RVCP_INTEGRATOR_LEGACY &&
+            !RVCP_KNOB("RVCP_NO_BVH_PREFIX")) {
+            K = bvh_big_prefix(P, n_faces, kJitMaxFaces);
+            if (K < 8 || n_faces - K < 64 || !jit_scene_in_range(tri.data(), K)) K = 0;
+            if (K) {
+                std::string jerr;
+                bvh_jit = jit_path_kernels(ctx->device, tri.data(), K, jerr, false, n_spheres == 0,
+                                           false, true);
+                HIP_TRY(ctx, hipSetDevice(ctx->device));
+                if (!bvh_jit || !bvh_jit->bvh_path || !bvh_jit->bvh_primary) {
+                    K = 0;
+                    bvh_jit.reset();
+                }
+            }
+        }
         std::vector<BvhNode> nodes;
         std::vector<uint32_t> order;
         int32_t root = 0;
-        const int depth = bvh_build(reinterpret_cast<const float (*)[3][3]>(pos.data()), n_faces,
-                                    nodes, order, root);
+        const int depth = bvh_build(P + K, n_faces - K, nodes, order, root);
+        for (uint32_t &id : order)                       // the BVH's ids are faces K ...
+            if (id != kBvhPadId) id += K;
+        ctx->bvh_prefix = K;
         if (depth >= kBvhStack) return fail(ctx, RVCP_E_UNSUPPORTED, "BVH deeper than the traversal stack");
         // the leaf-ordered triangles packed as 10 floats per slot (v0, e1, e2, face id bits),
         // what the traversal reads (bvh_leaf); leaves start at even slots, so 16-B aligned.
@@ -652,6 +680,7 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
     // scene-specialised scan: compiled here, once per scene and process
     ctx->jit.reset();
     ctx->jit_err.clear();
+    if (bvh_jit) ctx->jit = bvh_jit;          // the BVH hybrid's module (above)
     if (ctx->cfg.specialize == RVCP_SPECIALIZE_AUTO && ctx->cfg.accel == RVCP_ACCEL_NONE &&
         n_faces >= 1 && n_faces <= kJitMaxFaces && jit_scene_in_range(tri.data(), n_faces) &&
         !RVCP_KNOB("RVCP_NO_SPECIALIZE")) {
@@ -781,6 +810,7 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
     A.bvh_root = ctx->bvh_root;
     A.bvh_n4 = ctx->bvh_n4;
     A.bvh_slots = ctx->bvh_slots;
+    A.bvh_prefix = A.accel == RVCP_ACCEL_BVH ? ctx->bvh_prefix : 0u;
     const bool legacy = ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY;
     A.n_spheres = legacy ? ctx->n_spheres : 0u;
     A.n_mats = ctx->n_mats;
@@ -856,10 +886,15 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
             // mode 2 with the specialised triangle scan (its kernel also checks per wave
             // that every ray is finite and has t_min > 0)
             const bool spec_legacy = legacy && jk && jk->legacy && jk->blocks_per_cu_legacy > 0;
+            // the BVH hybrid's kernels (the prefix faces by the specialised scan); without them
+            // (t_min <= 0) the built-in BVH kernels test the prefix with the generic test
+            const bool spec_bvh = !legacy && A.accel && A.bvh_prefix > 0 && jk && jk->bvh_path &&
+                                  jk->bvh_primary && jk->blocks_per_cu_bvh > 0 && A.t_min > 0.0f;
             uint32_t cap = (uint32_t)(legacy ? ctx->legacy_capacity
                                      : A.accel ? ctx->bvh_capacity
                                                : ctx->grid_capacity[A.variant]);
             if (spec) cap = (uint32_t)jit_per_cu * (ctx->n_simds / 4u);
+            if (spec_bvh) cap = (uint32_t)jk->blocks_per_cu_bvh * (ctx->n_simds / 4u);
             if (spec_legacy) cap = (uint32_t)jk->blocks_per_cu_legacy * (ctx->n_simds / 4u);
             A.n_simds = ctx->n_simds;
             uint32_t waves = 0, chunk = 0;
@@ -948,13 +983,13 @@ static int render_frames(rvcp_ctx_t *ctx, const rvcp_push_constant_t *pushes, ui
                                                  ctx->d_bvh_nodes, ctx->d_bvh_tris,
                                                  blocks, s, ctx->evm,
                                                  spec ? (void *)(A.variant == 6 ? jk->path6 : jk->path5)
-                                                      : nullptr,
+                                                      : spec_bvh ? (void *)jk->bvh_path : nullptr,
                                                  cams && frame_px <= kPrepassBatchMaxPixels
                                                      ? ctx->d_cams : nullptr,
                                                  spec && jit_spec_prepass() ? (void *)jk->primary
-                                                                            : nullptr);
+                                                 : spec_bvh ? (void *)jk->bvh_primary : nullptr);
                 }
-                if (spec) ctx->last_spec = true;
+                if (spec || spec_bvh) ctx->last_spec = true;
             } else {
                 HIP_TRY(ctx, hipEventRecord(ctx->evm, s));
                 rc = rvcp_launch_games101(&A, ctx->d_tri, ctx->d_faces, ctx->d_verts, ctx->d_mats,

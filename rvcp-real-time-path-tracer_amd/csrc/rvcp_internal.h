@@ -247,6 +247,10 @@ struct FrameArgs {
     int32_t bvh_root;        // root reference (see BvhNode) when accel == RVCP_ACCEL_BVH
     uint32_t bvh_n4;         // Bvh4Node offset of the quantised nodes in the node buffer (0)
     uint32_t bvh_slots;      // TriRecord offset of the packed 10-float leaf records (0: buffer start)
+    // faces [0, bvh_prefix) are not in the BVH: every ray tests them first, with the
+    // scene-specialised scan where the module has one, else the generic test (the hybrid of
+    // DESIGN.md §4.6); 0 = the BVH holds every face
+    uint32_t bvh_prefix;
     // small frames (path kernels of schedules 3/6): when the surface list fits the resident
     // lanes, spread it over every resident wave, at least spread_min pixels each (0 = off),
     // and let waves with <= 32 rays split each ray's scan over R lanes from the first
@@ -279,6 +283,10 @@ int bvh4_collapse(const std::vector<BvhNode> &nodes, int32_t root, std::vector<B
                   int32_t &root4);
 // rvcp_bvh.cpp: the byte-quantised copy of a collapsed tree (same indices and refs).
 void bvh4_quantize(const std::vector<Bvh4Node> &in, std::vector<Bvh4QNode> &out);
+// rvcp_bvh.cpp: how many leading faces are "big" (box extent above the split-clipping
+// threshold: max(8 x the median extent, scene diagonal / 16)), at most `cap`; the hybrid tests
+// them with the specialised scan and builds the BVH over the rest.
+uint32_t bvh_big_prefix(const float (*pos)[3][3], uint32_t n, uint32_t cap);
 
 #endif  // __HIPCC_RTC__
 }  // namespace rvcp

@@ -776,7 +776,7 @@ JitKernels::~JitKernels()
 }
 
 int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
-                     bool legacy, int legacy_waves, bool lds_scene)
+                     bool legacy, int legacy_waves, bool lds_scene, bool bvh)
 {
     const RtcApi &api = rtc();
     if (!api.ok) {
@@ -797,6 +797,7 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
                                       "-fno-fast-math", "-fno-slp-vectorize", "-DRVCP_JIT",
                                       "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
     if (legacy) opts.push_back("-DRVCP_JIT_LEGACY");
+    if (bvh) opts.push_back("-DRVCP_JIT_BVH");
 #ifdef RVCP_TIMELINE
     opts.push_back("-DRVCP_TIMELINE");      // the debug library's modules keep the per-wave timeline
 #endif
@@ -824,7 +825,7 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
 
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
                                              std::string &err, bool legacy, bool sphereless,
-                                             bool lds_fits)
+                                             bool lds_fits, bool bvh)
 {
     // Mode 2 on a scene without spheres (the Cornell frame): 6 waves per SIMD measured 2.5 %
     // faster than 5, with spheres 5 % slower (profiles/r02_legacy_waves_ab.log).  With the
@@ -842,7 +843,8 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
     const std::string scan = jit_scan_source(tri, n, jit_scan_opts()) +
         (legacy ? "// +legacy " + std::to_string(legacy_waves) + (lds_scene ? " lds" : "") + "\n"
                 : std::string()) +
-        (key_flags.empty() ? std::string() : "// +flags" + key_flags + "\n");
+        (key_flags.empty() ? std::string() : "// +flags" + key_flags + "\n") +
+        (bvh ? "// +bvh\n" : "");
     const uint64_t h = fnv1a(scan);
     std::lock_guard<std::mutex> lock(g_mu);
     for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
@@ -852,7 +854,7 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         }
     }
     std::vector<char> code;
-    if (jit_compile_code(scan, code, err, legacy, legacy_waves, lds_scene) != 0) return nullptr;
+    if (jit_compile_code(scan, code, err, legacy, legacy_waves, lds_scene, bvh) != 0) return nullptr;
     auto k = std::make_shared<JitKernels>();
     k->device = device;
     if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&k->module, code.data()) != hipSuccess) {
@@ -869,6 +871,11 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
         err = "specialised pre-pass kernel missing from the module";
         return nullptr;
     }
+    if (bvh && (hipModuleGetFunction(&k->bvh_path, k->module, "rvcp_spec_bvh_path_kernel") != hipSuccess ||
+                hipModuleGetFunction(&k->bvh_primary, k->module, "rvcp_spec_bvh_primary_kernel") != hipSuccess)) {
+        err = "specialised BVH kernels missing from the module";
+        return nullptr;
+    }
     if (legacy && hipModuleGetFunction(&k->legacy, k->module, "rvcp_spec_legacy_kernel") != hipSuccess) {
         err = "specialised mode-2 kernel missing from the module";
         return nullptr;
@@ -876,6 +883,8 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
     int bpc = 0;
     if (legacy && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->legacy, kBlock, 0) == hipSuccess)
         k->blocks_per_cu_legacy = bpc;
+    if (bvh && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->bvh_path, kBlock, 0) == hipSuccess)
+        k->blocks_per_cu_bvh = bpc;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->path5, kBlock, 0) == hipSuccess)
         k->blocks_per_cu5 = bpc;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k->path6, kBlock, 0) == hipSuccess)

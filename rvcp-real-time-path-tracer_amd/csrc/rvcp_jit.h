@@ -19,7 +19,10 @@ struct JitKernels {
     hipFunction_t path6 = nullptr;     // schedule 6 (6 waves per SIMD)
     hipFunction_t legacy = nullptr;    // integrator mode 2 (modules compiled with `legacy`)
     hipFunction_t primary = nullptr;   // the schedule-3/6 pre-pass with the specialised scan
-    int blocks_per_cu5 = 0, blocks_per_cu6 = 0, blocks_per_cu_legacy = 0;
+    // the BVH hybrid (modules compiled with `bvh`): the BVH path kernel and pre-pass, the scan
+    // covering the scene's first FrameArgs::bvh_prefix faces
+    hipFunction_t bvh_path = nullptr, bvh_primary = nullptr;
+    int blocks_per_cu5 = 0, blocks_per_cu6 = 0, blocks_per_cu_legacy = 0, blocks_per_cu_bvh = 0;
     ~JitKernels();
 };
 
@@ -41,14 +44,17 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n, unsigned opts = 0)
 // `legacy` also builds the mode-2 kernel (RVCP_JIT_LEGACY).
 // `lds_scene`: the mode-2 kernel copies the scene into LDS (RVCP_LEGACY_LDS_SCENE).
 int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
-                     bool legacy = false, int legacy_waves = 0, bool lds_scene = false);
+                     bool legacy = false, int legacy_waves = 0, bool lds_scene = false,
+                     bool bvh = false);
 // Compiled + loaded kernels for the scene on `device` (process-wide cache keyed by the scan
 // source and `legacy`); nullptr with err set when hipRTC is unavailable or compilation fails.
 // `sphereless`: the mode-2 kernel is built for 6 waves per SIMD.
 // `lds_fits`: at most 64 spheres and 64 materials (and, as always here, 64 faces): the mode-2
 // kernel reads its hit records, spheres and materials from LDS copies.
+// `bvh`: also the BVH hybrid's kernels (RVCP_JIT_BVH; tri / n are then the prefix faces).
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
                                              std::string &err, bool legacy = false,
-                                             bool sphereless = false, bool lds_fits = false);
+                                             bool sphereless = false, bool lds_fits = false,
+                                             bool bvh = false);
 
 }  // namespace rvcp

@@ -661,7 +661,8 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
                                       bool nA_, bool nB_, f3 a_o, f3 a_d, f3 b_o, f3 b_d,
                                       float tmin, float tmax, bool may_carry, BvhCarry &c,
                                       bool &subA, bool &subB, bool &frozen, float &btA, int &bestA,
-                                      float &btB, int &bestB, uint32_t n4, uint32_t slots) {
+                                      float &btB, int &bestB, uint32_t n4, uint32_t slots,
+                                      float ibtA, int ibestA, float ibtB, int ibestB) {
     const uint64_t mA = __ballot(nA_), mB = __ballot(nB_);
     const uint32_t nA = (uint32_t)__builtin_popcountll(mA);
     const uint32_t nr = nA + (uint32_t)__builtin_popcountll(mB);
@@ -703,6 +704,9 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
             const f3 da = mk(__shfl(a_d.x, src), __shfl(a_d.y, src), __shfl(a_d.z, src));
             const f3 ob = mk(__shfl(b_o.x, src), __shfl(b_o.y, src), __shfl(b_o.z, src));
             const f3 db = mk(__shfl(b_d.x, src), __shfl(b_d.y, src), __shfl(b_d.z, src));
+            // the ray's starting bound and candidate: t_max / none, or the hybrid prefix's hit
+            const float i_tA = __shfl(ibtA, src), i_tB = __shfl(ibtB, src);
+            const int i_bA = __shfl(ibestA, src), i_bB = __shfl(ibestB, src);
             if (take) {
                 const bool isA = rr < nA;
                 c.key = 2u * (uint32_t)src + (isA ? 0u : 1u);
@@ -712,8 +716,8 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
                 px = inv.x >= 0.0f; py = inv.y >= 0.0f; pz = inv.z >= 0.0f;
                 c.ref = root;
                 c.sp = 0;
-                c.bt = tmax;
-                c.best = -1;
+                c.bt = isA ? i_tA : i_tB;
+                c.best = isA ? i_bA : i_bB;
                 c.has = true;
                 alive = true;
                 parked = false;
@@ -1623,6 +1627,18 @@ __device__ __forceinline__ void primary_body(
         int best = -1;
         float bt = tmax;
         if (BVH) {
+            // the hybrid's prefix faces first (FrameArgs::bvh_prefix), then the BVH over the rest
+            if (A.bvh_prefix) {
+#ifdef RVCP_SPEC_SCAN
+                if (SPEC && !__any(!(ray_in_range(o, d) && tmin > 0.0f))) {
+                    spec_scan1(o, d, tmin, bt, best);
+                } else
+#endif
+                for (uint32_t i = 0; i < A.bvh_prefix; ++i) {
+                    float t;
+                    if (tri_accept(tri[i], o, d, tmin, bt, t)) { bt = t; best = (int)i; }
+                }
+            }
             bvh_nearest<false>(bvh_nodes, bvh_tris, A.bvh_root, nullptr, o, d, tmin, bt, best, A.bvh_n4, A.bvh_slots);
         }
 #ifdef RVCP_SPEC_SCAN
@@ -1760,6 +1776,51 @@ __device__ __forceinline__ void scan_generic2(const TriRecord *__restrict__ tri,
 // The tiled scans issue the first pretest halves of two triangles together (ILP for the
 // latency-bound per-triangle chain; C5 -5 %); the one-slot schedule 5 too (3
 // and 4 triangles per step measured equal to 2).
+// The BVH hybrid's prefix (FrameArgs::bvh_prefix = K > 0: faces [0, K) are not in the BVH):
+// the new rays of the wave (nA: the shadow ray a, nB: the path ray b) are tested against
+// faces [0, K) first, with the specialised scan of the module (which covers exactly those
+// faces) when every new ray is in its range, else with the generic test; each ray then enters
+// the BVH with that nearest hit as its bound and candidate -- and the BVH's rule (smaller t,
+// or equal t and larger face) combines them as the brute-force scan's order would.  The
+// specialised dual scan keeps no face for the shadow slot (as in the brute-force dual scan):
+// a prefix hit is face 0 for the order rule -- resolve A needs only hit / no hit -- and a
+// nearest t of exactly t_max is settled by a generic re-scan that keeps the face.
+// SPEC_A = false (SINGLE): the shadow slot may hold a path ray, which needs its face.
+template <bool SPEC_A>
+__device__ __forceinline__ void bvh_prefix_scan(const FrameArgs &A, const TriRecord *__restrict__ tri,
+                                                bool nA, bool nB, f3 a_o, f3 a_d, f3 b_o, f3 b_d,
+                                                float &btA, int &bestA, float &btB, int &bestB) {
+    const uint32_t K = A.bvh_prefix;
+    btA = A.t_max;
+    bestA = -1;
+    btB = A.t_max;
+    bestB = -1;
+#ifdef RVCP_SPEC_SCAN
+    if (SPEC_A && A.t_min > 0.0f &&
+        !__any((nA && !ray_in_range(a_o, a_d)) || (nB && !ray_in_range(b_o, b_d)))) {
+        float sa = nA ? A.t_max : -1.0f;        // a lane without a new shadow ray: below t_min
+        spec_scan2(a_o, a_d, b_o, b_d, A.t_min, sa, btB, bestB);
+        const bool rescan = nA && sa == A.t_max;
+        if (nA) { btA = sa; bestA = sa != A.t_max ? 0 : -1; }
+        if (__builtin_expect(__any(rescan), 0)) {
+            float t2 = A.t_max;
+            int b2 = -1;
+            for (uint32_t i = 0; i < K; ++i) {
+                float t;
+                if (tri_accept(tri[i], a_o, a_d, A.t_min, t2, t) && rescan) { t2 = t; b2 = (int)i; }
+            }
+            if (rescan) { btA = t2; bestA = b2; }
+        }
+        return;
+    }
+#endif
+    for (uint32_t i = 0; i < K; ++i) {
+        float t;
+        if (nA && tri_accept(tri[i], a_o, a_d, A.t_min, btA, t)) { btA = t; bestA = (int)i; }
+        if (nB && tri_accept(tri[i], b_o, b_d, A.t_min, btB, t)) { btB = t; bestB = (int)i; }
+    }
+}
+
 // The variant-3 path kernel runs 5 waves per SIMD: 95 VGPRs without spills once the scan loop
 // is not unrolled and the pixel's surface record is re-read per sample instead of held in
 // registers (C3 5.93 -> 5.73 ms, C4 44.2 -> 41.3 ms, C2 unchanged, over 105 VGPRs / 4 waves;
@@ -2233,13 +2294,21 @@ __device__ __forceinline__ void path_body(
             // pooled over its lanes (bvh_pool) ----
             lds_i32 *stk = (lds_i32 *)bvh_stack;
             if (!SINGLE) {
+                // the hybrid's prefix faces first (bvh_prefix_scan), for the rays new this call
+                float pbtA = A.t_max, pbtB = A.t_max;
+                int pbestA = -1, pbestB = -1;
+                if (A.bvh_prefix)
+                    bvh_prefix_scan<true>(A, tri, newA, newB, s_ao, s_ad, b_o, b_d, pbtA, pbestA,
+                                          pbtB, pbestB);
                 float4 *pl = pool + wv * 72;            // res: 64 float4 (128 float2), tab: 8 float4
                 bvh_pool(bvh_nodes, bvh_tris, A.bvh_root, stk, reinterpret_cast<uint8_t *>(pl + 64),
                          reinterpret_cast<float2 *>(pl), lane, newA, newB, s_ao, s_ad, b_o, b_d,
                          A.t_min, A.t_max, !q.exhausted, carry, subA, subB, frozen, btA, bestA,
-                         btB, bestB, A.bvh_n4, A.bvh_slots);
+                         btB, bestB, A.bvh_n4, A.bvh_slots, pbtA, pbestA, pbtB, pbestB);
             } else
             {
+            if (A.bvh_prefix)
+                bvh_prefix_scan<false>(A, tri, sA, sB, s_ao, s_ad, b_o, b_d, btA, bestA, btB, bestB);
             if (sA) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, s_ao, s_ad, A.t_min, btA, bestA, A.bvh_n4, A.bvh_slots);
             if (sB) bvh_nearest<true>(bvh_nodes, bvh_tris, A.bvh_root, stk, b_o, b_d, A.t_min, btB, bestB, A.bvh_n4, A.bvh_slots);
             }
@@ -3055,6 +3124,37 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
 // Scene-specialised path kernels (rvcp_jit.cpp compiles this file with hipRTC, RVCP_JIT and
 // RVCP_SPEC_SCAN set): schedules 3 and 6 with the scan unrolled over the uploaded scene
 // (DESIGN.md §4.7).  extern "C" so that the host finds them by name in the module.
+#ifdef RVCP_JIT_BVH
+// The BVH hybrid (FrameArgs::bvh_prefix): the module's scan covers the scene's
+// first bvh_prefix faces; the BVH path kernel and pre-pass test them with it, then the BVH.
+extern "C" __global__ __launch_bounds__(kBlock, 4) void rvcp_spec_bvh_path_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const MatRecord *__restrict__ mats,
+    const LightRecord *__restrict__ lights, const float *__restrict__ gamma_t,
+    uint32_t *__restrict__ out_rgba, float *__restrict__ out_lin,
+    unsigned long long *__restrict__ counters, const SurfRecord *__restrict__ surf,
+    const FaceShade *__restrict__ shade, const Bvh4Node *__restrict__ bvh_nodes,
+    const TriRecord *__restrict__ bvh_tris)
+{
+    __shared__ uint8_t tail_tab[kBlock / kWave][kWave];
+    __shared__ int32_t bvh_stack[kBvhStack * kBlock];     // traversal stacks, column per thread
+    __shared__ float4 bvh_pool_lds[(kBlock / kWave) * 72];  // per wave: 128 results + 128-B owner table
+    path_body<false, true, false>(A, tri, mats, lights, gamma_t, out_rgba, out_lin, counters, surf,
+                           shade, tail_tab, nullptr, bvh_nodes, bvh_tris,
+                           bvh_stack + threadIdx.x, nullptr, nullptr, bvh_pool_lds);
+}
+extern "C" __global__ __launch_bounds__(kPrimaryBlock) void rvcp_spec_bvh_primary_kernel(
+    FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
+    const rvcp_vertex_t *__restrict__ verts, const MatRecord *__restrict__ mats,
+    const float *__restrict__ gamma_t, uint32_t *__restrict__ out_rgba,
+    float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
+    SurfRecord *__restrict__ surf, const FaceShade *__restrict__ shade,
+    const Bvh4Node *__restrict__ bvh_nodes, const TriRecord *__restrict__ bvh_tris,
+    const float *__restrict__ cams, uint32_t frame_stride)
+{
+    primary_body<true, true>(A, tri, faces, verts, mats, gamma_t, out_rgba, out_lin, counters,
+                             surf, shade, bvh_nodes, bvh_tris, cams, frame_stride);
+}
+#endif
 // the pre-pass with the specialised scan (rvcp_launch_games101_v3's spec_pre_fn)
 extern "C" __global__ __launch_bounds__(kPrimaryBlock) void rvcp_spec_primary_kernel(
     FrameArgs A, const TriRecord *__restrict__ tri, const rvcp_face_t *__restrict__ faces,
@@ -3159,8 +3259,9 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_f
     // the frames' pre-passes append to one surface list (the path kernel reads each record's
     // pixel and seed, so the list's order is free): a batch with its cameras in device memory
     // in one launch, one frame per grid row, else one launch per frame
-    if (spec_pre_fn && !args->accel) {
-        // the specialised pre-pass (same parameters as games101_primary_kernel)
+    if (spec_pre_fn) {
+        // the specialised pre-pass (same parameters as games101_primary_kernel; with the BVH:
+        // the hybrid's, rvcp_spec_bvh_primary_kernel)
         const bool batch = cams && n_frames > 1;
         for (uint32_t k = 0; k < (batch ? 1u : n_frames); ++k) {
             rvcp::FrameArgs a = args[k];
@@ -3190,7 +3291,16 @@ extern "C" int rvcp_launch_games101_v3(const rvcp::FrameArgs *args, uint32_t n_f
                                0u);
     if (main_event && hipEventRecord((hipEvent_t)main_event, (hipStream_t)stream) != hipSuccess)
         return -2;
-    if (spec_path_fn) {
+    if (spec_path_fn && args->accel) {
+        // the BVH hybrid's path kernel (rvcp_spec_bvh_path_kernel, games101_bvh_path_kernel's
+        // signature)
+        rvcp::FrameArgs a = *args;
+        void *params[] = {&a, &tri, &mats, &lights, &gamma_t, &out_rgba, &out_lin, &counters,
+                          &surf, &shade, &bvh_nodes, &bvh_tris};
+        if (hipModuleLaunchKernel((hipFunction_t)spec_path_fn, grid_blocks, 1, 1, rvcp::kBlock,
+                                  1, 1, 0, (hipStream_t)stream, params, nullptr) != hipSuccess)
+            return -2;
+    } else if (spec_path_fn) {
         // the scene-specialised schedule 3 / 6 kernel of rvcp_jit.cpp (same signature)
         rvcp::FrameArgs a = *args;
         void *params[] = {&a, &tri, &mats, &lights, &gamma_t, &out_rgba, &out_lin, &counters,

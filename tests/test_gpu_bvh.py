@@ -47,6 +47,17 @@ def test_bvh_c5_mesh(cornell):
     _same(sc, 48, 48, spp=1)
 
 
+@pytest.mark.parametrize("n", [3000, 20000])
+def test_bvh_hybrid_prefix(cornell, n):
+    """The hybrid: the Cornell faces that lead the mesh are scanned by the
+    scene-specialised module and left out of the BVH, which holds the random triangles only.
+    The stats must name the specialised module, and the frame and traversal count must be
+    the brute-force ones; the 20k case is large enough for carried traversals."""
+    sc = rvcp_amd.scene.with_random_triangles(cornell, n)
+    _, b = _same(sc, 160, 128, spp=2, time=3.5)
+    assert int(b[2]["kernel_variant"]) & rvcp_amd.abi.VARIANT_SPECIALIZED
+
+
 def test_bvh_moved_camera(cornell):
     base = rvcp_amd.Scene(rvcp_amd.Camera.new([120.0, 400.0, -700.0], [-50.0, 150.0, 100.0],
                                               0.1, 10000.0, 55.0, 150.0, 5.0),

@@ -54,3 +54,45 @@ def test_specialised_equals_generic_equals_oracle(seed):
     assert int(s[2]["traversals"]) == int(g[2]["traversals"]) == int(o_trav), desc
     # not an empty frame: some paths hit the geometry
     assert int(o_trav) > W * H * kw["spp"], desc
+
+
+def _with_specks(sc, n, seed):
+    """The fuzz scene with n small triangles appended, scattered over its bounding box
+    (material 0): enough faces behind the room for the BVH hybrid to leave
+    the leading room faces to the specialised scan and build the BVH over the rest."""
+    v = sc.mesh.aligned_vertices()
+    f = sc.mesh.aligned_faces()
+    pos = v["position"][:, :3].astype(np.float64)
+    lo, hi = pos.min(0), pos.max(0)
+    ext = np.maximum(hi - lo, 1e-30)
+    rng = np.random.default_rng(0xB1D + seed)
+    c = lo + rng.random((n, 3)) * ext
+    p = (c[:, None, :] + (rng.random((n, 3, 3)) - 0.5) * ext / 64).astype(np.float32)
+    V = rvcp_amd.scene.VERTEX_DTYPE
+    F = rvcp_amd.scene.FACE_DTYPE
+    nv = np.zeros(3 * n, V)
+    nv["position"][:, :3] = p.reshape(3 * n, 3)
+    nv["normal"][:, 1] = 1.0
+    nf = np.zeros(n, F)
+    nf["vertices"] = len(v) + np.arange(3 * n, dtype=np.uint32).reshape(n, 3)
+    mesh = rvcp_amd.scene.ArrayMesh(np.concatenate([v, nv]), np.concatenate([f, nf]))
+    return rvcp_amd.Scene(sc.camera, list(sc.materials), [], mesh)
+
+
+def test_bvh_hybrid_fuzz():
+    """The BVH hybrid on every fuzz scene with 160 small triangles appended: the specialised
+    scan over the leading faces plus the BVH over the rest == the generic brute-force scan,
+    bit for bit (linear RGB, RGBA8, traversal count).  The hybrid must engage (the stats name
+    the specialised module) on most of the scenes."""
+    engaged = 0
+    for seed in range(N_FUZZ):
+        sc0, kw, desc = fuzz_scene(seed)
+        sc = _with_specks(sc0, 160, seed)
+        t = 100.0 + seed
+        b = _render(sc, t, accel=rvcp_amd.abi.ACCEL_BVH, **kw)
+        g = _render(sc, t, specialize=rvcp_amd.abi.SPECIALIZE_OFF, **kw)
+        engaged += bool(int(b[2]["kernel_variant"]) & SPEC)
+        assert _diff(b, g) == 0, f"hybrid != generic on {_diff(b, g)} pixels; {desc}"
+        assert np.array_equal(b[0], g[0]), desc
+        assert int(b[2]["traversals"]) == int(g[2]["traversals"]), desc
+    assert engaged >= N_FUZZ // 2, f"hybrid engaged on {engaged} of {N_FUZZ} scenes"
