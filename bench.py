@@ -760,9 +760,21 @@ def main():
     # enqueued ahead.  Its ms per frame is config.interactive_ms_per_step beside ms_per_step.
     interactive_ms = None
     if args.interactive_pass > 0 and world == 1:
-        rts_i = [rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0)) for _ in range(2)]
-        for r in rts_i:
-            r.upload_scene(sc)
+        # the timed region's own contexts when they fit this shape (two or more, full grid);
+        # otherwise two new ones.  (Two more contexts beside the timed region's could share a
+        # hardware queue -- GPU_MAX_HW_QUEUES is 4 -- and then run one frame after another:
+        # measured, all 20 launches on one queue, 3.66 vs 3.02 ms, profiles/r06n_ovli.log.)
+        reuse = fif >= 2 and grid_waves == 0
+        rts_i = rts[:2] if reuse else [rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0))
+                                       for _ in range(2)]
+        if not reuse:
+            if grid_waves != 0:
+                # (the timed contexts are not used again: the launch pass below makes its own
+                # full-grid context; freeing theirs leaves the hardware queues to these two)
+                for r in rts:
+                    r.close()
+            for r in rts_i:
+                r.upload_scene(sc)
         bufs_i = [torch.zeros((H, W), dtype=torch.int32, device=dev) for _ in range(2)]
         sch_i = CallSchedule(
             2, 1, lambda i, pushes, nb: rts_i[i].render_shard_async(pushes[0], W, H, 0, 1,
@@ -774,8 +786,9 @@ def main():
         sch_i.run(args.interactive_pass)
         torch.cuda.synchronize()
         interactive_ms = (time.perf_counter() - ti) * 1000.0 / args.interactive_pass
-        for r in rts_i:
-            r.close()
+        if not reuse:
+            for r in rts_i:
+                r.close()
 
     # Isolated launch time (after the timed region): the path kernel with ONE frame in flight,
     # so its HIP-event time is its own (roofline.per_launch), on the full resident grid -- the

@@ -409,13 +409,10 @@ static int impl_create(const rvcp_config_t *cfg, rvcp_ctx_t **out_ctx)
         hipEventCreate(&ctx->evg1) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->evr, hipEventDisableTiming) != hipSuccess)
         return bail(fail(ctx, RVCP_E_HIP, "stream/event creation failed"));
-    {   // the frame gather's own stream, at the device's highest priority: its RCCL and
-        // assembly kernels are dispatched ahead of other streams' queued work (DESIGN.md §5)
-        int least = 0, greatest = 0;
-        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
-            hipStreamCreateWithPriority(&ctx->gstream, hipStreamNonBlocking, greatest) != hipSuccess)
-            return bail(fail(ctx, RVCP_E_HIP, "gather stream creation failed"));
-    }
+    // (the frame gather's own stream is created by the first gather that needs it: a context
+    // that never gathers holds one stream, so the hardware queues -- GPU_MAX_HW_QUEUES, 4 by
+    // default -- stay free for other contexts' render streams; frames in flight on contexts
+    // whose streams shared a queue would run one after another)
 
     // UNORM8 thresholds on the stored value g: u8 >= k  <=>  g >= G[k].
     // RVCP_UNORM_DRIVER: u8 = (floor(4096 g) * 255 + 2048) >> 12, so G[k] = m_k / 4096 with
@@ -1484,6 +1481,16 @@ static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, u
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     // the caller's stream, or the context's gather stream behind the render (evr): the
     // gather and rank 0's assembly then leave the render stream free for the next frame
+    if (!stream && !ctx->gstream) {
+        // the frame gather's own stream, at the device's highest priority: its RCCL and
+        // assembly kernels are dispatched ahead of other streams' queued work (DESIGN.md §5)
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+            hipStreamCreateWithPriority(&ctx->gstream, hipStreamNonBlocking, greatest) != hipSuccess) {
+            ctx->gstream = nullptr;
+            return fail(ctx, RVCP_E_HIP, "gather stream creation failed");
+        }
+    }
     hipStream_t s = stream ? (hipStream_t)stream : ctx->gstream;
     if (!stream) {
         HIP_TRY(ctx, hipEventRecord(ctx->evr, ctx->render_stream ? ctx->render_stream : ctx->stream));

@@ -61,6 +61,11 @@ for s in $STEPS; do
         # every launch timed (no warm-up, no launch pass): tools/trace_busy.py's busy time per frame,
 # skipping the warm-up launches the bench reports (config.warmup_frames / frames_per_launch)
         profbusy) run profbusy 600 rocprofv3 --kernel-trace --stats -d "$OUT/profbusy_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 && python3 tools/trace_busy.py "$OUT/profbusy_$TAG/run_kernel_trace.csv" --frames 20 --skip "$(python3 -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['config']; print(-(-d['warmup_frames'] // d['frames_per_launch']))" "$OUT/${TAG}_profbusy.log")" >> "$OUT/${TAG}_profbusy.log" ;;
+        # the reference's loop shape (1 frame per launch, 2 in flight) traced: do consecutive
+        # frames' kernels overlap (tools/trace_overlap.py)?
+        ovl) run ovl 300 rocprofv3 --kernel-trace -d "$OUT/ovl_$TAG" -o run --output-format csv -- python3 bench.py --steps 30 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 2 --batch 1 ${OVLARGS:-} && python3 tools/trace_overlap.py "$OUT/ovl_$TAG/run_kernel_trace.csv" >> "$OUT/${TAG}_ovl.log" ;;
+        ovli) run ovli 300 rocprofv3 --kernel-trace -d "$OUT/ovli_$TAG" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 20 ${OVLARGS:-} && python3 tools/trace_overlap.py "$OUT/ovli_$TAG/run_kernel_trace.csv" --last 20 >> "$OUT/${TAG}_ovli.log" ;;
+        fifsweep) for f in 1 2 3 4; do run fif$f 300 python bench.py --steps 40 --warmup 4 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 --frames-in-flight $f --batch 1 ${OVLARGS:-}; done ;;
         prof1) run prof1 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof1_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
         # PMC passes, one counter group per run (one frame in flight and one frame per launch, so
         # each dispatch is one frame of its own)
