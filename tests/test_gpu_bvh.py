@@ -58,6 +58,15 @@ def test_bvh_hybrid_prefix(cornell, n):
     assert int(b[2]["kernel_variant"]) & rvcp_amd.abi.VARIANT_SPECIALIZED
 
 
+def test_bvh_hybrid_prefix_generic(cornell):
+    """ray_t_min = 0 leaves the specialised module's range (its exactness argument needs
+    t_min > 0): the built-in BVH kernels then test the same prefix faces with the generic
+    test before the BVH (bvh_prefix_scan<false>); frames and counts as the brute-force scan."""
+    sc = rvcp_amd.scene.with_random_triangles(cornell, 3000)
+    _, b = _same(sc, 96, 80, spp=2, time=4.5, ray_t_min=0.0)
+    assert not int(b[2]["kernel_variant"]) & rvcp_amd.abi.VARIANT_SPECIALIZED
+
+
 def test_bvh_moved_camera(cornell):
     base = rvcp_amd.Scene(rvcp_amd.Camera.new([120.0, 400.0, -700.0], [-50.0, 150.0, 100.0],
                                               0.1, 10000.0, 55.0, 150.0, 5.0),
