@@ -47,7 +47,7 @@ for s in $STEPS; do
         benchtest) run pytest_bench 600 python -u -m pytest tests/test_gpu_bench.py -m gpu -x -v --timeout 280 --timeout-method thread ;;
         rankshare) run rank_share 300 python -u tools/rank_share.py ;;
         abi) run pytest_abi 300 python -u -m pytest tests/test_gpu_abi.py tests/test_gpu_specialize.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
-        bench) run bench_c3 600 python bench.py --steps 20 --warmup 3 ;;
+        bench) run bench_c3 600 python bench.py ;;
         benchq) run bench_c3q 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline ;;
         benchall) run bench_c3 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline && run bench_c2 300 python bench.py --workload c2 --steps 100 --warmup 10 --no-cpu-baseline && run bench_c4 300 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         benchc4) run bench_c4 300 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
@@ -57,7 +57,7 @@ for s in $STEPS; do
         benchs) run bench_spheres 300 python bench.py --workload spheres --steps 50 --warmup 5 --no-cpu-baseline ;;
         # the headline command under rocprofv3: default frames in flight, and one frame in flight
         # (per-launch durations that do not overlap -- roofline.per_launch)
-        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --interactive-pass 0 ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 bench.py --steps 60 --warmup 3 --no-cpu-baseline --interactive-pass 0 ;;
         # every launch timed (no warm-up, no launch pass): tools/trace_busy.py's busy time per frame,
 # skipping the warm-up launches the bench reports (config.warmup_frames / frames_per_launch)
         profbusy) run profbusy 600 rocprofv3 --kernel-trace --stats -d "$OUT/profbusy_$TAG" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 0 --launch-pass 0 --no-cpu-baseline --interactive-pass 0 && python3 tools/trace_busy.py "$OUT/profbusy_$TAG/run_kernel_trace.csv" --frames 20 --skip "$(python3 -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['config']; print(-(-d['warmup_frames'] // d['frames_per_launch']))" "$OUT/${TAG}_profbusy.log")" >> "$OUT/${TAG}_profbusy.log" ;;
