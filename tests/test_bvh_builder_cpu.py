@@ -104,3 +104,34 @@ def test_bvh4_split_clipping(checker, tmp_path):
         return float(line.split()[1])
 
     assert steps(checker) < 0.97 * steps(plain)
+
+
+def test_bvh4_hybrid_prefix(checker, tmp_path):
+    """The BVH hybrid (round 5, rvcp_host.cpp upload_one): bvh_big_prefix finds the 32 Cornell
+    faces that lead the C5-style mesh, the BVH is built over the rest, and brute force over the
+    prefix followed by the BVH gives the brute-force nearest hit on every ray, in fewer node
+    steps than the BVH over every face.  No prefix for a mesh of small triangles only, nor for
+    the Cornell box alone (fewer than 64 faces)."""
+    def run(tris, hybrid):
+        mesh = str(tmp_path / "mesh.bin")
+        np.ascontiguousarray(tris, np.float32).tofile(mesh)
+        r = subprocess.run([checker, mesh, "2000"] + (["hybrid"] if hybrid else []),
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "mismatches 0 of 2000" in r.stdout, r.stdout
+        k = int([l for l in r.stdout.splitlines() if l.startswith("prefix")][0].split()[1])
+        st = float([l for l in r.stdout.splitlines() if l.startswith("steps/ray")][0].split()[1])
+        return k, st
+
+    def positions(sc):
+        v = sc.mesh.aligned_vertices()
+        return v["position"][:, :3][sc.mesh.aligned_faces()["vertices"]]
+
+    cornell = rvcp_amd.Scene.default()
+    sc = rvcp_amd.scene.with_random_triangles(cornell, 20000)
+    k0, plain = run(positions(sc), False)
+    k1, hyb = run(positions(sc), True)
+    assert k0 == 0 and k1 == 32
+    assert hyb < 0.95 * plain
+    assert run(positions(sc)[32:], True)[0] == 0            # small triangles only
+    assert run(positions(cornell), True)[0] == 0            # 32 faces: below 64

@@ -2,12 +2,15 @@
 //          rvcp-real-time-path-tracer_amd/csrc/rvcp_bvh.cpp -o /tmp/bvh4_check
 // Input: raw float32 triangles [n][3][3] (e.g. the C5 mesh written by tools/dump_mesh.py).
 // CPU check of the real builder + collapse: stack bound, node count, traversal steps, and that
-// BVH4 traversal finds the same nearest hit as brute force on random rays.
+// BVH4 traversal finds the same nearest hit as brute force on random rays.  A third argument
+// `hybrid` checks the BVH hybrid instead (rvcp_host.cpp upload_one): the leading large faces
+// (bvh_big_prefix) tested by brute force first, the BVH built over the rest.
 #include <cstdio>
 #include <cmath>
 #include <vector>
 #include <random>
 #include <algorithm>
+#include <string>
 #include "rvcp_internal.h"
 using namespace rvcp;
 std::vector<float> P;
@@ -31,8 +34,12 @@ int main(int argc, char **argv) {
     FILE *f = fopen(argv[1], "rb"); float buf[9];
     while (fread(buf, 4, 9, f) == 9) P.insert(P.end(), buf, buf + 9);
     uint32_t n = P.size() / 9; int32_t root;
+    const bool hybrid = argc > 3 && std::string(argv[3]) == "hybrid";
+    const uint32_t K = hybrid ? bvh_big_prefix((const float (*)[3][3])P.data(), n, kJitMaxFaces) : 0u;
+    printf("prefix %u\n", K);
     std::vector<BvhNode> nodes; std::vector<uint32_t> order;
-    int depth = bvh_build((const float (*)[3][3])P.data(), n, nodes, order, root);
+    int depth = bvh_build((const float (*)[3][3])P.data() + K, n - K, nodes, order, root);
+    for (auto &id : order) if (id != kBvhPadId) id += K;
     std::vector<Bvh4Node> n4; int32_t r4;
     int need = bvh4_collapse(nodes, root, n4, r4);
     printf("n=%u nodes2=%zu depth=%d nodes4=%zu stack bound=%d\n", n, nodes.size(), depth, n4.size(), need);
@@ -62,6 +69,7 @@ int main(int argc, char **argv) {
         l = std::sqrt(l); for (int k = 0; k < 3; k++) d[k] /= l;
         float inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
         float bt = 1e30f; int best = -1; int32_t st[64]; int sp = 0; int32_t ref = r4;
+        for (uint32_t i = 0; i < K; i++) { float t; if (tri(&P[9 * i], o, d, 1e-4f, bt, t)) { bt = t; best = i; } }
         for (;;) {
             steps++;
             if (ref >= 0) {
