@@ -174,7 +174,10 @@ typedef struct rvcp_config {
      * bounding-volume hierarchy at upload and tests only the triangles whose (slightly
      * enlarged) boxes the ray reaches, with the same exact triangle test and nearest-hit
      * rule; frames match the brute-force ones except where a ray runs almost parallel to a
-     * triangle's plane. */
+     * triangle's plane.  With specialize = AUTO, a mesh whose leading faces
+     * (at most 64) are all large -- a room around many small triangles, as C5 -- keeps those
+     * faces out of the BVH and tests them first with the scene-specialised scan (the BVH
+     * hybrid; stats report RVCP_VARIANT_SPECIALIZED). */
     int32_t accel;
     /* GPUs one context drives (0 or 1 = one).  With n_gpus = N > 1, rvcp_create opens devices
      * device, device+1, ... (mod the device count), rvcp_upload_scene uploads to all of them,
@@ -193,8 +196,9 @@ typedef struct rvcp_config {
     int32_t unorm_rule;
     /* Scene-specialised scan: RVCP_SPECIALIZE_AUTO (0, default) compiles, at
      * rvcp_upload_scene, path kernels whose triangle scan is written out for the uploaded
-     * scene (games101 integrator, brute force, at most 64 faces; hipRTC, ~2 s once per scene
-     * and process) and uses them for schedules 3 and 6 when ray_t_min > 0.  Frames are
+     * scene (games101 integrator, brute force, at most 64 faces; hipRTC, ~1 s once per scene
+     * and process) and uses them for schedules 3 and 6 when ray_t_min > 0 (and, with accel =
+     * BVH, for the BVH hybrid's leading faces).  Frames are
      * bit-identical to the generic kernels; without hipRTC the generic kernels run.
      * RVCP_SPECIALIZE_OFF (1): always the generic kernels. */
     int32_t specialize;
