@@ -654,7 +654,25 @@ struct BvhCarry {
     int sp = 0;             // stack depth (the stack is the lane's LDS column)
     float bt = 0.0f;
     int best = -1;
+    float stop = 0.0f;      // a shadow ray ends once bt <= stop (shadow_stop); -inf: never
 };
+
+// The shadow ray's early end (bvh_pool).  Resolve A (:447-449) only asks whether
+// |dist - |hp - p|| < eps, hp = a_o + a_d t at the nearest hit t.  With a_o = p + ws eps (rounded)
+// and a_d = ws, the computed |hp - p| is at most (eps + t)(1 + 8u) + 10 u M for any t in
+// [0, dist] (u = 2^-24, M = max |p_k| + eps + dist: the rounding of a_o, of a_d t, of the sum, of
+// hp - p, of the dot product and of the root), so every hit with t <= stop below -- the one
+// found and the nearest, which is no farther -- gives |hp - p| <= dist - eps: the light sample
+// is blocked either way, and the traversal may end at the first such hit.  The margin is
+// 2^-18 (M + dist + eps), four times what that bound needs, so the float evaluation of stop
+// (a few ulps of dist) stays inside it.  t_min < 0 (hits behind the origin) or a non-finite
+// dist: never (-inf / NaN compare false).
+__device__ __forceinline__ float shadow_stop(float eps, float t_min, f3 p, float dist) {
+    const float M = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(p.x), __builtin_fabsf(p.y)),
+                                    __builtin_fabsf(p.z)) + eps + dist;
+    const float stop = dist - 2.0f * eps - 0x1p-18f * (M + dist + eps);
+    return t_min >= 0.0f ? stop : -__builtin_inff();
+}
 __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
                                       const TriRecord *__restrict__ btri, int32_t root,
                                       lds_i32 *stk, uint8_t *tab, float2 *res, uint32_t lane,
@@ -662,7 +680,8 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
                                       float tmin, float tmax, bool may_carry, BvhCarry &c,
                                       bool &subA, bool &subB, bool &frozen, float &btA, int &bestA,
                                       float &btB, int &bestB, uint32_t n4, uint32_t slots,
-                                      float ibtA, int ibestA, float ibtB, int ibestB) {
+                                      float ibtA, int ibestA, float ibtB, int ibestB,
+                                      float istopA) {
     const uint64_t mA = __ballot(nA_), mB = __ballot(nB_);
     const uint32_t nA = (uint32_t)__builtin_popcountll(mA);
     const uint32_t nr = nA + (uint32_t)__builtin_popcountll(mB);
@@ -707,6 +726,7 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
             // the ray's starting bound and candidate: t_max / none, or the hybrid prefix's hit
             const float i_tA = __shfl(ibtA, src), i_tB = __shfl(ibtB, src);
             const int i_bA = __shfl(ibestA, src), i_bB = __shfl(ibestB, src);
+            const float i_sA = __shfl(istopA, src);
             if (take) {
                 const bool isA = rr < nA;
                 c.key = 2u * (uint32_t)src + (isA ? 0u : 1u);
@@ -718,8 +738,10 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
                 c.sp = 0;
                 c.bt = isA ? i_tA : i_tB;
                 c.best = isA ? i_bA : i_bB;
+                c.stop = isA ? i_sA : -__builtin_inff();
                 c.has = true;
-                alive = true;
+                // (a shadow ray the hybrid prefix already blocked needs no traversal)
+                alive = !(c.bt <= c.stop);
                 parked = false;
             }
             const uint32_t pm = (uint32_t)__builtin_popcountll(M);
@@ -746,6 +768,7 @@ __device__ __forceinline__ void bvh_pool(const Bvh4Node *__restrict__ nodes,
         if (parked) {
             bvh_leaf<kBvhPoolChunk>(btri, lref, o, d, tmin, c.bt, c.best, slots);
             parked = false;
+            if (c.bt <= c.stop) alive = false;      // a shadow ray already blocked (shadow_stop)
         }
         if (c.has && !alive) {          // this ray is done: leave its result for the owner
             res[c.key] = make_float2(c.bt, __int_as_float(c.best));
@@ -2304,7 +2327,12 @@ __device__ __forceinline__ void path_body(
                 bvh_pool(bvh_nodes, bvh_tris, A.bvh_root, stk, reinterpret_cast<uint8_t *>(pl + 64),
                          reinterpret_cast<float2 *>(pl), lane, newA, newB, s_ao, s_ad, b_o, b_d,
                          A.t_min, A.t_max, !q.exhausted, carry, subA, subB, frozen, btA, bestA,
-                         btB, bestB, A.bvh_n4, A.bvh_slots, pbtA, pbestA, pbtB, pbestB);
+                         btB, bestB, A.bvh_n4, A.bvh_slots, pbtA, pbestA, pbtB, pbestB,
+#ifdef RVCP_NO_SHADOW_STOP     // A/B: every shadow ray traversed to its nearest hit
+                         -__builtin_inff());
+#else
+                         newA ? shadow_stop(A.eps, A.t_min, a_p, nee_dist) : -__builtin_inff());
+#endif
             } else
             {
             if (A.bvh_prefix)
