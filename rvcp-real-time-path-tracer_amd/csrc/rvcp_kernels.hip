@@ -2109,6 +2109,15 @@ __device__ __forceinline__ void path_body(
             // test wherever it is scanned, so every nearest hit is unchanged.
             f3 so0 = s_ao, sd0 = s_ad, so1 = b_o, sd1 = b_d;
             uint64_t m0 = mA, m1 = mB;
+            // a slot's shadow ray leaves the scan's gates once a hit already blocks its light
+            // sample (shadow_stop; -inf: a path ray, never); a wave whose slots are all settled
+            // skips the tests of the remaining tiles (it still loads them with the workgroup)
+#ifdef RVCP_NO_SHADOW_STOP
+            const float my_stop = -__builtin_inff();
+#else
+            const float my_stop = hasA ? shadow_stop(A.eps, A.t_min, a_p, nee_dist) : -__builtin_inff();
+#endif
+            float stop0 = my_stop, stop1 = -__builtin_inff();
             bool ttail = tail;
             uint32_t R = 1, part = 0;
             bool worker = false;
@@ -2120,11 +2129,11 @@ __device__ __forceinline__ void path_body(
                 jA = pool_baseA + rank_in(mA);
                 jB = pool_baseB + rank_in(mB);
                 if (sA) {
-                    pool[2 * jA] = make_float4(s_ao.x, s_ao.y, s_ao.z, 0.0f);
+                    pool[2 * jA] = make_float4(s_ao.x, s_ao.y, s_ao.z, my_stop);
                     pool[2 * jA + 1] = make_float4(s_ad.x, s_ad.y, s_ad.z, 0.0f);
                 }
                 if (sB) {
-                    pool[2 * jB] = make_float4(b_o.x, b_o.y, b_o.z, 0.0f);
+                    pool[2 * jB] = make_float4(b_o.x, b_o.y, b_o.z, -__builtin_inff());
                     pool[2 * jB + 1] = make_float4(b_d.x, b_d.y, b_d.z, 0.0f);
                 }
                 __syncthreads();
@@ -2155,6 +2164,8 @@ __device__ __forceinline__ void path_body(
                     sd0 = mk(d0r.x, d0r.y, d0r.z);
                     so1 = mk(o1r.x, o1r.y, o1r.z);
                     sd1 = mk(d1r.x, d1r.y, d1r.z);
+                    stop0 = o0r.w;
+                    stop1 = o1r.w;
                     m0 = __ballot(v0);
                     m1 = __ballot(v1);
                 }
@@ -2185,6 +2196,7 @@ __device__ __forceinline__ void path_body(
                 btA = btB = A.t_max;
                 bestA = bestB = -1;
             }
+            uint64_t a0 = m0, a1 = m1;      // the slots' lanes still scanning
             for (uint32_t base = 0; base < A.n_faces; base += kTile) {
                 const uint32_t n = A.n_faces - base < kTile ? A.n_faces - base : kTile;
                 const float4 *src = reinterpret_cast<const float4 *>(tri + base);
@@ -2198,7 +2210,7 @@ __device__ __forceinline__ void path_body(
                             if (tri_accept(tile[i], o, d, A.t_min, bt, t)) { bt = t; best = (int)(base + i); }
                         }
                     }
-                } else if ((m0 | m1) != 0ull) {
+                } else if ((a0 | a1) != 0ull) {
                     // Two-stage exact test: stage 2 (1/den, t, b1, b2, the
                     // compares) only when some lane may accept.  (A software-pipelined read of
                     // the next triangle costs 12 VGPRs and was slower at 4 waves/SIMD.)
@@ -2217,10 +2229,10 @@ __device__ __forceinline__ void path_body(
 #pragma unroll
                         for (uint32_t h = 0; h < kStep; ++h) {
                             Pa[h] = tri_stage1a(Tp[h], so0, sd0);
-                            ga[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pa[h])) & m0;
+                            ga[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pa[h])) & a0;
                             if (!SINGLE) {
                                 Pb[h] = tri_stage1a(Tp[h], so1, sd1);
-                                gb[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pb[h])) & m1;
+                                gb[h] = __builtin_amdgcn_ballot_w64(tri_maybe_a(Pb[h])) & a1;
                             }
                         }
 #pragma unroll
@@ -2248,7 +2260,7 @@ __device__ __forceinline__ void path_body(
                         // compare each): __any(sA && p) materialised the predicate in a VGPR
                         // and compared it again, 2 VALU per gate (C5 schedule 4: -7 %)
                         const TriPartA PaA = tri_stage1a(T, so0, sd0);
-                        const uint64_t gA = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaA)) & m0;
+                        const uint64_t gA = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaA)) & a0;
                         if (gA != 0ull) {
                             const TriPart PA = tri_stage1b(T, PaA, sd0);
                             if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PA.n2) <= PaA.m) & gA) != 0ull) {
@@ -2258,7 +2270,7 @@ __device__ __forceinline__ void path_body(
                         }
                         if (!SINGLE) {
                             const TriPartA PaB = tri_stage1a(T, so1, sd1);
-                            const uint64_t gB = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaB)) & m1;
+                            const uint64_t gB = __builtin_amdgcn_ballot_w64(tri_maybe_a(PaB)) & a1;
                             if (gB != 0ull) {
                                 const TriPart PB = tri_stage1b(T, PaB, sd1);
                                 if ((__builtin_amdgcn_ballot_w64(__builtin_fabsf(PB.n2) <= PaB.m) & gB) != 0ull) {
@@ -2268,6 +2280,8 @@ __device__ __forceinline__ void path_body(
                             }
                         }
                     }
+                    a0 &= ~__builtin_amdgcn_ballot_w64(btA <= stop0);
+                    if (!SINGLE) a1 &= ~__builtin_amdgcn_ballot_w64(btB <= stop1);
                 }
                 __syncthreads();
             }
