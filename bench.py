@@ -482,7 +482,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     # 60 frames by default: the pipeline's fill and drain (the last launch's tail, which no
     # later frame overlaps) spread over 60 frames instead of 20 -- C3 2.848 / 2.775 / 2.750 ms
-    # per frame at 20 / 40 / 60 (profiles/r06t_ab_steps.log); the run still takes well under
+    # per frame at 20 / 40 / 60 (profiles/r05zt_ab_steps.log); the run still takes well under
     # a second of GPU time
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=3)
@@ -767,7 +767,7 @@ def main():
         # the timed region's own contexts when they fit this shape (two or more, full grid);
         # otherwise two new ones.  (Two more contexts beside the timed region's could share a
         # hardware queue -- GPU_MAX_HW_QUEUES is 4 -- and then run one frame after another:
-        # measured, all 20 launches on one queue, 3.66 vs 3.02 ms, profiles/r06n_ovli.log.)
+        # measured, all 20 launches on one queue, 3.66 vs 3.02 ms, profiles/r05zn_ovli.log.)
         reuse = fif >= 2 and grid_waves == 0
         rts_i = rts[:2] if reuse else [rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0))
                                        for _ in range(2)]
