@@ -47,12 +47,13 @@ def test_bvh_c5_mesh(cornell):
     _same(sc, 48, 48, spp=1)
 
 
-@pytest.mark.parametrize("n", [3000, 20000])
+@pytest.mark.parametrize("n", [310, 3000, 20000])
 def test_bvh_hybrid_prefix(cornell, n):
     """The hybrid: the Cornell faces that lead the mesh are scanned by the
     scene-specialised module and left out of the BVH, which holds the random triangles only.
     The stats must name the specialised module, and the frame and traversal count must be
-    the brute-force ones; the 20k case is large enough for carried traversals."""
+    the brute-force ones; 310 is the c6 mesh, the 20k case is large enough for carried
+    traversals."""
     sc = rvcp_amd.scene.with_random_triangles(cornell, n)
     _, b = _same(sc, 160, 128, spp=2, time=3.5)
     assert int(b[2]["kernel_variant"]) & rvcp_amd.abi.VARIANT_SPECIALIZED
