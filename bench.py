@@ -512,10 +512,11 @@ def main():
                          "wait (rvcp_rccl_set_timeout); past it the rank aborts its communicator "
                          "-- at creation every rank then takes the labelled host gather, during "
                          "the run the command exits non-zero with a line naming rank and stage")
-    ap.add_argument("--interactive-pass", type=int, default=20,
+    ap.add_argument("--interactive-pass", type=int, default=60,
                     help="N=1: frames of the post-timing pass in the reference's own loop shape "
-                         "(one frame per launch, 2 in flight, each frame's push made just before "
-                         "its submission: ray_tracer.rs:80-98, vulkan.rs:367-369) -> "
+                         "(one frame per launch, one in flight per swapchain image -- at most 3, "
+                         "vulkan.rs:213 -- each frame's push made just before its submission: "
+                         "ray_tracer.rs:80-98, vulkan.rs:367-369) -> "
                          "config.interactive_ms_per_step (0 = skip)")
     ap.add_argument("--launch-pass", type=int, default=10,
                     help="frames (at most --steps) of the post-timing one-frame-in-flight pass "
@@ -758,42 +759,6 @@ def main():
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed * 1000.0 / args.steps
 
-    # The reference's own loop shape (after the timed region): one frame per submission, the
-    # push constant of each frame stamped just before it is submitted (ray_tracer.rs:80-98),
-    # two frames in flight behind per-image fences (vulkan.rs:367-369) -- no batches, nothing
-    # enqueued ahead.  Its ms per frame is config.interactive_ms_per_step beside ms_per_step.
-    interactive_ms = None
-    if args.interactive_pass > 0 and world == 1:
-        # the timed region's own contexts when they fit this shape (two or more, full grid);
-        # otherwise two new ones.  (Two more contexts beside the timed region's could share a
-        # hardware queue -- GPU_MAX_HW_QUEUES is 4 -- and then run one frame after another:
-        # measured, all 20 launches on one queue, 3.66 vs 3.02 ms, profiles/r05zn_ovli.log.)
-        reuse = fif >= 2 and grid_waves == 0
-        rts_i = rts[:2] if reuse else [rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=0))
-                                       for _ in range(2)]
-        if not reuse:
-            if grid_waves != 0:
-                # (the timed contexts are not used again: the launch pass below makes its own
-                # full-grid context; freeing theirs leaves the hardware queues to these two)
-                for r in rts:
-                    r.close()
-            for r in rts_i:
-                r.upload_scene(sc)
-        bufs_i = [torch.zeros((H, W), dtype=torch.int32, device=dev) for _ in range(2)]
-        sch_i = CallSchedule(
-            2, 1, lambda i, pushes, nb: rts_i[i].render_shard_async(pushes[0], W, H, 0, 1,
-                                                                   bufs_i[i].data_ptr()),
-            lambda i, nb: rts_i[i].sync_stats(), lambda t: sc.push_constant(t))
-        sch_i.run(4)
-        torch.cuda.synchronize()
-        ti = time.perf_counter()
-        sch_i.run(args.interactive_pass)
-        torch.cuda.synchronize()
-        interactive_ms = (time.perf_counter() - ti) * 1000.0 / args.interactive_pass
-        if not reuse:
-            for r in rts_i:
-                r.close()
-
     # Isolated launch time (after the timed region): the path kernel with ONE frame in flight,
     # so its HIP-event time is its own (roofline.per_launch), on the full resident grid -- the
     # launch a one-frame-at-a-time caller makes (a grid left partly free for the next frame,
@@ -813,6 +778,48 @@ def main():
             latency_ms.append((time.perf_counter() - tl) * 1000.0)
         if rt_iso is not rt:
             rt_iso.close()
+
+    # The reference's own loop shape (after the timed region and the launch pass): one frame
+    # per submission, the push constant of each frame stamped just before it is submitted
+    # (ray_tracer.rs:80-98), one frame in flight per swapchain image behind per-image fences
+    # (vulkan.rs:367-369) -- min_image_count + 1 images (vulkan.rs:213), 3 on common drivers --
+    # no batches, nothing enqueued ahead.  Its pipeline is auto_pipeline's for single frames
+    # (frames up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD), at most 3 in flight; its ms
+    # per frame is config.interactive_ms_per_step beside ms_per_step.
+    interactive_ms = None
+    fif_i = grid_i = None
+    if args.interactive_pass > 0 and world == 1:
+        fif_i, grid_i, _ = auto_pipeline(W * H, spp, legacy, small_scene, hw_queues, args.accel, 1)
+        fif_i = min(fif_i, 3)
+        reuse = fif == fif_i and grid_waves == grid_i
+        if reuse:
+            rts_i = rts[:fif_i]
+        else:
+            # the timed contexts are not used again at world 1: freed first, so that the new
+            # ones get hardware queues of their own (GPU_MAX_HW_QUEUES is 4; contexts sharing a
+            # queue run their frames one after another: C3 3.66 vs 2.91 ms per frame,
+            # profiles/r05zn_ovli.log; 3 in flight on 3 waves per SIMD: 2.82 ms,
+            # r05zzj_ab_c3interactive.log)
+            for r in rts:
+                r.close()
+            rts_i = [rvcp_amd.RayTracer(**dict(cfg_kw, grid_waves_per_simd=grid_i))
+                     for _ in range(fif_i)]
+            for r in rts_i:
+                r.upload_scene(sc)
+        bufs_i = [torch.zeros((H, W), dtype=torch.int32, device=dev) for _ in range(fif_i)]
+        sch_i = CallSchedule(
+            fif_i, 1, lambda i, pushes, nb: rts_i[i].render_shard_async(pushes[0], W, H, 0, 1,
+                                                                       bufs_i[i].data_ptr()),
+            lambda i, nb: rts_i[i].sync_stats(), lambda t: sc.push_constant(t))
+        sch_i.run(2 * fif_i)
+        torch.cuda.synchronize()
+        ti = time.perf_counter()
+        sch_i.run(args.interactive_pass)
+        torch.cuda.synchronize()
+        interactive_ms = (time.perf_counter() - ti) * 1000.0 / args.interactive_pass
+        if not reuse:
+            for r in rts_i:
+                r.close()
 
     # roofline of the dominant kernel (this rank's launches).  The pre-pass (schedules 3-6,
     # games101 only) traces each pixel's primary ray once; every other reference-algorithm
@@ -965,6 +972,8 @@ def main():
                        "interactive_ms_per_step": (None if interactive_ms is None else
                                                    round(interactive_ms, 4)),
                        "interactive_frames": args.interactive_pass if interactive_ms else 0,
+                       "interactive_frames_in_flight": fif_i,
+                       "interactive_grid_waves_per_simd": grid_i,
                        "gpu_max_hw_queues": hw_queues,
                        "gather": ("none" if world == 1 else
                                   "gloo-rehearsal (all ranks on GPU 0)" if rehearsal else
