@@ -67,6 +67,19 @@ def test_auto_pipeline():
     assert ap(1024 * 1024, 30, False, True, "x", "none", 20) == (2, 0, 4)
 
 
+def test_interactive_pipeline():
+    """The reference's loop shape (bench.py's interactive pass): auto_pipeline for single
+    frames (steps = 1: no batches), at most 3 in flight -- one per swapchain image,
+    min_image_count + 1 (vulkan.rs:213)."""
+    ap = bench.auto_pipeline
+    assert ap(1024 * 1024, 30, False, True, "4", "none", 1) == (3, 3, 1)           # C3
+    assert ap(384 * 384, 10, False, True, "4", "none", 1) == (3, 3, 1)             # C2
+    assert ap(1024 * 1024, 5, True, True, "4", "none", 1) == (3, 3, 1)             # sphere room
+    assert ap(1024 * 1024, 30, False, False, "4", "bvh", 1) == (3, 3, 1)           # C5, BVH
+    assert ap(1024 * 1024, 30, False, False, "4", "none", 1) == (2, 0, 1)          # c6 / C5 mesh
+    assert ap(2048 * 2048, 64, False, True, "4", "none", 1) == (2, 0, 1)           # C4 frame
+
+
 def test_roofline_constants():
     assert bench.FLOP_PER_TEST == 52 and bench.FP32_PEAK_TFLOPS == 157.3
     assert bench.REFERENCE_MSAMPLES["c3"] == pytest.approx(1024 * 1024 * 30 * 3 / 1e6, rel=0.01)
