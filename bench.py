@@ -145,38 +145,77 @@ def workload(name, n_gpus):
     raise SystemExit(f"unknown workload {name}")
 
 
+def profile_summary(kind, workload_name, kernel_name):
+    """The newest committed PMC summary of `kind` ("valu": tools/pmc_valu.py, "traffic":
+    tools/pmc_traffic.py) for the workload: (the dominant kernel's record or None, the file
+    relative to the repo or None, the build it measured -- {"source", "module"} from the PMC
+    pass's own bench line, tools/pmc_*.py --bench-log -- or None for a summary without one)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{kind}_{workload_name}.json")))
+    if not files:
+        return None, None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    rec = next((k for name, k in d.get("kernels", {}).items() if kernel_name in name), None)
+    return rec, os.path.relpath(files[-1], ROOT), d.get("build")
+
+
 def load_valu_busy(workload_name, kernel_name, want_insts=False):
     """VALU issue utilisation of the dominant kernel from the newest committed SQ PMC summary:
     (busy at 2 cycles per wave64 instruction, fraction of the measured issue peak), and with
-    want_insts also (wave64 VALU instructions per launch, summary file)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_valu_{workload_name}.json")))
-    none = (None, None, None, None) if want_insts else (None, None)
-    if not files:
-        return none
-    with open(files[-1]) as f:
-        d = json.load(f)
-    for name, k in d.get("kernels", {}).items():
-        if kernel_name in name:
-            if want_insts:
-                return (k.get("valu_busy"), k.get("issue_frac"), k.get("valu_insts"),
-                        os.path.relpath(files[-1], ROOT))
-            return k.get("valu_busy"), k.get("issue_frac")
-    return none
+    want_insts also (wave64 VALU instructions per launch, summary file).  Whatever build the
+    summary measured (bench.py checks that with profile_summary's build)."""
+    k, src, _ = profile_summary("valu", workload_name, kernel_name)
+    if k is None:
+        return (None, None, None, None) if want_insts else (None, None)
+    if want_insts:
+        return k.get("valu_busy"), k.get("issue_frac"), k.get("valu_insts"), src
+    return k.get("valu_busy"), k.get("issue_frac")
 
 
 def load_traffic(workload_name, kernel_name):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{workload_name}.json")))
-    if not files:
+    k, src, _ = profile_summary("traffic", workload_name, kernel_name)
+    if k is None or not k.get("bytes"):
         return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    for name, k in d.get("kernels", {}).items():
-        if kernel_name in name and k.get("bytes"):
-            return float(k["bytes"]), os.path.relpath(files[-1], ROOT)
-    return None, None
+    return float(k["bytes"]), src
+
+
+def build_identity(rt):
+    """What this run executes: the library's source identity (SHA-256 prefix of the sources it
+    was built from, rvcp_internal_build_id) and the key of rt's scene-specialised module
+    (hipRTC version, options, embedded sources and generated scan; None when the generic
+    kernels run).  PMC-derived roofline fields are reported only from a summary of this same
+    build."""
+    import ctypes
+    L = rvcp_amd_abi().load()
+    L.rvcp_internal_build_id.restype = ctypes.c_char_p
+    L.rvcp_internal_module_key.restype = ctypes.c_uint64
+    L.rvcp_internal_module_key.argtypes = [ctypes.c_void_p]
+    key = int(L.rvcp_internal_module_key(rt.handle))
+    return {"source": L.rvcp_internal_build_id().decode(), "module": f"{key:016x}" if key else None}
+
+
+def rvcp_amd_abi():
+    import rvcp_amd
+    return rvcp_amd.abi
+
+
+def bound_profile(kind, workload_name, kernel_name, build):
+    """profile_summary's record when it measured `build`, else None; and the binding record the
+    line carries: {source file, its build, match}."""
+    rec, src, pbuild = profile_summary(kind, workload_name, kernel_name)
+    match = None if rec is None else (pbuild == build)
+    return (rec if match else None), {"source": src, "build": pbuild, "build_match": match}
+
+
+def vs_baseline_loop_shape(wname, world, samples_per_frame, interactive_ms):
+    """vs_baseline on the reference's own loop shape: the interactive pass's Msamples/s (one
+    frame per launch, pushes stamped at submission, at most 3 in flight) over the reference's
+    published Msamples/s for the same frame; None without a published row or without the pass."""
+    if world != 1 or wname not in REFERENCE_MSAMPLES or not interactive_ms:
+        return None
+    return round(samples_per_frame / (interactive_ms / 1000.0) / 1e6 / REFERENCE_MSAMPLES[wname], 2)
 
 
 def cpu_model():
@@ -529,13 +568,11 @@ def main():
         # anything here touches the GPU
         sys.exit(self_launch(args.gpus, sys.argv[1:]))
 
-    # Hardware queues per process: HIP's default is 4; with 4 frames in flight on small frames
-    # (C2) the contexts' streams then share queues and serialise.  8 queues let C2 take a fourth
-    # frame: 0.284 -> 0.269 ms (profiles/r02_hwq_fif_sweep.log).  Only when the variable is unset
-    # (an explicit value is the user's), before HIP initialises; the value used is in the line.
-    if "GPU_MAX_HW_QUEUES" not in os.environ:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
-    hw_queues = os.environ["GPU_MAX_HW_QUEUES"]
+    # Hardware queues per process: the process's own setting, else HIP's default of 4 (what the
+    # GPU box runs).  No override: frames in flight are sized to the queues
+    # (auto_pipeline keeps them below the queue count), and contexts sharing a queue would run
+    # their frames one after another.  The value used is in the line.
+    hw_queues = os.environ.get("GPU_MAX_HW_QUEUES", "4")
 
     import torch
     import torch.distributed as dist
@@ -941,9 +978,18 @@ def main():
             "frame_interval_ms_median": round(float(np.median(intervals)), 4) if intervals else None,
             "higher_is_better": True,
             "scaling": wl["scaling"],
-            # the reference's published rows are single-GPU (RTX 3060) C3 / C2 frames
-            "vs_baseline": (round(value / REFERENCE_MSAMPLES[wname], 2)
-                            if world == 1 and wname in REFERENCE_MSAMPLES else None),
+            # the reference's published rows are single-GPU (RTX 3060) C3 / C2 frames, timed by
+            # its own loop (one frame per submission, a push per frame made just before it,
+            # ray_tracer.rs:80-98): compared on that loop shape here (the interactive pass), not
+            # on the batched pipeline's rate, which the reference's loop cannot run
+            "vs_baseline": vs_baseline_loop_shape(wname, world, W * H * spp, interactive_ms),
+            "vs_baseline_batched": (round(value / REFERENCE_MSAMPLES[wname], 2)
+                                    if world == 1 and wname in REFERENCE_MSAMPLES else None),
+            "vs_baseline_definition": (
+                "Msamples/s of the reference's loop shape (config.interactive_ms_per_step: one "
+                "frame per launch, one in flight per swapchain image, push stamped at submission) "
+                "/ the reference's published row (README.md:19-26, RTX 3060); "
+                "vs_baseline_batched: value (batched pipeline) / the same row"),
             "dtype": "f32",
             "data": ("synthetic (the reference's deprecated sphere-room scene, integrator mode 2"
                      if wl.get("scene") == "spheres" else
@@ -966,11 +1012,14 @@ def main():
                        # rvcp_render of this rank's frame; ms_per_step is the pipelined rate)
                        "frame_latency_ms_alone": (round(float(np.median(latency_ms)), 4)
                                                   if latency_ms else None),
-                       # the reference's loop shape: one frame per launch, 2 in flight, a push
-                       # per frame made just before its submission (ray_tracer.rs:80-98,
-                       # vulkan.rs:367-369); ms_per_step is the batched pipeline's rate
+                       # the reference's loop shape: one frame per launch, one in flight per
+                       # swapchain image (at most 3), a push per frame made just before its
+                       # submission (ray_tracer.rs:80-98, vulkan.rs:213, 367-369); ms_per_step
+                       # is the batched pipeline's rate.  vs_baseline is quoted on this one.
                        "interactive_ms_per_step": (None if interactive_ms is None else
                                                    round(interactive_ms, 4)),
+                       "interactive_msamples_s": (None if not interactive_ms else
+                                                  round(W * H * spp / (interactive_ms / 1000.0) / 1e6, 2)),
                        "interactive_frames": args.interactive_pass if interactive_ms else 0,
                        "interactive_frames_in_flight": fif_i,
                        "interactive_grid_waves_per_simd": grid_i,

@@ -273,6 +273,14 @@ typedef struct rvcp_ctx rvcp_ctx_t;
 #define RVCP_E_TIMEOUT      (-7)   /* a collective did not complete within the deadline
                                     * (rvcp_rccl_set_timeout): a peer rank is missing or failed;
                                     * the context's own communicator has been aborted */
+#define RVCP_E_BUSY         (-8)   /* rvcp_rccl_init refused: the context's previous creation
+                                    * timed out and its worker is still blocked inside RCCL */
+
+/* ABI revision of this header, returned by rvcp_abi_version().  2 (round 6): rvcp_stats_t grew
+ * from 56 to 64 bytes (shader_clock_ghz), RVCP_E_TIMEOUT / RVCP_E_BUSY, rvcp_abi_version and the
+ * code-cache entry points.  A caller compiled against another revision must not pass its
+ * rvcp_stats_t ("ABI revisions"). */
+#define RVCP_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------------------------
  * Entry points
@@ -280,6 +288,27 @@ typedef struct rvcp_ctx rvcp_ctx_t;
 
 /* Library version string. */
 const char *rvcp_version(void);
+
+/* RVCP_ABI_VERSION of the header the library was built with: a caller checks it against its
+ * own before passing structs (rvcp_stats_t changed size between revisions 1 and 2). */
+uint32_t rvcp_abi_version(void);
+
+/* On-disk cache of the scene-specialised code objects: rvcp_upload_scene
+ * compiles a module per scene with hipRTC (~0.7 s); with a cache directory the code object is
+ * stored under a key that covers the generated source, the kernel source, the compile options
+ * and the hipRTC version, and a later process that uploads the same scene loads it instead.
+ * An entry is checked (header, key, length, checksum) before it is loaded; a damaged or
+ * foreign entry is recompiled and rewritten, never trusted.  The reference has no counterpart
+ * (its SPIR-V is compiled into the binary, src/ray_tracer/shader.rs:9-14).
+ * dir: the directory (created if missing); NULL or "" disables the cache.  Default:
+ * $XDG_CACHE_HOME/rvcp-mi355x, else $HOME/.cache/rvcp-mi355x (the only environment the product
+ * library reads).  Process-wide. */
+int rvcp_set_code_cache_dir(const char *dir);
+
+/* Counters of the on-disk cache since the process started: out[0] modules loaded from disk,
+ * out[1] modules compiled (and stored), out[2] entries rejected (damaged / foreign / unloadable)
+ * and recompiled. */
+int rvcp_code_cache_counts(uint64_t out[3]);
 
 /* Fill `cfg` with the reference's #define defaults.  Replaces nothing (the reference bakes
  * them into the SPIR-V at `vulkano_shaders::shader!`, src/ray_tracer/shader.rs:9-14). */
@@ -424,9 +453,13 @@ int rvcp_rccl_unique_id(uint8_t out_id[RVCP_RCCL_ID_BYTES]);
 
 /* Every rank, collectively: create ctx's communicator (non-blocking ncclCommInitRankConfig on
  * ctx's device, polled with ncclCommGetAsyncError).  Returns once all `world` ranks have
- * joined, or RVCP_E_TIMEOUT when they have not within the context's deadline (the half-made
- * communicator is aborted with ncclCommAbort; the context stays usable and may try again).
- * Destroyed with the context.  The reference has no counterpart (single device); its own
+ * joined, or RVCP_E_TIMEOUT when they have not within the context's deadline.  The creation
+ * runs on a worker thread, because RCCL's "non-blocking" creation call itself does not return
+ * while a peer is absent: on a timeout the worker is left behind (it aborts the half-made
+ * communicator if RCCL ever returns), the message counts such workers in the process, and the
+ * context refuses a further rvcp_rccl_init with RVCP_E_BUSY while its worker is still blocked --
+ * at most one blocked worker per context; the context stays usable for single-GPU renders (and
+ * rvcp_rccl_attach).  Destroyed with the context.  The reference has no counterpart (single device); its own
  * recover-not-hang path is the swapchain's OutOfDate -> recreate (src/ray_tracer/vulkan.rs:
  * 355-364). */
 int rvcp_rccl_init(rvcp_ctx_t *ctx, const uint8_t id[RVCP_RCCL_ID_BYTES], uint32_t world,
@@ -438,7 +471,9 @@ int rvcp_rccl_init(rvcp_ctx_t *ctx, const uint8_t id[RVCP_RCCL_ID_BYTES], uint32
 int rvcp_rccl_set_timeout(rvcp_ctx_t *ctx, uint32_t timeout_ms);
 
 /* Use the caller's existing communicator (an ncclComm_t over ctx's device, rank `rank` of
- * `world`) instead; the caller keeps ownership. */
+ * `world`) instead; the caller keeps ownership (and is the one to abort it).  A non-blocking
+ * communicator (ncclConfig_t.blocking = 0) is supported: a gather that returns ncclInProgress
+ * is polled until it is on the stream, bounded by the deadline. */
 int rvcp_rccl_attach(rvcp_ctx_t *ctx, void *nccl_comm, uint32_t world, uint32_t rank);
 
 /* Every rank, collectively, after its rvcp_render_shard_async on the same stream: gather the
@@ -461,7 +496,15 @@ int rvcp_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, uint32_t
  * against the context's deadline (rvcp_rccl_set_timeout): when the gather has not finished by
  * then -- a peer rank never entered it -- or RCCL reports an asynchronous error, the
  * context's communicator is aborted (ncclCommAbort; its kernels exit) and RVCP_E_TIMEOUT
- * (resp. RVCP_E_HIP) is returned; rvcp_rccl_init may then build a new one.
+ * (resp. RVCP_E_HIP) is returned; rvcp_rccl_init may then build a new one.  An attached
+ * communicator is not aborted (it is the caller's) but dropped.  When the gather's stream has
+ * not drained (always the case for an attached communicator whose peer never comes), later
+ * renders on ctx no longer wait for that gather, later gathers return RVCP_E_TIMEOUT until a
+ * new communicator is initialised or attached (they then run on a fresh gather stream), and
+ * rvcp_destroy waits for the stuck gather at most min(deadline, 10 s): past that it frees the
+ * host side, leaks the context's device memory and streams (a hipFree would wait for the stuck
+ * collective: HIP synchronises the device) and returns RVCP_E_TIMEOUT, with the message in
+ * rvcp_last_error(NULL).
  * rvcp_sync_stats / rvcp_wait wait for the render only: rank 0's assembled frame (d_frame)
  * is complete after this call, not after theirs. */
 int rvcp_gather_wait(rvcp_ctx_t *ctx, float *gather_ms, float *frame_ms);

@@ -44,7 +44,9 @@ DEFAULTS = dict(device=0, integrator=0, spp=20, max_bounces=15, attenuation_stop
 
 # Error codes
 RVCP_OK, RVCP_E_INVALID, RVCP_E_HIP, RVCP_E_NO_SCENE, RVCP_E_UNSUPPORTED, RVCP_E_NOMEM, \
-    RVCP_E_INTERNAL, RVCP_E_TIMEOUT = 0, -1, -2, -3, -4, -5, -6, -7
+    RVCP_E_INTERNAL, RVCP_E_TIMEOUT, RVCP_E_BUSY = 0, -1, -2, -3, -4, -5, -6, -7, -8
+# RVCP_ABI_VERSION of include/rvcp.h this binding's struct layouts follow (load() checks it)
+ABI_VERSION = 2
 RCCL_ID_BYTES = 128
 
 EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "rvcp_create",
@@ -52,7 +54,8 @@ EXPORTED = ["rvcp_version", "rvcp_config_default", "rvcp_config_default_for", "r
             "rvcp_sync_stats", "rvcp_shard_rows", "rvcp_assemble_frame_async",
             "rvcp_upload_scene_file", "rvcp_mandelbrot", "rvcp_render_async", "rvcp_wait",
             "rvcp_rccl_unique_id", "rvcp_rccl_init", "rvcp_rccl_attach", "rvcp_gather_frame_async",
-            "rvcp_gather_wait", "rvcp_render_frames_async", "rvcp_rccl_set_timeout"]
+            "rvcp_gather_wait", "rvcp_render_frames_async", "rvcp_rccl_set_timeout",
+            "rvcp_abi_version", "rvcp_set_code_cache_dir", "rvcp_code_cache_counts"]
 
 
 # Integrator mode 2 (ray_tracer.comp ray_trace): its own #defines (ray_tracer.comp:5-13).
@@ -118,6 +121,9 @@ def load():
     L = ctypes.CDLL(LIB_PATH)
     P, u32 = ctypes.c_void_p, ctypes.c_uint32
     L.rvcp_version.restype = ctypes.c_char_p
+    L.rvcp_abi_version.restype = u32
+    L.rvcp_set_code_cache_dir.argtypes = [ctypes.c_char_p]
+    L.rvcp_code_cache_counts.argtypes = [P]
     L.rvcp_config_default.argtypes = [P]
     L.rvcp_config_default_for.argtypes = [ctypes.c_int32, P]
     L.rvcp_create.argtypes = [P, ctypes.POINTER(ctypes.c_void_p)]
@@ -147,8 +153,12 @@ def load():
                  "rvcp_assemble_frame_async", "rvcp_upload_scene_file", "rvcp_mandelbrot",
                  "rvcp_render_async", "rvcp_wait", "rvcp_rccl_unique_id", "rvcp_rccl_init",
                  "rvcp_rccl_attach", "rvcp_gather_frame_async", "rvcp_gather_wait",
-                 "rvcp_render_frames_async", "rvcp_rccl_set_timeout"):
+                 "rvcp_render_frames_async", "rvcp_rccl_set_timeout", "rvcp_set_code_cache_dir",
+                 "rvcp_code_cache_counts"):
         getattr(L, name).restype = ctypes.c_int
+    if L.rvcp_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI revision {L.rvcp_abi_version()}, this binding "
+                           f"follows {ABI_VERSION} (rebuild: __graft_entry__.build())")
     _lib = L
     return L
 
@@ -159,3 +169,20 @@ def ptr(a):
     if isinstance(a, int):
         return ctypes.c_void_p(a)
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def set_code_cache_dir(path):
+    """rvcp_set_code_cache_dir: the on-disk cache of scene-specialised code objects (None or ""
+    disables it; default $XDG_CACHE_HOME/rvcp-mi355x, else ~/.cache/rvcp-mi355x)."""
+    rc = load().rvcp_set_code_cache_dir(None if path is None else os.fsencode(path))
+    if rc != RVCP_OK:
+        raise RvcpError(rc, "rvcp_set_code_cache_dir failed")
+
+
+def code_cache_counts():
+    """rvcp_code_cache_counts: dict(loads, compiles, rejects) of the on-disk module cache."""
+    out = (ctypes.c_uint64 * 3)()
+    rc = load().rvcp_code_cache_counts(ctypes.cast(out, ctypes.c_void_p))
+    if rc != RVCP_OK:
+        raise RvcpError(rc, "rvcp_code_cache_counts failed")
+    return dict(loads=int(out[0]), compiles=int(out[1]), rejects=int(out[2]))

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -29,6 +30,7 @@
 #include "rvcp_internal.h"
 #include "rvcp_jit.h"
 #include "rvcp_scene_prep.h"
+#include "build/rvcp_build_id.h"     // kRvcpSourceHash (Makefile)
 
 using namespace rvcp;
 
@@ -142,6 +144,22 @@ struct rvcp_ctx {
     uint32_t comm_world = 0, comm_rank = 0;
     // deadline of rvcp_rccl_init and rvcp_gather_wait (rvcp_rccl_set_timeout; 0 = none)
     uint32_t comm_timeout_ms = kDefaultCommTimeoutMs;
+    // the last communicator was given up after a deadline: gathers return RVCP_E_TIMEOUT (not
+    // "no communicator") until rvcp_rccl_init / rvcp_rccl_attach provides a new one
+    bool comm_timed_out = false;
+    // the creation worker of an rvcp_rccl_init that timed out, while it is still blocked inside
+    // RCCL: a further rvcp_rccl_init on this context is refused (RVCP_E_BUSY) until it returns,
+    // so retries cannot pile up blocked threads and half-made communicators
+    std::shared_ptr<struct CommJob> init_job;
+    // detached ncclCommAbort calls of this context's communicators (abort_comm): rvcp_destroy
+    // waits for them (bounded) before it frees the buffers and streams their kernels used
+    std::vector<std::shared_ptr<std::atomic<bool>>> aborts;
+    // end events of gathers that timed out and whose stream did not drain (a collective on an
+    // attached communicator, which only its owner can abort): renders no longer wait for them,
+    // the gather stream they sit on is retired, and rvcp_destroy checks them before freeing
+    // device memory (HIP's hipFree synchronises the whole device)
+    std::vector<hipEvent_t> stuck_gathers;
+    std::vector<hipStream_t> retired_gstreams;
 
     // last launch
     bool pending = false;
@@ -319,7 +337,29 @@ static int wait_gather_done(rvcp_ctx_t *ctx);
 
 extern "C" {
 
-const char *rvcp_version(void) { return "rvcp-mi355x 0.1.0 (gfx950)"; }
+// 0.2.0: ABI revision 2 (rvcp.h RVCP_ABI_VERSION: rvcp_stats_t is 64 B)
+const char *rvcp_version(void) { return "rvcp-mi355x 0.2.0 (gfx950, ABI 2)"; }
+
+uint32_t rvcp_abi_version(void) { return RVCP_ABI_VERSION; }
+
+// Self-test / measurement hooks (not part of rvcp.h): the library's source identity (SHA-256
+// prefix of every source it is built from, "+debug" for the knob build) and the key of the
+// scene-specialised module ctx's last upload built (0: none) -- bench.py binds the committed
+// PMC summaries to both.
+const char *rvcp_internal_build_id(void)
+{
+#ifdef RVCP_DEBUG_KNOBS
+    static const std::string id = std::string(kRvcpSourceHash) + "+debug";
+    return id.c_str();
+#else
+    return kRvcpSourceHash;
+#endif
+}
+
+uint64_t rvcp_internal_module_key(const rvcp_ctx_t *ctx)
+{
+    return (ctx && ctx->jit) ? ctx->jit->key_hash : 0;
+}
 
 static int impl_config_default_for(int32_t integrator, rvcp_config_t *cfg)
 {
@@ -511,9 +551,34 @@ static int impl_destroy(rvcp_ctx_t *ctx)
     if (ctx->gather_pending && ctx->evg1 && wait_gather_done(ctx) == RVCP_OK)
         ctx->gather_pending = false;
     if (ctx->gather_pending) abort_comm(ctx);
+    // the detached aborts must have returned before their communicators' buffers and streams
+    // go; and a gather that never drained still reads this context's buffers, while any hipFree
+    // would wait for it (HIP synchronises the device): both bounded by the deadline
+    const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(
+        ctx->comm_timeout_ms ? std::min<uint32_t>(ctx->comm_timeout_ms, 10000u) : 10000u);
+    bool stuck = false;
+    for (;;) {
+        stuck = false;
+        for (const auto &a : ctx->aborts) stuck |= !a->load();
+        for (hipEvent_t e : ctx->stuck_gathers) stuck |= hipEventQuery(e) == hipErrorNotReady;
+        if (!stuck || Clock::now() >= deadline) break;
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    if (stuck) {
+        // leak the device side rather than hang: the streams, events, buffers and modules stay
+        // allocated for the life of the process (the owner of the attached communicator can
+        // still abort it); the host side is freed
+        g_create_error = "rvcp_destroy: a gather (or its communicator's abort) is still stuck "
+                         "after the deadline; the context's device memory and streams are leaked";
+        new std::shared_ptr<JitKernels>(std::move(ctx->jit));   // never unloaded
+        delete ctx;
+        return RVCP_E_TIMEOUT;
+    }
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm && ctx->comm_owned) (void)rccl_api().comm_destroy(ctx->comm);
     ctx->comm = nullptr;
+    for (hipEvent_t e : ctx->stuck_gathers) (void)hipEventDestroy(e);
+    for (hipStream_t s : ctx->retired_gstreams) (void)hipStreamDestroy(s);
     free_scene(ctx);
     (void)hipFree(ctx->d_gamma);
     (void)hipFree(ctx->d_unorm);
@@ -1326,9 +1391,34 @@ static void abort_comm(rvcp_ctx_t *ctx)
     if (ctx->comm && ctx->comm_owned) {
         const ncclComm_t c = ctx->comm;
         rccl_trace("abort: detached ncclCommAbort");
-        std::thread([c] { (void)rccl_api().comm_abort(c); }).detach();
+        auto done = std::make_shared<std::atomic<bool>>(false);
+        ctx->aborts.push_back(done);          // rvcp_destroy waits for it (bounded)
+        std::thread([c, done] {
+            (void)rccl_api().comm_abort(c);
+            done->store(true);
+        }).detach();
     }
     if (ctx->comm_owned) ctx->comm = nullptr;
+}
+
+// A gather that timed out and whose stream did not drain (an attached communicator, which this
+// library cannot abort, or an abort that has not taken effect): the context forgets the
+// communicator (the caller's stays the caller's to abort), later renders stop waiting for the
+// gather (a wait on its end event would never return), the gather stream it sits on is retired
+// (a new gather gets a fresh one), and its end event is kept for rvcp_destroy.
+static int retire_stuck_gather(rvcp_ctx_t *ctx)
+{
+    ctx->stuck_gathers.push_back(ctx->evg1);
+    ctx->evg1 = nullptr;
+    if (ctx->gather_on_gstream && ctx->gstream) {
+        ctx->retired_gstreams.push_back(ctx->gstream);
+        ctx->gstream = nullptr;
+    }
+    ctx->gather_on_gstream = false;
+    ctx->gather_pending = false;
+    ctx->comm = nullptr;
+    HIP_TRY(ctx, hipEventCreate(&ctx->evg1));
+    return RVCP_OK;
 }
 
 // Wait until a non-blocking communicator has finished its last call (ncclInProgress ->
@@ -1367,12 +1457,28 @@ struct CommJob {
     ncclComm_t comm = nullptr;
 };
 
+// Creation workers abandoned at their deadline and still blocked inside RCCL, process-wide
+// (reported in the messages: each holds a thread and a half-made communicator until RCCL
+// returns, which on RCCL 2.27.7 is never while the peer stays absent)
+static std::atomic<int> g_blocked_init_workers{0};
+
 static int impl_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, uint32_t rank)
 {
     if (!ctx) return RVCP_E_INVALID;
     if (!id || world == 0 || rank >= world || world > 4096)
         return fail(ctx, RVCP_E_INVALID, "invalid RCCL rank / world");
     if (ctx->comm) return fail(ctx, RVCP_E_INVALID, "context already has a communicator");
+    if (ctx->init_job) {
+        // the worker of this context's last timed-out creation: refuse a new one while it is
+        // still blocked inside RCCL (retries must not leak a thread each)
+        std::lock_guard<std::mutex> g(ctx->init_job->m);
+        if (!ctx->init_job->done)
+            return fail(ctx, RVCP_E_BUSY, "rvcp_rccl_init: this context's previous creation timed "
+                        "out and its worker is still blocked inside RCCL (" +
+                        std::to_string(g_blocked_init_workers.load()) + " such worker(s) in the "
+                        "process); use another context, or retry once RCCL has returned");
+    }
+    ctx->init_job.reset();
     const RcclApi &R = rccl_api();
     if (!R.ok) return fail(ctx, RVCP_E_UNSUPPORTED, R.why);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1409,6 +1515,7 @@ static int impl_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, ui
             job->result = r;
             if (keep) job->comm = comm;
             job->done = true;
+            if (job->abandoned) g_blocked_init_workers--;
         }
         job->cv.notify_all();
         if (!keep && comm) {
@@ -1427,15 +1534,21 @@ static int impl_rccl_init(rvcp_ctx_t *ctx, const uint8_t *id, uint32_t world, ui
     }
     if (!finished) {
         job->abandoned = true;
+        const int blocked = ++g_blocked_init_workers;
+        ctx->init_job = job;
+        ctx->comm_timed_out = true;
         rccl_trace("init: deadline, worker abandoned");
         return fail(ctx, RVCP_E_TIMEOUT, "ncclCommInitRankConfig: no rendezvous within " +
                     std::to_string(ctx->comm_timeout_ms) + " ms (a peer rank missing or failed); "
-                    "the half-made communicator is aborted");
+                    "the half-made communicator is aborted once RCCL returns; its creation worker "
+                    "is left blocked inside RCCL (" + std::to_string(blocked) + " in the process) "
+                    "and this context refuses another rvcp_rccl_init until it returns");
     }
     if (job->result != ncclSuccess)
         return fail(ctx, RVCP_E_HIP, std::string("ncclCommInitRankConfig: ") + R.error_string(job->result));
     ctx->comm = job->comm;
     ctx->comm_owned = true;
+    ctx->comm_timed_out = false;
     ctx->comm_world = world;
     ctx->comm_rank = rank;
     return RVCP_OK;
@@ -1457,6 +1570,7 @@ static int impl_rccl_attach(rvcp_ctx_t *ctx, void *nccl_comm, uint32_t world, ui
     if (!rccl_api().ok) return fail(ctx, RVCP_E_UNSUPPORTED, rccl_api().why);
     ctx->comm = (ncclComm_t)nccl_comm;
     ctx->comm_owned = false;
+    ctx->comm_timed_out = false;
     ctx->comm_world = world;
     ctx->comm_rank = rank;
     return RVCP_OK;
@@ -1466,6 +1580,9 @@ static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, u
                                    uint32_t height, void *d_gathered, void *d_frame, void *stream)
 {
     if (!ctx) return RVCP_E_INVALID;
+    if (!ctx->comm && ctx->comm_timed_out)
+        return fail(ctx, RVCP_E_TIMEOUT, "the communicator was given up after a gather or creation "
+                    "deadline; rvcp_rccl_init / rvcp_rccl_attach a new one first");
     if (!ctx->comm) return fail(ctx, RVCP_E_INVALID, "no communicator (rvcp_rccl_init first)");
     const bool root = ctx->comm_rank == 0;
     if (!d_shard_rgba8 || width == 0 || height == 0 || (root && (!d_gathered || !d_frame)))
@@ -1503,12 +1620,17 @@ static int impl_gather_frame_async(rvcp_ctx_t *ctx, const void *d_shard_rgba8, u
                                              (size_t)slot * width, ncclUint32, 0, ctx->comm, s);
     if (r != ncclSuccess && r != ncclInProgress)
         return fail(ctx, RVCP_E_HIP, std::string("ncclGather: ") + rccl_api().error_string(r));
-    if (r == ncclInProgress && ctx->comm_owned) {
-        // a non-blocking communicator may still be connecting to its peers (first gather):
-        // the enqueue completes once it has, bounded by the deadline
+    if (r == ncclInProgress) {
+        // a non-blocking communicator -- ours, or an attached one created with blocking = 0
+        // (torch's non-blocking communicators) -- may still be connecting to its peers (first
+        // gather): the collective is on stream s only once it has, so the assembly and evg1
+        // must not be queued before that; bounded by the deadline
         const int rc = wait_comm_ready(ctx, ctx->comm, comm_deadline(ctx), "ncclGather");
         if (rc != RVCP_OK) {
+            // ours is aborted; an attached one only its owner may abort: dropped either way
             abort_comm(ctx);
+            ctx->comm = nullptr;
+            ctx->comm_timed_out = rc == RVCP_E_TIMEOUT;
             return rc;
         }
     }
@@ -1543,16 +1665,30 @@ static int wait_gather_done(rvcp_ctx_t *ctx)
             }
         }
         if (Clock::now() >= deadline) {
+            const bool owned = ctx->comm_owned;
             abort_comm(ctx);
             // the aborted kernels exit; give the stream a bounded moment to drain so that the
             // context's buffers are no longer read when the caller frees or reuses them
-            const Clock::time_point drain = Clock::now() + std::chrono::seconds(5);
+            const Clock::time_point drain = Clock::now() + std::chrono::seconds(owned ? 5 : 0);
             while (hipEventQuery(ctx->evg1) == hipErrorNotReady && Clock::now() < drain)
                 std::this_thread::sleep_for(std::chrono::milliseconds(1));
-            if (hipEventQuery(ctx->evg1) == hipSuccess) ctx->gather_pending = false;
+            const bool drained = hipEventQuery(ctx->evg1) == hipSuccess;
+            ctx->comm_timed_out = true;
+            if (drained) {
+                ctx->gather_pending = false;
+                ctx->gather_on_gstream = false;
+                ctx->comm = nullptr;
+            } else {
+                const int rc = retire_stuck_gather(ctx);
+                if (rc != RVCP_OK) return rc;
+            }
             return fail(ctx, RVCP_E_TIMEOUT, "gather not complete within " +
                         std::to_string(ctx->comm_timeout_ms) +
-                        " ms (a peer rank missing or failed); communicator aborted");
+                        " ms (a peer rank missing or failed); " +
+                        (owned ? "communicator aborted" : "the attached communicator is dropped "
+                                 "(abort it: only its owner can)") +
+                        (drained ? "" : "; its stream has not drained: later renders do not wait "
+                                        "for it, and a new gather needs a new communicator"));
         }
         std::this_thread::sleep_for(std::chrono::microseconds(spin < 2000 ? 5 : 200));
     }

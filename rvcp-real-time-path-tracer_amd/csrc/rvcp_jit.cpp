@@ -31,8 +31,12 @@
 #include <hip/hip_runtime.h>
 
 #include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cerrno>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -66,6 +70,7 @@ struct RtcApi {
     rtc_result (*code_size)(rtc_program, size_t *) = nullptr;
     rtc_result (*code)(rtc_program, char *) = nullptr;
     rtc_result (*destroy)(rtc_program *) = nullptr;
+    rtc_result (*version)(int *, int *) = nullptr;     // optional: part of the disk-cache key
 };
 
 const RtcApi &rtc()
@@ -87,6 +92,7 @@ const RtcApi &rtc()
         api.code_size = (decltype(api.code_size))dlsym(h, "hiprtcGetCodeSize");
         api.code = (decltype(api.code))dlsym(h, "hiprtcGetCode");
         api.destroy = (decltype(api.destroy))dlsym(h, "hiprtcDestroyProgram");
+        api.version = (decltype(api.version))dlsym(h, "hiprtcVersion");
         api.ok = api.create && api.compile && api.log_size && api.log && api.code_size &&
                  api.code && api.destroy;
         if (!api.ok) api.why = "libhiprtc lacks a required symbol";
@@ -740,6 +746,8 @@ unsigned jit_scan_opts()
     return opts;
 }
 
+std::vector<std::string> jit_options(bool legacy, int legacy_waves, bool lds_scene, bool bvh);
+
 namespace {
 
 uint64_t fnv1a(const std::string &s)
@@ -762,7 +770,154 @@ std::mutex g_mu;
 std::list<CacheEntry> g_cache;            // most recently used first
 constexpr size_t kCacheEntries = 16;
 
+// ---- on-disk code-object cache (rvcp_set_code_cache_dir) ----
+// One file per module, <fnv1a(key) in hex>.rvcpco:
+//   "RVCPCO01" | u64 key bytes | u64 code bytes | u64 fnv1a(code) | u64 fnv1a(key) | key | code
+// The key is the whole input of the compile: the hipRTC version, the options, the hash and
+// length of every embedded source (kernels, headers) and the generated scan text itself, so an
+// entry is used only for exactly the module it was compiled as; a file whose header, lengths,
+// key or code checksum disagree -- or whose code the runtime refuses -- is rejected, recompiled
+// and rewritten.  Writes go to a temporary file renamed into place (readers never see half a
+// file; concurrent writers of one key write the same bytes).
+constexpr char kCoMagic[8] = {'R', 'V', 'C', 'P', 'C', 'O', '0', '1'};
+std::string g_cache_dir;                  // "" = disk cache off
+bool g_cache_dir_set = false;             // rvcp_set_code_cache_dir was called
+std::atomic<uint64_t> g_disk_loads{0}, g_disk_compiles{0}, g_disk_rejects{0};
+
+std::string default_cache_dir()
+{
+    const char *x = std::getenv("XDG_CACHE_HOME");
+    if (x && *x == '/') return std::string(x) + "/rvcp-mi355x";
+    const char *h = std::getenv("HOME");
+    if (h && *h == '/') return std::string(h) + "/.cache/rvcp-mi355x";
+    return std::string();
+}
+
+std::string cache_dir()          // with g_mu held
+{
+    if (!g_cache_dir_set) {
+        g_cache_dir = default_cache_dir();
+        g_cache_dir_set = true;
+    }
+    return g_cache_dir;
+}
+
+bool make_dirs(const std::string &dir)
+{
+    if (dir.empty()) return false;
+    for (size_t i = 1; i <= dir.size(); i++) {
+        if (i == dir.size() || dir[i] == '/') {
+            const std::string p = dir.substr(0, i);
+            if (::mkdir(p.c_str(), 0700) != 0 && errno != EEXIST) return false;
+        }
+    }
+    struct stat st;
+    return ::stat(dir.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+std::string code_key(const std::string &scan, const std::vector<std::string> &opts)
+{
+    int maj = -1, mnr = -1;
+    if (rtc().version) (void)rtc().version(&maj, &mnr);
+    std::string k = "rvcp code object\nhiprtc " + std::to_string(maj) + "." + std::to_string(mnr) + "\n";
+    for (const std::string &o : opts) k += o + "\n";
+    for (const char *src : {kJitSrcKernels, kJitSrcInternal, kJitSrcAbi, kJitSrcSqrt}) {
+        const std::string s(src);
+        k += "src " + std::to_string(s.size()) + " " + std::to_string(fnv1a(s)) + "\n";
+    }
+    return k + scan;
+}
+
+std::string hex64(uint64_t v)
+{
+    char b[17];
+    std::snprintf(b, sizeof(b), "%016llx", (unsigned long long)v);
+    return b;
+}
+
+uint64_t fnv1a_bytes(const char *p, size_t n)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; i++) {
+        h ^= (unsigned char)p[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+// The entry for `key` in `dir`: 1 = code read and verified, 0 = no entry, -1 = entry rejected
+int disk_read(const std::string &dir, const std::string &key, std::vector<char> &code)
+{
+    const std::string path = dir + "/" + hex64(fnv1a(key)) + ".rvcpco";
+    std::FILE *f = std::fopen(path.c_str(), "rb");
+    if (!f) return 0;
+    std::vector<char> buf;
+    char tmp[1 << 16];
+    size_t got;
+    while ((got = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
+    std::fclose(f);
+    uint64_t hdr[4];
+    if (buf.size() < 8 + sizeof(hdr) || std::memcmp(buf.data(), kCoMagic, 8) != 0) return -1;
+    std::memcpy(hdr, buf.data() + 8, sizeof(hdr));
+    const size_t off = 8 + sizeof(hdr);
+    if (hdr[0] != key.size() || hdr[1] == 0 || buf.size() != off + hdr[0] + hdr[1] ||
+        hdr[3] != fnv1a(key) || std::memcmp(buf.data() + off, key.data(), key.size()) != 0)
+        return -1;
+    const char *c = buf.data() + off + hdr[0];
+    if (fnv1a_bytes(c, hdr[1]) != hdr[2] || hdr[1] < 4 || std::memcmp(c, "\x7f" "ELF", 4) != 0)
+        return -1;
+    code.assign(c, c + hdr[1]);
+    return 1;
+}
+
+void disk_write(const std::string &dir, const std::string &key, const std::vector<char> &code)
+{
+    if (!make_dirs(dir)) return;
+    static std::atomic<unsigned> seq{0};
+    const std::string path = dir + "/" + hex64(fnv1a(key)) + ".rvcpco";
+    const std::string tmp = path + ".tmp." + std::to_string((long)::getpid()) + "." + std::to_string(seq++);
+    std::FILE *f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const uint64_t hdr[4] = {key.size(), code.size(), fnv1a_bytes(code.data(), code.size()), fnv1a(key)};
+    bool ok = std::fwrite(kCoMagic, 1, 8, f) == 8 && std::fwrite(hdr, 1, sizeof(hdr), f) == sizeof(hdr) &&
+              std::fwrite(key.data(), 1, key.size(), f) == key.size() &&
+              std::fwrite(code.data(), 1, code.size(), f) == code.size();
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+}
+
 }  // namespace
+
+// The module's code object: from the disk cache when it holds a verified entry for exactly this
+// compile (from_disk = true), else compiled with hipRTC and stored.  force_compile: the caller
+// found the disk entry unusable (the runtime refused it) -- count it rejected, compile, overwrite.
+// With g_mu held.
+int jit_cached_code(const std::string &scan, std::vector<char> &code, std::string &err,
+                    bool legacy, int legacy_waves, bool lds_scene, bool bvh, bool *from_disk,
+                    bool force_compile)
+{
+    *from_disk = false;
+    const std::string dir = cache_dir();
+    std::string key;
+    if (!dir.empty()) {
+        key = code_key(scan, jit_options(legacy, legacy_waves, lds_scene, bvh));
+        if (force_compile) {
+            g_disk_rejects++;
+        } else {
+            const int r = disk_read(dir, key, code);
+            if (r == 1) {
+                g_disk_loads++;
+                *from_disk = true;
+                return 0;
+            }
+            if (r < 0) g_disk_rejects++;
+        }
+    }
+    if (jit_compile_code(scan, code, err, legacy, legacy_waves, lds_scene, bvh) != 0) return -1;
+    g_disk_compiles++;
+    if (!dir.empty()) disk_write(dir, key, code);
+    return 0;
+}
 
 JitKernels::~JitKernels()
 {
@@ -773,6 +928,25 @@ JitKernels::~JitKernels()
         (void)hipModuleUnload(module);
         if (cur >= 0) (void)hipSetDevice(cur);
     }
+}
+
+// The hipRTC options of a module: the flags of the static build (Makefile), on which the
+// numeric contract depends, and the module's variant defines.
+std::vector<std::string> jit_options(bool legacy, int legacy_waves, bool lds_scene, bool bvh)
+{
+    std::vector<std::string> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17",
+                                     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+                                     "-fno-fast-math", "-fno-slp-vectorize", "-DRVCP_JIT",
+                                     "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
+    if (legacy) opts.push_back("-DRVCP_JIT_LEGACY");
+    if (bvh) opts.push_back("-DRVCP_JIT_BVH");
+#ifdef RVCP_TIMELINE
+    opts.push_back("-DRVCP_TIMELINE");      // the debug library's modules keep the per-wave timeline
+#endif
+    if (legacy && legacy_waves > 0) opts.push_back("-DRVCP_LEGACY_MIN_WAVES=" + std::to_string(legacy_waves));
+    if (legacy && lds_scene) opts.push_back("-DRVCP_LEGACY_LDS_SCENE");
+    for (const std::string &x : jit_extra_flags()) opts.push_back(x);
+    return opts;
 }
 
 int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
@@ -790,21 +964,9 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
         err = "hiprtcCreateProgram failed";
         return -1;
     }
-    // the flags of the static build (Makefile): the numeric contract depends on them
-    const std::vector<std::string> extra = jit_extra_flags();
-    std::vector<const char *> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17",
-                                      "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
-                                      "-fno-fast-math", "-fno-slp-vectorize", "-DRVCP_JIT",
-                                      "-DRVCP_SPEC_SCAN=\"rvcp_spec_scan.inc\""};
-    if (legacy) opts.push_back("-DRVCP_JIT_LEGACY");
-    if (bvh) opts.push_back("-DRVCP_JIT_BVH");
-#ifdef RVCP_TIMELINE
-    opts.push_back("-DRVCP_TIMELINE");      // the debug library's modules keep the per-wave timeline
-#endif
-    const std::string lw = "-DRVCP_LEGACY_MIN_WAVES=" + std::to_string(legacy_waves);
-    if (legacy && legacy_waves > 0) opts.push_back(lw.c_str());
-    if (legacy && lds_scene) opts.push_back("-DRVCP_LEGACY_LDS_SCENE");
-    for (const std::string &x : extra) opts.push_back(x.c_str());
+    const std::vector<std::string> opt_s = jit_options(legacy, legacy_waves, lds_scene, bvh);
+    std::vector<const char *> opts;
+    for (const std::string &x : opt_s) opts.push_back(x.c_str());
     const int rc = api.compile(prog, (int)opts.size(), opts.data());
     if (rc != 0) {
         size_t ls = 0;
@@ -853,31 +1015,49 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
             return g_cache.front().kernels;
         }
     }
+    if (hipSetDevice(device) != hipSuccess) {
+        err = "hipSetDevice failed";
+        return nullptr;
+    }
+    // the module's kernels from its code object; "" or what is missing
+    auto load = [&](JitKernels &k, const std::vector<char> &code) -> std::string {
+        if (hipModuleLoadData(&k.module, code.data()) != hipSuccess) {
+            k.module = nullptr;
+            return "hipModuleLoadData failed";
+        }
+        if (hipModuleGetFunction(&k.path5, k.module, "rvcp_spec_path_kernel5") != hipSuccess ||
+            hipModuleGetFunction(&k.path6, k.module, "rvcp_spec_path_kernel6") != hipSuccess)
+            return "specialised kernels missing from the module";
+        if (hipModuleGetFunction(&k.primary, k.module, "rvcp_spec_primary_kernel") != hipSuccess)
+            return "specialised pre-pass kernel missing from the module";
+        if (bvh && (hipModuleGetFunction(&k.bvh_path, k.module, "rvcp_spec_bvh_path_kernel") != hipSuccess ||
+                    hipModuleGetFunction(&k.bvh_primary, k.module, "rvcp_spec_bvh_primary_kernel") != hipSuccess))
+            return "specialised BVH kernels missing from the module";
+        if (legacy && hipModuleGetFunction(&k.legacy, k.module, "rvcp_spec_legacy_kernel") != hipSuccess)
+            return "specialised mode-2 kernel missing from the module";
+        return std::string();
+    };
     std::vector<char> code;
-    if (jit_compile_code(scan, code, err, legacy, legacy_waves, lds_scene, bvh) != 0) return nullptr;
+    bool from_disk = false;
+    if (jit_cached_code(scan, code, err, legacy, legacy_waves, lds_scene, bvh, &from_disk, false) != 0)
+        return nullptr;
+    const uint64_t key_hash = fnv1a(code_key(scan, jit_options(legacy, legacy_waves, lds_scene, bvh)));
     auto k = std::make_shared<JitKernels>();
     k->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&k->module, code.data()) != hipSuccess) {
-        k->module = nullptr;
-        err = "hipModuleLoadData failed";
-        return nullptr;
+    k->key_hash = key_hash;
+    std::string why = load(*k, code);
+    if (!why.empty() && from_disk) {
+        // a verified entry the runtime still refuses (another ROCm, another device): not
+        // trusted -- compiled afresh and the entry overwritten
+        k = std::make_shared<JitKernels>();
+        k->device = device;
+        k->key_hash = key_hash;
+        if (jit_cached_code(scan, code, err, legacy, legacy_waves, lds_scene, bvh, &from_disk, true) != 0)
+            return nullptr;
+        why = load(*k, code);
     }
-    if (hipModuleGetFunction(&k->path5, k->module, "rvcp_spec_path_kernel5") != hipSuccess ||
-        hipModuleGetFunction(&k->path6, k->module, "rvcp_spec_path_kernel6") != hipSuccess) {
-        err = "specialised kernels missing from the module";
-        return nullptr;
-    }
-    if (hipModuleGetFunction(&k->primary, k->module, "rvcp_spec_primary_kernel") != hipSuccess) {
-        err = "specialised pre-pass kernel missing from the module";
-        return nullptr;
-    }
-    if (bvh && (hipModuleGetFunction(&k->bvh_path, k->module, "rvcp_spec_bvh_path_kernel") != hipSuccess ||
-                hipModuleGetFunction(&k->bvh_primary, k->module, "rvcp_spec_bvh_primary_kernel") != hipSuccess)) {
-        err = "specialised BVH kernels missing from the module";
-        return nullptr;
-    }
-    if (legacy && hipModuleGetFunction(&k->legacy, k->module, "rvcp_spec_legacy_kernel") != hipSuccess) {
-        err = "specialised mode-2 kernel missing from the module";
+    if (!why.empty()) {
+        err = why;
         return nullptr;
     }
     int bpc = 0;
@@ -966,4 +1146,57 @@ extern "C" size_t rvcp_internal_jit_scan_source(const void *tri_records, uint32_
                                                 size_t cap)
 {
     return rvcp_internal_jit_scan_source_opt(tri_records, n, 0, out, cap);
+}
+
+// ---- the on-disk code-object cache's C-ABI (rvcp.h) ----
+extern "C" int rvcp_set_code_cache_dir(const char *dir)
+{
+    try {
+        std::lock_guard<std::mutex> lock(rvcp::g_mu);
+        rvcp::g_cache_dir = dir ? std::string(dir) : std::string();
+        while (rvcp::g_cache_dir.size() > 1 && rvcp::g_cache_dir.back() == '/') rvcp::g_cache_dir.pop_back();
+        rvcp::g_cache_dir_set = true;
+        return 0;
+    } catch (...) {
+        return -5;      // RVCP_E_NOMEM: the only thing that can throw here
+    }
+}
+
+extern "C" int rvcp_code_cache_counts(uint64_t out[3])
+{
+    if (!out) return -1;
+    out[0] = rvcp::g_disk_loads.load();
+    out[1] = rvcp::g_disk_compiles.load();
+    out[2] = rvcp::g_disk_rejects.load();
+    return 0;
+}
+
+// Self-test hook for the CPU suite (not part of rvcp.h): the specialised module's code object
+// for n triangle records through the on-disk cache, without a GPU (no module load).  Returns 0
+// with *from_disk and *code_bytes, or -1 with the message in err.
+extern "C" int rvcp_internal_jit_cached_code(const void *tri_records, uint32_t n, int legacy,
+                                             int *from_disk, size_t *code_bytes, char *err,
+                                             size_t err_cap)
+{
+    try {
+        std::string e;
+        std::vector<char> code;
+        const std::string scan =
+            rvcp::jit_scan_source(static_cast<const rvcp::TriRecord *>(tri_records), n);
+        bool disk = false;
+        int rc;
+        {
+            std::lock_guard<std::mutex> lock(rvcp::g_mu);
+            rc = rvcp::jit_cached_code(scan, code, e, legacy != 0, 0, false, false, &disk, false);
+        }
+        if (from_disk) *from_disk = disk ? 1 : 0;
+        if (code_bytes) *code_bytes = code.size();
+        if (err && err_cap) {
+            std::strncpy(err, e.c_str(), err_cap - 1);
+            err[err_cap - 1] = '\0';
+        }
+        return rc;
+    } catch (...) {
+        return -1;
+    }
 }

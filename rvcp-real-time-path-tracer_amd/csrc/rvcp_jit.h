@@ -23,6 +23,9 @@ struct JitKernels {
     // covering the scene's first FrameArgs::bvh_prefix faces
     hipFunction_t bvh_path = nullptr, bvh_primary = nullptr;
     int blocks_per_cu5 = 0, blocks_per_cu6 = 0, blocks_per_cu_legacy = 0, blocks_per_cu_bvh = 0;
+    // fnv1a of the module's whole compile input (hipRTC version, options, embedded sources,
+    // generated scan): the disk-cache key, and the identity bench.py binds PMC summaries to
+    uint64_t key_hash = 0;
     ~JitKernels();
 };
 
@@ -46,6 +49,12 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n, unsigned opts = 0)
 int jit_compile_code(const std::string &scan, std::vector<char> &code, std::string &err,
                      bool legacy = false, int legacy_waves = 0, bool lds_scene = false,
                      bool bvh = false);
+// jit_compile_code behind the on-disk code-object cache (rvcp_set_code_cache_dir): a verified
+// entry for exactly this compile is read (*from_disk = true), else the module is compiled and
+// stored; force_compile counts the entry rejected and recompiles it (the runtime refused it).
+int jit_cached_code(const std::string &scan, std::vector<char> &code, std::string &err,
+                    bool legacy, int legacy_waves, bool lds_scene, bool bvh, bool *from_disk,
+                    bool force_compile);
 // Compiled + loaded kernels for the scene on `device` (process-wide cache keyed by the scan
 // source and `legacy`); nullptr with err set when hipRTC is unavailable or compilation fails.
 // `sphereless`: the mode-2 kernel is built for 6 waves per SIMD.

@@ -43,9 +43,13 @@ class RayTracer:
 
     # ------------------------------------------------------------------ lifetime
     def close(self):
+        """rvcp_destroy; returns its code (RVCP_E_TIMEOUT: a gather was still stuck behind a
+        collective at the deadline and the context's device memory was leaked, rvcp.h)."""
+        rc = abi.RVCP_OK
         if getattr(self, "_ctx", None):
-            self._lib.rvcp_destroy(self._ctx)
+            rc = self._lib.rvcp_destroy(self._ctx)
             self._ctx = None
+        return rc
 
     def __del__(self):
         try:
@@ -196,6 +200,11 @@ class RayTracer:
             raise ValueError("unique_id must be 128 bytes")
         buf = (ctypes.c_uint8 * abi.RCCL_ID_BYTES).from_buffer_copy(unique_id)
         self._check(self._lib.rvcp_rccl_init(self._ctx, ctypes.cast(buf, ctypes.c_void_p), world, rank))
+
+    def rccl_attach(self, nccl_comm: int, world: int, rank: int):
+        """rvcp_rccl_attach: gather over the caller's communicator (an ncclComm_t on this
+        context's device; blocking or not); the caller keeps it and is the one to abort it."""
+        self._check(self._lib.rvcp_rccl_attach(self._ctx, ctypes.c_void_p(nccl_comm), world, rank))
 
     def rccl_set_timeout(self, timeout_ms: int):
         """rvcp_rccl_set_timeout: deadline of rccl_init / gather_wait in ms (0 = none); past it

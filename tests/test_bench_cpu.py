@@ -86,6 +86,18 @@ def test_roofline_constants():
     assert bench.REFERENCE_MSAMPLES["c2"] == pytest.approx(384 * 384 * 10 * 51 / 1e6, rel=0.01)
 
 
+def test_vs_baseline_uses_the_reference_loop_shape():
+    """vs_baseline is the reference loop shape's rate (one frame per launch,
+    interactive_ms_per_step) over the published row, not the batched pipeline's."""
+    # C2 at the round-5 loop-shape time 0.237 ms: x83, not the batched x125
+    assert bench.vs_baseline_loop_shape("c2", 1, 384 * 384 * 10, 0.237) == pytest.approx(82.7, abs=0.1)
+    assert bench.vs_baseline_loop_shape("c3", 1, 1024 * 1024 * 30, 2.81) == pytest.approx(118.6, abs=0.1)
+    # no published row (C4, mode 2), N > 1, or no interactive pass: null
+    assert bench.vs_baseline_loop_shape("c4", 1, 2048 * 2048 * 64, 22.0) is None
+    assert bench.vs_baseline_loop_shape("c3", 2, 1024 * 1024 * 30, 2.81) is None
+    assert bench.vs_baseline_loop_shape("c3", 1, 1024 * 1024 * 30, None) is None
+
+
 def test_committed_pmc_summaries_load():
     """The bench line's traffic / VALU fields come from these summaries: they exist for the
     headline C3 kernel and the C5 tiled kernel, and carry per-launch numbers."""

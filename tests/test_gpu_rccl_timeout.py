@@ -33,6 +33,16 @@ try:
     print("RESULT ok", flush=True)
 except abi.RvcpError as e:
     print("RESULT", e.code, round(time.perf_counter() - t0, 3), str(e), flush=True)
+# a second creation on this context while the first one's worker is still blocked inside RCCL
+# is refused (RVCP_E_BUSY), not started: retries cannot pile up blocked threads (VERDICT r5
+# item 5); the message counts the one blocked worker
+print("STAGE retry", flush=True)
+t0 = time.perf_counter()
+try:
+    rt.rccl_init(rvcp_amd.rccl_unique_id(), 2, 0)
+    print("RETRY ok", flush=True)
+except abi.RvcpError as e:
+    print("RETRY", e.code, round(time.perf_counter() - t0, 3), str(e), flush=True)
 # the context outlives the aborted communicator: it still renders, bit-identically
 print("STAGE render", flush=True)
 after = rt.render(40, 24, 123.0)
@@ -43,11 +53,13 @@ try:
     print("WAIT ok", flush=True)
 except abi.RvcpError as e:
     print("WAIT", e.code, flush=True)
-# and a world-1 communicator can still be made on the same context afterwards
+# and a world-1 communicator can still be made on another context meanwhile
 print("STAGE reinit", flush=True)
-rt.rccl_init(rvcp_amd.rccl_unique_id(), 1, 0)
+rt2 = rvcp_amd.RayTracer(spp=2)
+rt2.rccl_init(rvcp_amd.rccl_unique_id(), 1, 0)
 print("REINIT ok", flush=True)
 print("STAGE close", flush=True)
+rt2.close()
 rt.close()
 print("DONE", flush=True)
 '''
@@ -66,7 +78,10 @@ def _run(code, limit):
 @pytest.mark.gpu
 def test_rccl_init_without_peer_times_out():
     """rvcp_rccl_init(world = 2, rank = 0) with no rank 1 returns RVCP_E_TIMEOUT within the
-    deadline (+ a bounded abort), the process keeps its context usable and exits cleanly."""
+    deadline (+ a bounded abort); a second try on that context is refused with RVCP_E_BUSY
+    while the first worker is still blocked inside RCCL (exactly one such worker reported);
+    the process keeps its context usable, can build a communicator on another context, and
+    exits cleanly."""
     timeout_ms = 3000
     r = _run(_NO_PEER.replace("TIMEOUT_MS", str(timeout_ms)), 120)
     out = r.stdout
@@ -77,6 +92,10 @@ def test_rccl_init_without_peer_times_out():
     assert parts[1] == "-7", res[0]                     # RVCP_E_TIMEOUT
     elapsed = float(parts[2])
     assert timeout_ms / 1000.0 <= elapsed < timeout_ms / 1000.0 + 20.0, res[0]
+    retry = [l for l in out.splitlines() if l.startswith("RETRY")]
+    assert retry and retry[0].split()[1] == "-8", retry      # RVCP_E_BUSY, at once
+    assert float(retry[0].split()[2]) < 1.0, retry[0]
+    assert "(1 such worker(s) in the process)" in retry[0], retry[0]
     assert "SAME True" in out
     assert "WAIT -1" in out                             # RVCP_E_INVALID: no gather in flight
     assert "REINIT ok" in out and "DONE" in out
@@ -90,3 +109,183 @@ def test_rccl_set_timeout_validates_context():
     with rvcp_amd.RayTracer(spp=1) as rt:
         rt.rccl_set_timeout(0)                          # 0 = no deadline
         rt.rccl_set_timeout(250)
+
+
+# A communicator the caller owns, created with torch's RCCL (the copy librvcp dlopen()s too):
+# world 1 on device 0, blocking or not (ncclConfig_t of rccl.h 2.27, NCCL_CONFIG_INITIALIZER).
+_CALLER_COMM = r"""
+import ctypes, time
+import numpy as np
+import torch
+import rvcp_amd
+from rvcp_amd import abi
+torch.cuda.set_device(0)
+R = ctypes.CDLL("librccl.so.1")
+class UID(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+class Cfg(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_size_t), ("magic", ctypes.c_uint), ("version", ctypes.c_uint),
+                ("blocking", ctypes.c_int), ("cgaClusterSize", ctypes.c_int), ("minCTAs", ctypes.c_int),
+                ("maxCTAs", ctypes.c_int), ("netName", ctypes.c_char_p), ("splitShare", ctypes.c_int),
+                ("trafficClass", ctypes.c_int), ("commName", ctypes.c_char_p),
+                ("collnetEnable", ctypes.c_int), ("CTAPolicy", ctypes.c_int),
+                ("shrinkShare", ctypes.c_int), ("nvlsCTAs", ctypes.c_int)]
+R.ncclCommInitRank.argtypes = [ctypes.c_void_p, ctypes.c_int, UID, ctypes.c_int]
+R.ncclCommInitRankConfig.argtypes = [ctypes.c_void_p, ctypes.c_int, UID, ctypes.c_int, ctypes.c_void_p]
+R.ncclCommGetAsyncError.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+R.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+def make_comm(blocking):
+    uid = UID()
+    assert R.ncclGetUniqueId(ctypes.byref(uid)) == 0
+    comm = ctypes.c_void_p()
+    if blocking:
+        assert R.ncclCommInitRank(ctypes.byref(comm), 1, uid, 0) == 0
+        return comm
+    ver = ctypes.c_int()
+    assert R.ncclGetVersion(ctypes.byref(ver)) == 0
+    undef = -2147483648
+    cfg = Cfg(ctypes.sizeof(Cfg), 0xcafebeef, ver.value, 0, undef, undef, undef, None, undef,
+              undef, None, undef, undef, undef, undef)
+    r = R.ncclCommInitRankConfig(ctypes.byref(comm), 1, uid, 0, ctypes.byref(cfg))
+    assert r in (0, 7), r                                  # ncclSuccess / ncclInProgress
+    st, t0 = ctypes.c_int(7), time.perf_counter()
+    while st.value == 7 and time.perf_counter() - t0 < 30:
+        assert R.ncclCommGetAsyncError(comm, ctypes.byref(st)) == 0
+    assert st.value == 0, st.value
+    return comm
+sc = rvcp_amd.Scene.default()
+W, H = 64, 48
+push = sc.push_constant(123.0)
+dev = "cuda:0"
+shard = torch.zeros((H, W), dtype=torch.int32, device=dev)
+gat = torch.zeros((1, H, W), dtype=torch.int32, device=dev)
+frame = torch.zeros((H, W), dtype=torch.int32, device=dev)
+BODY
+"""
+
+_NONBLOCKING_BODY = r"""
+comm = make_comm(False)
+rt = rvcp_amd.RayTracer(spp=2)
+rt.upload_scene(sc)
+rt.rccl_set_timeout(20000)
+rt.rccl_attach(comm.value, 1, 0)
+for k in range(3):
+    frame.zero_()
+    rt.render_shard_async(sc.push_constant(123.0 + k), W, H, 0, 1, shard.data_ptr())
+    rt.gather_frame_async(shard.data_ptr(), W, H, gat.data_ptr(), frame.data_ptr())
+    rt.sync_stats()
+    rt.gather_wait()
+    ref = rt.render(W, H, 123.0 + k)
+    got = frame.cpu().numpy().view(np.uint8).reshape(H, W, 4)
+    print("FRAME", k, bool(np.array_equal(got, ref)), flush=True)
+print("CLOSE", rt.close(), flush=True)
+torch.cuda.synchronize()
+assert R.ncclCommDestroy(comm) == 0
+print("DONE", flush=True)
+"""
+
+
+@pytest.mark.gpu
+def test_attached_nonblocking_communicator_gathers():
+    """a caller's non-blocking communicator (ncclConfig_t.blocking = 0, as torch's
+    non-blocking process groups make) attached with rvcp_rccl_attach: a gather that RCCL
+    reports ncclInProgress is polled onto the stream before the assembly and the end event are
+    queued, so rank 0's frame is the render's, every time."""
+    r = _run(_CALLER_COMM.replace("BODY", _NONBLOCKING_BODY), 120)
+    out = r.stdout
+    assert r.returncode == 0, (r.returncode, out[-2000:], r.stderr[-3000:])
+    for k in range(3):
+        assert f"FRAME {k} True" in out, out
+    assert "CLOSE 0" in out and "DONE" in out
+
+
+_STUCK_BODY = r"""
+comm = make_comm(True)
+rt = rvcp_amd.RayTracer(spp=2)
+rt.upload_scene(sc)
+rt.rccl_set_timeout(1000)
+rt.rccl_attach(comm.value, 1, 0)
+rt.render_shard_async(push, W, H, 0, 1, shard.data_ptr())
+rt.gather_frame_async(shard.data_ptr(), W, H, gat.data_ptr(), frame.data_ptr())
+rt.sync_stats()
+rt.gather_wait()
+print("FIRST", bool(torch.equal(frame, shard)), flush=True)
+# a stall of STALL_S seconds on the caller's render stream S, behind the render: the gather
+# (on the context's gather stream, joined to S's render by an event recorded after the stall)
+# cannot start before it ends -- a collective whose peer never comes, as far as the context can
+# tell, but finite, so that the process drains it at the end
+S = torch.cuda.Stream()
+t = time.perf_counter()
+with torch.cuda.stream(S):
+    torch.cuda._sleep(10 ** 7)
+S.synchronize()
+rate = 10 ** 7 / max(time.perf_counter() - t, 1e-4)
+n = int(min(max(rate * 0.2, 10 ** 6), 10 ** 11))
+t = time.perf_counter()
+with torch.cuda.stream(S):
+    torch.cuda._sleep(n)
+S.synchronize()
+rate = n / max(time.perf_counter() - t, 1e-4)
+shard2 = torch.zeros_like(shard)
+rt.render_shard_async(push, W, H, 0, 1, shard2.data_ptr(), stream=S.cuda_stream)
+with torch.cuda.stream(S):
+    torch.cuda._sleep(int(rate * STALL_S))
+t_stall = time.perf_counter()
+rt.gather_frame_async(shard2.data_ptr(), W, H, gat.data_ptr(), frame.data_ptr())
+rt.sync_stats()                          # the render itself, before the stall: returns at once
+t0 = time.perf_counter()
+try:
+    rt.gather_wait()
+    print("WAIT ok", flush=True)
+except abi.RvcpError as e:
+    print("WAIT", e.code, round(time.perf_counter() - t0, 3), flush=True)
+    print("WAITMSG", str(e), flush=True)
+# the next render on the context's own stream does not wait for the stuck gather
+t0 = time.perf_counter()
+shard3 = torch.zeros_like(shard)
+rt.render_shard_async(push, W, H, 0, 1, shard3.data_ptr())
+rt.sync_stats()
+print("RENDER", round(time.perf_counter() - t0, 3), bool(torch.equal(shard3, shard)), flush=True)
+# a new gather is refused with RVCP_E_TIMEOUT until a new communicator replaces the dropped one
+try:
+    rt.gather_frame_async(shard3.data_ptr(), W, H, gat.data_ptr(), frame.data_ptr())
+    print("GATHER2 ok", flush=True)
+except abi.RvcpError as e:
+    print("GATHER2", e.code, flush=True)
+# destroy returns (bounded), reporting that it leaked the device side
+t0 = time.perf_counter()
+rc = rt.close()
+print("DESTROY", rc, round(time.perf_counter() - t0, 3), flush=True)
+print("DESTROYMSG", abi.load().rvcp_last_error(None).decode(), flush=True)
+print("BEFORE_STALL_END", round(time.perf_counter() - t_stall, 3), STALL_S, flush=True)
+torch.cuda.synchronize()                 # the stall ends, the stuck gather runs on the caller's comm
+assert R.ncclCommDestroy(comm) == 0
+print("DONE", flush=True)
+"""
+
+
+@pytest.mark.gpu
+def test_gather_timeout_with_undrained_stream_does_not_hang():
+    """a gather that times out on an attached communicator (which the library must
+    not abort) and whose stream does not drain: gather_wait returns RVCP_E_TIMEOUT at the
+    deadline; the next render does not wait for the stuck gather; a further gather returns
+    RVCP_E_TIMEOUT until a new communicator is attached; rvcp_destroy returns within its bound
+    (RVCP_E_TIMEOUT, device side leaked) -- all while the gather is still stuck."""
+    stall = 15
+    r = _run(_CALLER_COMM.replace("BODY", _STUCK_BODY.replace("STALL_S", str(stall))), 150)
+    out = r.stdout
+    assert r.returncode == 0, (r.returncode, out[-2000:], r.stderr[-3000:])
+    assert "FIRST True" in out
+    wait = [l for l in out.splitlines() if l.startswith("WAIT ")]
+    assert wait and wait[0].split()[1] == "-7", out             # RVCP_E_TIMEOUT
+    assert 1.0 <= float(wait[0].split()[2]) < 4.0, wait[0]
+    assert "attached communicator is dropped" in out
+    render = [l for l in out.splitlines() if l.startswith("RENDER")][0].split()
+    assert float(render[1]) < 4.0 and render[2] == "True", render
+    assert "GATHER2 -7" in out
+    destroy = [l for l in out.splitlines() if l.startswith("DESTROY ")][0].split()
+    assert destroy[1] == "-7" and float(destroy[2]) < 4.0, destroy
+    assert "leaked" in out
+    # all of the above happened while the gather was still stuck
+    assert float([l for l in out.splitlines() if l.startswith("BEFORE_STALL_END")][0].split()[1]) < stall
+    assert "DONE" in out
