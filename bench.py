@@ -205,7 +205,7 @@ def bound_profile(kind, workload_name, kernel_name, build):
     """profile_summary's record when it measured `build`, else None; and the binding record the
     line carries: {source file, its build, match}."""
     rec, src, pbuild = profile_summary(kind, workload_name, kernel_name)
-    match = None if rec is None else (pbuild == build)
+    match = None if rec is None else (pbuild is not None and pbuild == build)
     return (rec if match else None), {"source": src, "build": pbuild, "build_match": match}
 
 
@@ -641,9 +641,17 @@ def main():
     grid_waves = args.grid_waves if args.grid_waves >= 0 else (grid_auto if fif >= 3 else 0)
     cfg_kw["grid_waves_per_simd"] = grid_waves
     rts = [rvcp_amd.RayTracer(**cfg_kw) for _ in range(fif)]
+    cc0 = rvcp_amd.abi.code_cache_counts()
     t_up = time.perf_counter()
     rts[0].upload_scene(sc)              # includes the scene-specialised compile (§4.7)
     upload_s = time.perf_counter() - t_up
+    cc1 = rvcp_amd.abi.code_cache_counts()
+    # where the upload's specialised module came from: the on-disk code-object cache
+    # (rvcp_set_code_cache_dir; a verified entry of this exact compile), a hipRTC compile, or
+    # none (the generic kernels; or the process's own in-memory cache)
+    upload_module = ("disk cache" if cc1["loads"] > cc0["loads"] else
+                     "compiled" if cc1["compiles"] > cc0["compiles"] else "none")
+    build = build_identity(rts[0])
     for r in rts[1:]:
         r.upload_scene(sc)               # (the compiled module is cached per process)
     rt = rts[0]
@@ -877,8 +885,17 @@ def main():
     bytes_per_launch = units * (n_faces * 36 + n_spheres * 16)
     algo_gbs = bytes_per_launch / wall_s / 1e9
     kname = rvcp_amd.abi.KERNEL_NAMES.get(variant, "?")
-    traffic, traffic_src = load_traffic(wl["workload"], kname)
-    valu_busy, _, valu_insts, valu_src = load_valu_busy(wl["workload"], kname, want_insts=True)
+    # the committed PMC summaries count only when they measured this build (the library's
+    # sources and, for the specialised scan, the module): else their fields are null and the
+    # line says which summary is stale
+    trec, traffic_bind = bound_profile("traffic", wl["workload"], kname, build)
+    vrec, valu_bind = bound_profile("valu", wl["workload"], kname, build)
+    traffic = float(trec["bytes"]) if trec and trec.get("bytes") else None
+    traffic_src = traffic_bind["source"]
+    valu_busy = vrec.get("valu_busy") if vrec else None
+    valu_insts = vrec.get("valu_insts") if vrec else None
+    lane_util = vrec.get("lane_utilisation") if vrec else None
+    valu_src = valu_bind["source"]
     # the shader clock of THIS run: the path kernel's own per-wave s_memtime / s_memrealtime
     # stamps (rvcp_stats_t.shader_clock_ghz), averaged over the timed calls by kernel time
     clk = [(float(st["shader_clock_ghz"]), float(st["main_kernel_ms"])) for st in stats]
@@ -1004,6 +1021,7 @@ def main():
                        "scan": ("scene-specialised (hipRTC at upload, DESIGN.md §4.7)"
                                 if variant & rvcp_amd.abi.VARIANT_SPECIALIZED else "generic"),
                        "upload_s": round(upload_s, 3),
+                       "upload_module": upload_module,
                        # warm-up frames actually run: at least one full batch per context
                        "warmup_frames": warm,
                        "frames_in_flight": fif, "grid_waves_per_simd": grid_waves,
@@ -1071,6 +1089,13 @@ def main():
                          if world == 1 else None,
                          "executed_traversal_frac": round(trav_exec / max(trav, 1), 4),
                          "valu_issue_frac_pmc_guide": valu_busy,
+                         "lane_utilisation_pmc": lane_util,
+                         # the build this run executes and the summaries' own: PMC-derived
+                         # fields are null unless the summary measured this same build
+                         "profile_binding": {"build": build, "valu": valu_bind,
+                                             "traffic": traffic_bind},
+                         "stale_profile": any(b["build_match"] is False
+                                              for b in (valu_bind, traffic_bind)),
                          "valu_insts_per_frame_pmc": None if not valu_insts else round(valu_insts),
                          "shader_clock_ghz": None if clock_ghz is None else round(clock_ghz, 4),
                          "shader_clock_ghz_isolated": (round(float(np.mean(iso_clk)), 4)

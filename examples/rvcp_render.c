@@ -32,6 +32,11 @@ int main(int argc, char **argv)
     const float time = strtof(argv[5], NULL);
     const int frames = atoi(argv[6]);
     if (W == 0 || H == 0 || spp == 0 || frames < 1) return 2;
+    if (rvcp_abi_version() != RVCP_ABI_VERSION) {   /* struct layouts of another header */
+        fprintf(stderr, "librvcp ABI %u, this program was built for %u\n",
+                (unsigned)rvcp_abi_version(), (unsigned)RVCP_ABI_VERSION);
+        return 1;
+    }
 
     rvcp_config_t cfg;
     int rc = rvcp_config_default(&cfg);      /* the shader's #defines */

@@ -169,8 +169,8 @@ struct alignas(16) BvhNode {
 static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
 // at most this many triangles per BVH leaf: 2 since round 5 -- with the node-phase break
 // (rvcp_kernels.hip) the 4-triangle leaves' tests cost more than the extra node steps of 2
-// (C5 BVH 52.0 -> 47.0 ms; 1: 46.5 ms for 1.8x the nodes; profiles/r06c_ab_bvhleaf.log,
-// r06d_ab_bvhleaf2.log)
+// (C5 BVH 52.0 -> 47.0 ms; 1: 46.5 ms for 1.8x the nodes; profiles/r05zc_ab_bvhleaf.log,
+// r05zd_ab_bvhleaf2.log)
 #ifndef RVCP_BVH_LEAF_MAX
 #define RVCP_BVH_LEAF_MAX 2
 #endif

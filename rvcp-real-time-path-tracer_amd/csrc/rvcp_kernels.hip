@@ -634,7 +634,7 @@ constexpr uint32_t kBvhPoolChunk = 2;      // leaf triangles loaded together in 
 // (32: 53.02, 48: 52.42; the absolute form, at most N stepping lanes: 54.6 ms at N = 36-40,
 // 103 ms at 64 = if-if; profiles/r05u_ab_bvhnb.log, r05v_ab_bvhnb2.log, r05w_ab_bvhnb3.log);
 // with 2-triangle leaves 48 / 64 is best (46.75 ms; 40: 47.03, 52: 47.36, 56: 49.38,
-// r06f_ab_bvhtune2.log, r06g_ab_bvhtune3.log).  Leaf order does not change a nearest hit (the
+// profiles/r05zf_ab_bvhtune2.log, r05zg_ab_bvhtune3.log).  Leaf order does not change a nearest hit (the
 // order rule), so neither does the schedule.
 #ifndef RVCP_BVH_NODE_BREAK_REL
 #define RVCP_BVH_NODE_BREAK_REL 48

@@ -111,6 +111,43 @@ def test_committed_pmc_summaries_load():
     assert 0 < busy <= 1 and 0 < frac <= 1
 
 
+def test_pmc_fields_bound_to_the_build(monkeypatch):
+    """a PMC summary counts only for the build it measured (the library's
+    source identity and the specialised module's key, recorded from the PMC passes' own bench
+    lines); any other build gets null fields and build_match False."""
+    rec = {"valu_insts": 2.8e9, "valu_busy": 0.7}
+    mine = {"source": "15761ae75e2389d3", "module": "00000000deadbeef"}
+    for pbuild, want in [(dict(mine), True), (dict(mine, module="0000000000000001"), False),
+                         (dict(mine, source="0"), False), (None, False)]:
+        monkeypatch.setattr(bench, "profile_summary", lambda *a, pb=pbuild: (rec, "profiles/x.json", pb))
+        got, bind = bench.bound_profile("valu", "w", "k", mine)
+        assert bind["build_match"] is want and (got is rec) == want and bind["source"] == "profiles/x.json"
+    monkeypatch.setattr(bench, "profile_summary", lambda *a: (None, None, None))
+    got, bind = bench.bound_profile("valu", "w", "k", mine)
+    assert got is None and bind["build_match"] is None
+
+
+def test_pmc_summary_build_from_bench_logs(tmp_path):
+    """tools/pmc_valu.py / pmc_traffic.py take the build from the passes' bench lines; passes
+    that disagree (or a log without a line) give None, which bench.py treats as stale."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pmc_valu", os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "pmc_valu.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    b = {"source": "a", "module": "b"}
+    logs = []
+    for i, build in enumerate([b, b, dict(b, module="c")]):
+        p = tmp_path / f"p{i}.log"
+        p.write_text("noise\n" + json.dumps({"roofline": {"profile_binding": {"build": build}}}) + "\n")
+        logs.append(str(p))
+    assert m.build_of(logs[:2]) == b
+    assert m.build_of(logs) is None
+    empty = tmp_path / "e.log"
+    empty.write_text("no line\n")
+    assert m.build_of([str(empty)]) is None and m.build_of([]) is None
+
+
 def _negotiate_worker(rank, world, port, outdir):
     """One rank of bench.py's N>1 control flow (negotiate_gather) over gloo, with the RCCL
     calls replaced by stand-ins that fail on chosen ranks."""

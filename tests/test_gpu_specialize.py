@@ -91,6 +91,55 @@ def test_compiled_once_per_scene(cornell):
     assert times[1] < 0.5 * times[0] or times[0] < 0.05, times
 
 
+_CACHE_CHILD = r"""
+import json, sys, time
+import numpy as np
+import rvcp_amd
+rvcp_amd.abi.set_code_cache_dir(sys.argv[1])
+sc = rvcp_amd.Scene.default()
+with rvcp_amd.RayTracer(spp=2) as rt:
+    t0 = time.perf_counter()
+    rt.upload_scene(sc)
+    up = time.perf_counter() - t0
+    img = rt.render(64, 48, 123.0)
+    spec = bool(int(rt.last_stats["kernel_variant"]) & 16)
+print(json.dumps(dict(upload_s=up, spec=spec, counts=rvcp_amd.abi.code_cache_counts(),
+                      digest=int(np.frombuffer(img.tobytes(), np.uint64).sum() % (1 << 61)))))
+"""
+
+
+def test_code_cache_across_processes(tmp_path):
+    """a second process uploading the Cornell scene loads the specialised
+    module from the on-disk cache instead of compiling it (upload < 0.05 s), and renders the
+    same frame; a corrupted entry is recompiled, not trusted."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cache = tmp_path / "cc"
+
+    def child():
+        r = subprocess.run([sys.executable, "-c", _CACHE_CHILD, str(cache)], cwd=root,
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    first = child()
+    assert first["spec"] and first["counts"]["compiles"] == 1 and first["counts"]["loads"] == 0
+    second = child()
+    assert second["spec"] and second["counts"] == dict(loads=1, compiles=0, rejects=0)
+    assert second["upload_s"] < 0.05, (first["upload_s"], second["upload_s"])
+    assert second["digest"] == first["digest"]
+    (entry,) = list(cache.glob("*.rvcpco"))
+    blob = bytearray(entry.read_bytes())
+    blob[len(blob) // 2] ^= 0xFF                                   # inside the code object
+    entry.write_bytes(bytes(blob))
+    third = child()
+    assert third["counts"] == dict(loads=0, compiles=1, rejects=1), third
+    assert third["spec"] and third["digest"] == first["digest"]
+    assert child()["counts"] == dict(loads=1, compiles=0, rejects=0)   # rewritten entry
+
+
 @pytest.mark.parametrize("W,H,spp", [(1024, 1024, 5), (97, 61, 3)])
 def test_specialised_mode2_equals_generic(W, H, spp):
     """Mode 2 (ray_tracer.comp) with the specialised triangle scan equals the generic mode-2

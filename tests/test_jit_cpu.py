@@ -294,6 +294,54 @@ def test_hiprtc_compiles_specialised_module():
     assert size.value > 10000
 
 
+def test_code_object_disk_cache(tmp_path):
+    """the specialised module's code object goes through the on-disk cache
+    (rvcp_set_code_cache_dir): compiled and stored once, then read back (a second process does
+    the same: tests/test_gpu_specialize.py); a damaged, truncated or foreign entry is rejected
+    and recompiled, never used."""
+    L = rvcp_amd.abi.load()
+    fn = L.rvcp_internal_jit_cached_code
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                   ctypes.POINTER(ctypes.c_size_t), ctypes.c_char_p, ctypes.c_size_t]
+    rec = _tri_records(_cornell_positions())
+    cache = tmp_path / "cache" / "nested"
+    rvcp_amd.abi.set_code_cache_dir(str(cache))
+
+    def get():
+        disk, size = ctypes.c_int(-1), ctypes.c_size_t(0)
+        err = ctypes.create_string_buffer(4096)
+        rc = fn(rec.ctypes.data, len(rec), 0, ctypes.byref(disk), ctypes.byref(size), err, 4096)
+        if rc != 0 and b"libhiprtc not found" in err.value:
+            pytest.skip("hipRTC not installed")
+        assert rc == 0, err.value.decode()
+        return disk.value, size.value
+    try:
+        c0 = rvcp_amd.abi.code_cache_counts()
+        disk, size = get()
+        assert disk == 0 and size > 10000                         # compiled, stored
+        files = list(cache.glob("*.rvcpco"))
+        assert len(files) == 1 and not list(cache.glob("*.tmp.*"))
+        assert get() == (1, size)                                 # read back
+        blob = files[0].read_bytes()
+        for bad in (blob[:-1] + bytes([blob[-1] ^ 1]),            # code bit flipped
+                    blob[: len(blob) // 2],                       # truncated
+                    b"RVCPCO01" + blob[8:40] + b"X" + blob[41:],  # key text altered
+                    b"garbage"):
+            files[0].write_bytes(bad)
+            assert get() == (0, size)                             # rejected -> recompiled
+            assert files[0].read_bytes() == blob                  # ... and rewritten
+            assert get() == (1, size)
+        c1 = rvcp_amd.abi.code_cache_counts()
+        assert c1["rejects"] - c0["rejects"] == 4
+        assert c1["loads"] - c0["loads"] == 5 and c1["compiles"] - c0["compiles"] == 5
+        rvcp_amd.abi.set_code_cache_dir("")                       # off: compiles, stores nothing
+        files[0].unlink()
+        assert get() == (0, size) and not list(cache.glob("*.rvcpco"))
+    finally:
+        rvcp_amd.abi.set_code_cache_dir("")
+
+
 def test_hiprtc_compiles_specialised_mode2_module():
     """The mode-2 (ray_tracer.comp) kernel with the specialised triangle scan, compiled for the
     sphere room's 12 faces (RVCP_JIT_LEGACY)."""

@@ -46,6 +46,14 @@ for s in $STEPS; do
         bvh) run pytest_bvh 600 python -u -m pytest tests/test_gpu_bvh.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread -k "bvh or BVH" ;;
         benchtest) run pytest_bench 600 python -u -m pytest tests/test_gpu_bench.py -m gpu -x -v --timeout 280 --timeout-method thread ;;
         rankshare) run rank_share 300 python -u tools/rank_share.py ;;
+        # rank 0's share with bench.py's per-frame gather (world-1 RCCL
+        # communicator attached as world N), under the box's own hardware queues; c4 strong and
+        # c3 weak; and the N=8 share traced (queues of render, gather and assembly kernels)
+        ranksharegather) run rank_share_c4 400 python -u tools/rank_share.py --workload c4 --gather && run rank_share_c4_nogather 400 python -u tools/rank_share.py --workload c4 --ns 2,4,8 && run rank_share_c3 400 python -u tools/rank_share.py --workload c3 --gather ;;
+        rstrace) run rstrace 300 rocprofv3 --kernel-trace -d "$OUT/rstrace_$TAG" -o run --output-format csv -- python3 tools/rank_share.py --workload c4 --ns 8 --gather --frames 24 && python3 tools/trace_overlap.py "$OUT/rstrace_$TAG/run_kernel_trace.csv" --skip 6 >> "$OUT/${TAG}_rstrace.log" ;;
+        # the four PMC passes of the headline command, for tools/pmc_valu.py / pmc_traffic.py
+        # (--bench-log binds each summary to the build the passes ran)
+        pmcc3) run sqpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sqpmc_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 && run sqpmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d "$OUT/sqpmc2_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 && run pmcf 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 && run pmcw 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --interactive-pass 0 --frames-in-flight 1 --batch 1 ;;
         abi) run pytest_abi 300 python -u -m pytest tests/test_gpu_abi.py tests/test_gpu_specialize.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         bench) run bench_c3 600 python bench.py ;;
         benchq) run bench_c3q 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline ;;

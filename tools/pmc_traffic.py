@@ -8,6 +8,7 @@ profiles/r02_traffic_calib.json).  Writes the JSON bench.py rea
 `roofline.traffic`.
 
   python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json --workload NAME
+         [--bench-log FETCH_PASS.log WRITE_PASS.log]
 """
 import argparse
 import csv
@@ -27,6 +28,22 @@ def per_kernel(path, counter):
     return vals
 
 
+def build_of(bench_logs):
+    """The build the PMC passes measured: the `roofline.profile_binding.build` of the bench
+    line each pass printed (bench.py, rvcp_internal_build_id + the specialised module's key);
+    all passes must agree, else None (bench.py then treats the summary as stale)."""
+    builds = []
+    for path in bench_logs or []:
+        lines = [l for l in open(path) if l.startswith("{")]
+        if not lines:
+            return None
+        d = json.loads(lines[-1])
+        builds.append(d.get("roofline", {}).get("profile_binding", {}).get("build"))
+    if not builds or any(b != builds[0] for b in builds) or builds[0] is None:
+        return None
+    return builds[0]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_csv")
@@ -34,6 +51,8 @@ def main():
     ap.add_argument("out_json")
     ap.add_argument("--workload", required=True)
     ap.add_argument("--skip", type=int, default=1, help="warm-up launches to drop per kernel")
+    ap.add_argument("--bench-log", nargs="*", default=[],
+                    help="the bench.py output of each PMC pass: the build they measured")
     a = ap.parse_args()
     fetch = per_kernel(a.fetch_csv, "FETCH_SIZE")
     write = per_kernel(a.write_csv, "WRITE_SIZE")
@@ -51,6 +70,8 @@ def main():
                                 "fetch_bytes": None if fb is None else round(fb),
                                 "write_bytes": None if wb is None else round(wb),
                                 "bytes": None if fb is None or wb is None else round(fb + wb)}
+    out["build"] = build_of(a.bench_log)
+    out["bench_logs"] = list(a.bench_log)
     with open(a.out_json, "w") as fo:
         json.dump(out, fo, indent=1)
     print(json.dumps(out, indent=1))

@@ -19,6 +19,7 @@ kernel's cycles.  Writes the JSON bench.py reads into roofline.valu_busy_pmc /
 roofline.valu_issue_frac_pmc.
 
   python tools/pmc_valu.py SQ.csv GRBM.csv OUT.json --workload NAME [--simds 1024 --xcds 8]
+         [--bench-log SQ_PASS.log GRBM_PASS.log]
 """
 import argparse
 import csv
@@ -36,6 +37,22 @@ def per_kernel(path, counter):
     return vals
 
 
+def build_of(bench_logs):
+    """The build the PMC passes measured: the `roofline.profile_binding.build` of the bench
+    line each pass printed (bench.py, rvcp_internal_build_id + the specialised module's key);
+    all passes must agree, else None (bench.py then treats the summary as stale)."""
+    builds = []
+    for path in bench_logs or []:
+        lines = [l for l in open(path) if l.startswith("{")]
+        if not lines:
+            return None
+        d = json.loads(lines[-1])
+        builds.append(d.get("roofline", {}).get("profile_binding", {}).get("build"))
+    if not builds or any(b != builds[0] for b in builds) or builds[0] is None:
+        return None
+    return builds[0]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("sq_csv")
@@ -45,6 +62,8 @@ def main():
     ap.add_argument("--simds", type=int, default=1024)
     ap.add_argument("--xcds", type=int, default=8)
     ap.add_argument("--issue-peak", type=float, default=0.3888)
+    ap.add_argument("--bench-log", nargs="*", default=[],
+                    help="the bench.py output of each PMC pass: the build they measured")
     a = ap.parse_args()
     valu = per_kernel(a.sq_csv, "SQ_INSTS_VALU")
     grbm = per_kernel(a.grbm_csv, "GRBM_GUI_ACTIVE")
@@ -63,6 +82,8 @@ def main():
                              "issue_frac": round(v / (g * a.simds) / a.issue_peak, 4) if g else None}
         if thr.get(k) and act.get(k) and sum(act[k]) > 0:
             out["kernels"][k]["lane_utilisation"] = round(sum(thr[k]) / (64.0 * sum(act[k])), 4)
+    out["build"] = build_of(a.bench_log)
+    out["bench_logs"] = list(a.bench_log)
     with open(a.out_json, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
