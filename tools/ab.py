@@ -81,7 +81,9 @@ def main():
     ap.add_argument("--runner", choices=sorted(RUNNERS), default="bench")
     ap.add_argument("--passes", type=int, default=2)
     ap.add_argument("--timeout", type=int, default=200)
-    ap.add_argument("--field", default="ms_per_step", help="bench runner: the figure to compare")
+    ap.add_argument("--field", default="ms_per_step",
+                    help="bench runner: the figure to compare (several: comma-separated, the first "
+                         "one the headline of each line)")
     ap.add_argument("--cases-file", help="cases one per line (# comments), after the positional ones; "
                     "$DBG is the debug library")
     ap.add_argument("cases", nargs="*")
@@ -101,7 +103,9 @@ def main():
         if stale:
             sys.exit(f"case {label}: {', '.join(stale)} no longer exist in the kernel sources -- a "
                      "historical case file, not re-runnable (it would measure noise as an effect)")
+    fields = a.field.split(",") if a.runner == "bench" else [a.field]
     got = {label: [] for label, _, _ in cases}
+    extra = {(label, f): [] for label, _, _ in cases for f in fields[1:]}
     for p in range(1, a.passes + 1):
         for label, env, args in cases:
             cmd = ["timeout", "-k", "10", str(a.timeout)] + RUNNERS[a.runner] + args
@@ -112,13 +116,22 @@ def main():
                 if r.returncode >= 124:      # time limit / signal: stop here
                     sys.exit(r.returncode)
                 continue
-            v = measure(a.runner, r.stdout, a.field)
+            v = measure(a.runner, r.stdout, fields[0])
             got[label].append(v)
-            print(f"pass {p} {label:>24}  {v:.4f} ms", flush=True)
+            more = ""
+            for f in fields[1:]:
+                x = measure(a.runner, r.stdout, f)
+                extra[(label, f)].append(x)
+                more += f"  {f}={x:.4f}"
+            print(f"pass {p} {label:>24}  {v:.4f} ms{more}", flush=True)
     for label, vals in got.items():
         if vals:
             print(f"median {label:>24}  {statistics.median(vals):.4f} ms  (n={len(vals)}, "
                   f"min {min(vals):.4f})", flush=True)
+            for f in fields[1:]:
+                xs = extra[(label, f)]
+                print(f"median {label:>24}  {f} {statistics.median(xs):.4f}  (min {min(xs):.4f})",
+                      flush=True)
 
 
 if __name__ == "__main__":
