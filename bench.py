@@ -1064,6 +1064,9 @@ def main():
                              "kernel_ms_min": round(min(iso_ms), 4),
                              "achieved": round(flop_per_launch / iso_s / 1e12, 2),
                              "frac": round(flop_per_launch / iso_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+                             # the honest kernel fraction: only the
+                             # traversals the kernel executes (the primary hit once per pixel)
+                             "frac_executed": round(flop_exec / iso_s / 1e12 / FP32_PEAK_TFLOPS, 4),
                              "frames": len(iso_ms),
                              "grid_waves_per_simd": 0,
                              "definition": "useful FLOP / the path kernel's HIP-event time with "

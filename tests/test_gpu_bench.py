@@ -59,6 +59,16 @@ def test_bench_line(tmp_path, workload, side, spp, steps):
     assert 0 < rl["frac"] <= 1 and 0 < rl["frac_executed"] <= rl["frac"]
     pl = rl["per_launch"]
     assert pl["frames"] >= 1 and 0 < pl["frac"] <= 1
+    assert 0 < pl["frac_executed"] <= pl["frac"]
+    assert pl["frac_executed"] == pytest.approx(pl["frac"] * rl["frac_executed"] / rl["frac"], rel=2e-3)
+    # PMC-derived fields only from a summary of this very build
+    pb = rl["profile_binding"]
+    assert set(pb["build"]) == {"source", "module"} and pb["build"]["source"]
+    assert rl["stale_profile"] == any(pb[k]["build_match"] is False for k in ("valu", "traffic"))
+    if pb["valu"]["build_match"] is not True:
+        assert rl["valu_issue_frac_pmc_guide"] is None and rl["valu_insts_per_frame_pmc"] is None
+    if pb["traffic"]["build_match"] is not True:
+        assert rl["traffic"] is None
     assert pl["kernel_ms_min"] <= pl["kernel_ms"]
     # the clock is this run's (the path kernel's own stamps), not a
     # constant; no "ceiling" field that the wall clock exceeds; the reference's loop shape
