@@ -557,6 +557,12 @@ def main():
                          "vulkan.rs:213 -- each frame's push made just before its submission: "
                          "ray_tracer.rs:80-98, vulkan.rs:367-369) -> "
                          "config.interactive_ms_per_step (0 = skip)")
+    ap.add_argument("--interactive-frames-in-flight", type=int, default=0,
+                    help="the interactive pass's frames in flight (1-3; 0 = auto_pipeline's "
+                         "single-frame choice); for A/Bs")
+    ap.add_argument("--interactive-grid-waves", type=int, default=-1,
+                    help="the interactive pass's grid per frame in waves per SIMD (0 = every "
+                         "resident slot; -1 = auto_pipeline's single-frame choice); for A/Bs")
     ap.add_argument("--launch-pass", type=int, default=10,
                     help="frames (at most --steps) of the post-timing one-frame-in-flight pass "
                          "that measures the path kernel's isolated launch time "
@@ -835,7 +841,9 @@ def main():
     fif_i = grid_i = None
     if args.interactive_pass > 0 and world == 1:
         fif_i, grid_i, _ = auto_pipeline(W * H, spp, legacy, small_scene, hw_queues, args.accel, 1)
-        fif_i = min(fif_i, 3)
+        fif_i = min(args.interactive_frames_in_flight or fif_i, 3)
+        if args.interactive_grid_waves >= 0:
+            grid_i = args.interactive_grid_waves
         reuse = fif == fif_i and grid_waves == grid_i
         if reuse:
             rts_i = rts[:fif_i]

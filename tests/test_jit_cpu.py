@@ -338,6 +338,13 @@ def test_code_object_disk_cache(tmp_path):
         rvcp_amd.abi.set_code_cache_dir("")                       # off: compiles, stores nothing
         files[0].unlink()
         assert get() == (0, size) and not list(cache.glob("*.rvcpco"))
+        # a cache path that cannot be a directory (a regular file on the way): the module is
+        # still compiled, nothing is written, nothing fails
+        blocker = tmp_path / "not_a_dir"
+        blocker.write_text("x")
+        rvcp_amd.abi.set_code_cache_dir(str(blocker / "cache"))
+        assert get() == (0, size)
+        assert blocker.read_text() == "x"
     finally:
         rvcp_amd.abi.set_code_cache_dir("")
 
