@@ -109,6 +109,19 @@ def test_library_exports_every_declared_symbol():
     assert sorted(abi.EXPORTED) == declared
 
 
+def test_abi_revision_matches_header_and_binding():
+    """rvcp_stats_t grew to 64 B in revision 2; the header's RVCP_ABI_VERSION, the
+    library's rvcp_abi_version() and the Python binding's struct layouts name one revision, and
+    the version string says so (rvcp_abi_version needs no GPU)."""
+    text = open(HEADER).read()
+    m = re.search(r"#define RVCP_ABI_VERSION (\d+)", text)
+    assert m and int(m.group(1)) == abi.ABI_VERSION == 2
+    L = abi.load()
+    assert L.rvcp_abi_version() == abi.ABI_VERSION
+    assert b"ABI 2" in L.rvcp_version()
+    assert abi.STATS_DTYPE.itemsize == 64
+
+
 def test_library_links_no_oracle():
     """The product must not link or embed the CPU oracle."""
     out = subprocess.run(["nm", "-D", abi.LIB_PATH], check=True, capture_output=True, text=True).stdout
