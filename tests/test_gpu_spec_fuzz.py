@@ -96,3 +96,45 @@ def test_bvh_hybrid_fuzz():
         assert np.array_equal(b[0], g[0]), desc
         assert int(b[2]["traversals"]) == int(g[2]["traversals"]), desc
     assert engaged >= N_FUZZ // 2, f"hybrid engaged on {engaged} of {N_FUZZ} scenes"
+
+
+def _mode2_scene(sc, seed):
+    """The fuzz scene for integrator mode 2 (ray_tracer.comp, the shader north_star names):
+    its faces keep their materials with material 1 turned into a fuzzy metal, and two spheres
+    -- a dielectric and a metal -- sit between the camera and its look point, sized to the
+    room, so that every material branch of mode 2's scatter runs next to the specialised
+    triangle scan."""
+    M = rvcp_amd.scene.Material
+    mats = [sc.materials[0], M.new_metal([0.8, 0.8, 0.8], 0.25), sc.materials[2],
+            M.new_dielectric(1.5), M.new_metal([0.9, 0.6, 0.4], 0.0)]
+    pos = sc.mesh.aligned_vertices()["position"][:, :3].astype(np.float64)
+    lo, hi = pos.min(0), pos.max(0)
+    c = (lo + hi) / 2
+    r = float(np.float32(np.max(hi - lo) / 8))
+    rng = np.random.default_rng(0x3D2 + seed)
+    sph = [rvcp_amd.scene.Sphere((c + rng.uniform(-1, 1, 3) * r).astype(np.float32), r, 3),
+           rvcp_amd.scene.Sphere((c + rng.uniform(-1, 1, 3) * r).astype(np.float32),
+                                 float(np.float32(r / 2)), 4)]
+    return rvcp_amd.Scene(sc.camera, mats, sph, sc.mesh)
+
+
+@pytest.mark.parametrize("seed", range(N_FUZZ))
+def test_mode2_specialised_equals_generic_equals_oracle(seed):
+    """Mode 2 with the scene-specialised triangle scan (rvcp_spec_legacy_kernel) on every fuzz
+    scene, with spheres of every material beside it: == the generic mode-2 kernel == the CPU
+    oracle, bit for bit (ray_tracer.comp:300-393 is the scene intersection being specialised)."""
+    sc0, kw, desc = fuzz_scene(seed)
+    sc = _mode2_scene(sc0, seed)
+    kw = dict(kw, integrator=rvcp_amd.abi.INTEGRATOR_LEGACY)
+    t = 200.0 + seed
+    s = _render(sc, t, **kw)
+    g = _render(sc, t, specialize=rvcp_amd.abi.SPECIALIZE_OFF, **kw)
+    assert int(s[2]["kernel_variant"]) & SPEC, desc
+    assert not int(g[2]["kernel_variant"]) & SPEC
+    o_lin, o_rgba, o_trav = O.render(scene_arrays(sc), sc.push_constant(t),
+                                     rvcp_amd.abi.make_config(**kw), W, H)
+    o = (o_rgba, o_lin, {"traversals": o_trav})
+    assert _diff(s, g) == 0, f"mode 2: specialised != generic on {_diff(s, g)} pixels; {desc}"
+    assert _diff(s, o) == 0, f"mode 2: specialised != oracle on {_diff(s, o)} pixels; {desc}"
+    assert np.array_equal(s[0], g[0]) and np.array_equal(s[0], o_rgba), desc
+    assert int(s[2]["traversals"]) == int(g[2]["traversals"]) == int(o_trav), desc
