@@ -298,7 +298,9 @@ uint32_t rvcp_abi_version(void);
  * stored under a key that covers the generated source, the kernel source, the compile options
  * and the hipRTC version, and a later process that uploads the same scene loads it instead.
  * An entry is checked (header, key, length, checksum) before it is loaded; a damaged or
- * foreign entry is recompiled and rewritten, never trusted.  The reference has no counterpart
+ * foreign entry is recompiled and rewritten, never trusted.  The checksum detects damage, not
+ * tampering: the directory is trusted like the user's own files (as any JIT cache is), so it
+ * must not be writable by others (the library creates it 0700).  The reference has no counterpart
  * (its SPIR-V is compiled into the binary, src/ray_tracer/shader.rs:9-14).
  * dir: the directory (created if missing); NULL or "" disables the cache.  Default:
  * $XDG_CACHE_HOME/rvcp-mi355x, else $HOME/.cache/rvcp-mi355x (the only environment the product
