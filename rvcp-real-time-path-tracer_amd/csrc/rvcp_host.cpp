@@ -748,7 +748,8 @@ static int upload_one(rvcp_ctx_t *ctx, const rvcp_material_t *materials, uint32_
         !RVCP_KNOB("RVCP_NO_SPECIALIZE")) {
         ctx->jit = jit_path_kernels(ctx->device, tri.data(), n_faces, ctx->jit_err,
                                     ctx->cfg.integrator == RVCP_INTEGRATOR_LEGACY,
-                                    n_spheres == 0, n_spheres <= 64 && n_materials <= 64);
+                                    n_spheres == 0, n_spheres <= 64 && n_materials <= 64, false,
+                                    spheres, n_spheres, n_materials);
         HIP_TRY(ctx, hipSetDevice(ctx->device));
     }
     ctx->rcp_fast = scan_rcp_fast_scene(tri.data(), n_faces);

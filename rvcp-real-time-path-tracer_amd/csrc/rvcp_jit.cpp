@@ -694,6 +694,39 @@ std::string jit_scan_source(const TriRecord *tri, uint32_t n, unsigned opts)
     return out;
 }
 
+// Mode 2's spheres (RVCP_JIT_LEGACY modules): the uploaded records as an X-macro over
+// (index, center x, y, z, radius) with the floats as bit patterns, which legacy_spheres expands
+// into its unrolled sphere tests (rvcp_kernels.hip).  Empty for no spheres or more than
+// kJitMaxSpheres (the kernel then keeps its loop over the records).
+std::string jit_sphere_source(const rvcp_sphere_t *sph, uint32_t n)
+{
+    if (n == 0 || n > kJitMaxSpheres || !sph) return std::string();
+    std::string out = "// the scene's " + std::to_string(n) + " spheres (rvcp_jit.cpp jit_sphere_source)\n"
+                      "#define RVCP_SPEC_SPHERES(X)";
+    for (uint32_t i = 0; i < n; i++) {
+        out += " \\\n    X(" + std::to_string(i);
+        for (float v : {sph[i].center[0], sph[i].center[1], sph[i].center[2], sph[i].radius})
+            out += ", " + lit_text(v);
+        out += ")";
+    }
+    return out + "\n";
+}
+
+// Mode 2 with the scene in LDS (RVCP_LEGACY_LDS_SCENE): the LDS copies sized to the scene
+// (every one at least 1 entry) and the cached primary hit in LDS columns
+// (RVCP_LEGACY_LDS_PRIMARY, rvcp_kernels.hip legacy_body) -- the block's LDS then stays small
+// enough for the resident blocks its registers allow.
+std::string jit_legacy_lds_source(uint32_t n_faces, uint32_t n_spheres, uint32_t n_materials)
+{
+    auto at_least_1 = [](uint32_t v) { return std::to_string(v ? v : 1u); };
+    std::string out = "#define RVCP_LDS_FACES " + at_least_1(n_faces) + "\n#define RVCP_LDS_SPHERES " +
+                      at_least_1(n_spheres) + "\n#define RVCP_LDS_MATS " + at_least_1(n_materials) + "\n";
+#ifndef RVCP_NO_LDS_PRIMARY         // (A/B variant only, tools/build_variant.sh)
+    out += "#define RVCP_LEGACY_LDS_PRIMARY 1\n";
+#endif
+    return out;
+}
+
 // ------------------------------------------------------------------ compile + cache -----
 namespace {
 
@@ -987,7 +1020,8 @@ int jit_compile_code(const std::string &scan, std::vector<char> &code, std::stri
 
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
                                              std::string &err, bool legacy, bool sphereless,
-                                             bool lds_fits, bool bvh)
+                                             bool lds_fits, bool bvh, const rvcp_sphere_t *spheres,
+                                             uint32_t n_spheres, uint32_t n_materials)
 {
     // Mode 2 on a scene without spheres (the Cornell frame): 6 waves per SIMD measured 2.5 %
     // faster than 5, with spheres 5 % slower (profiles/r02_legacy_waves_ab.log).  With the
@@ -996,7 +1030,10 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
     // (profiles/r04d_ab_m2.log, r04e_ab_m2b.log).
     // (debug build: RVCP_JIT_LEGACY_WAVES overrides; 0 = the compiler's choice)
     const bool lds_scene = legacy && lds_fits;
-    int legacy_waves = legacy && sphereless ? 6 : lds_scene ? 5 : 0;
+#ifndef RVCP_SPHERELESS_LEGACY_WAVES   // (A/B variants only, tools/build_variant.sh)
+#define RVCP_SPHERELESS_LEGACY_WAVES 6
+#endif
+    int legacy_waves = legacy && sphereless ? RVCP_SPHERELESS_LEGACY_WAVES : lds_scene ? 5 : 0;
 #ifdef RVCP_DEBUG_KNOBS
     if (const char *e = std::getenv("RVCP_JIT_LEGACY_WAVES")) legacy_waves = std::atoi(e);
 #endif
@@ -1004,6 +1041,10 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
     for (const std::string &x : jit_extra_flags()) key_flags += " " + x;
     const std::string scan = jit_scan_source(tri, n, jit_scan_opts()) +
         (legacy ? "// +legacy " + std::to_string(legacy_waves) + (lds_scene ? " lds" : "") + "\n"
+#ifndef RVCP_NO_SPHERE_LITERALS     // (A/B variant only, tools/build_variant.sh)
+                      + jit_sphere_source(spheres, n_spheres)
+#endif
+                      + (lds_scene ? jit_legacy_lds_source(n, n_spheres, n_materials) : std::string())
                 : std::string()) +
         (key_flags.empty() ? std::string() : "// +flags" + key_flags + "\n") +
         (bvh ? "// +bvh\n" : "");
@@ -1097,15 +1138,16 @@ extern "C" int rvcp_internal_jit_scene_in_range(const void *tri_records, uint32_
 // Self-test hooks for the CPU test suite (not part of rvcp.h): generate and compile the
 // specialised module for n triangle records without a GPU (`legacy`: with the mode-2 kernel).
 // Returns 0 and the code-object size, or -1 with the message in err (err_cap bytes).
-extern "C" int rvcp_internal_jit_compile_check_mode(const void *tri_records, uint32_t n,
-                                                     int legacy, size_t *code_bytes, char *err,
-                                                     size_t err_cap)
+// (with n_spheres sphere records: a mode-2 module with the spheres as literals, as upload
+// builds it for a scene with spheres -- rvcp_internal_jit_compile_check_spheres)
+static int jit_compile_check(const void *tri_records, uint32_t n, int legacy, const void *spheres,
+                             uint32_t n_spheres, size_t *code_bytes, char *err, size_t err_cap)
 {
     try {
         std::string e;
         std::vector<char> code;
-        const std::string scan =
-            rvcp::jit_scan_source(static_cast<const rvcp::TriRecord *>(tri_records), n);
+        std::string scan = rvcp::jit_scan_source(static_cast<const rvcp::TriRecord *>(tri_records), n);
+        if (legacy) scan += rvcp::jit_sphere_source(static_cast<const rvcp_sphere_t *>(spheres), n_spheres);
         const int rc = rvcp::jit_compile_code(scan, code, e, legacy != 0);
         if (code_bytes) *code_bytes = code.size();
         if (err && err_cap) {
@@ -1116,6 +1158,21 @@ extern "C" int rvcp_internal_jit_compile_check_mode(const void *tri_records, uin
     } catch (...) {
         return -1;
     }
+}
+
+extern "C" int rvcp_internal_jit_compile_check_mode(const void *tri_records, uint32_t n,
+                                                     int legacy, size_t *code_bytes, char *err,
+                                                     size_t err_cap)
+{
+    return jit_compile_check(tri_records, n, legacy, nullptr, 0, code_bytes, err, err_cap);
+}
+
+extern "C" int rvcp_internal_jit_compile_check_spheres(const void *tri_records, uint32_t n,
+                                                        const void *spheres, uint32_t n_spheres,
+                                                        size_t *code_bytes, char *err,
+                                                        size_t err_cap)
+{
+    return jit_compile_check(tri_records, n, 1, spheres, n_spheres, code_bytes, err, err_cap);
 }
 
 extern "C" int rvcp_internal_jit_compile_check(const void *tri_records, uint32_t n,
@@ -1136,6 +1193,20 @@ extern "C" size_t rvcp_internal_jit_scan_source_opt(const void *tri_records, uin
             std::strncpy(out, s.c_str(), cap - 1);
             out[cap - 1] = '\0';
         }
+        return s.size();
+    } catch (...) {
+        return 0;
+    }
+}
+
+// Self-test hook: the sphere X-macro of a mode-2 module for n sphere records (rvcp_sphere_t);
+// the length without the terminator, written into out when it fits cap bytes.
+extern "C" size_t rvcp_internal_jit_sphere_source(const void *spheres, uint32_t n, char *out,
+                                                   size_t cap)
+{
+    try {
+        const std::string s = rvcp::jit_sphere_source(static_cast<const rvcp_sphere_t *>(spheres), n);
+        if (out && cap > s.size()) std::memcpy(out, s.c_str(), s.size() + 1);
         return s.size();
     } catch (...) {
         return 0;

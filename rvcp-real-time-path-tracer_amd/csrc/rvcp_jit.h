@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/rvcp.h"
 #include "rvcp_internal.h"
 
 namespace rvcp {
@@ -61,9 +62,17 @@ int jit_cached_code(const std::string &scan, std::vector<char> &code, std::strin
 // `lds_fits`: at most 64 spheres and 64 materials (and, as always here, 64 faces): the mode-2
 // kernel reads its hit records, spheres and materials from LDS copies.
 // `bvh`: also the BVH hybrid's kernels (RVCP_JIT_BVH; tri / n are then the prefix faces).
+// `spheres` (legacy modules): the scene's sphere records, written into the module as literals
+// (jit_sphere_source) -- the module is then valid for these spheres only, like its scan.
 std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, uint32_t n,
                                              std::string &err, bool legacy = false,
                                              bool sphereless = false, bool lds_fits = false,
-                                             bool bvh = false);
+                                             bool bvh = false, const rvcp_sphere_t *spheres = nullptr,
+                                             uint32_t n_spheres = 0, uint32_t n_materials = 64);
+// The sphere X-macro of a mode-2 module ("" for none or more than kJitMaxSpheres).
+constexpr uint32_t kJitMaxSpheres = 64;
+std::string jit_sphere_source(const rvcp_sphere_t *sph, uint32_t n);
+// The LDS sizes of a mode-2 module with the scene in LDS, and its LDS primary-hit columns.
+std::string jit_legacy_lds_source(uint32_t n_faces, uint32_t n_spheres, uint32_t n_materials);
 
 }  // namespace rvcp

@@ -2743,12 +2743,12 @@ __device__ __forceinline__ float quot_markstein(float x, float s, float y) {
     return __builtin_fmaf(__builtin_fmaf(-s, q, x), y, q);
 }
 template <bool FAST>
-__device__ __forceinline__ bool sphere_accept(const rvcp_sphere_t &S, f3 o, f3 d, float a,
+__device__ __forceinline__ bool sphere_accept(f3 ce, float radius, f3 o, f3 d, float a,
                                               float two_a, float y, float tmin, float bt,
                                               float &t_out) {
-    const f3 co = mk(o.x - S.center[0], o.y - S.center[1], o.z - S.center[2]);
+    const f3 co = mk(o.x - ce.x, o.y - ce.y, o.z - ce.z);
     const float b = 2.0f * dot(d, co);
-    const float c = dot(co, co) - S.radius * S.radius;
+    const float c = dot(co, co) - radius * radius;
     const float delta = b * b - 4.0f * a * c;
     // no lane's line meets the sphere (delta < 0 or NaN everywhere): every lane rejects it
     // below (!(delta < 0) fails, or NaN roots fail the compares), so the wave skips the
@@ -2777,10 +2777,31 @@ __device__ __forceinline__ void legacy_spheres(const FrameArgs &A, const rvcp_sp
                                                f3 ro, f3 rd, float a, float two_a, float rtmin,
                                                float &bt, int &best) {
     const float y = FAST ? rcp_ieee(two_a) : 0.0f;
+#ifdef RVCP_SPEC_SPHERES
+    // the scene-specialised module (rvcp_jit.cpp jit_sphere_source): the uploaded spheres as
+    // literals, X(index, center x, y, z, radius) in index order -- the loop unrolled, no record
+    // loads, the radius' square folded; the same operations on the same values
+    (void)A;
+    (void)sph;
+#define RVCP_SPHERE_TEST(i, cx, cy, cz, r)                                                        \
+    {                                                                                             \
+        float t;                                                                                  \
+        if (sphere_accept<FAST>(mk(cx, cy, cz), r, ro, rd, a, two_a, y, rtmin, bt, t)) {          \
+            bt = t;                                                                               \
+            best = (i);                                                                           \
+        }                                                                                         \
+    }
+    RVCP_SPEC_SPHERES(RVCP_SPHERE_TEST)
+#undef RVCP_SPHERE_TEST
+#else
     for (uint32_t i = 0; i < A.n_spheres; ++i) {
         float t;
-        if (sphere_accept<FAST>(sph[i], ro, rd, a, two_a, y, rtmin, bt, t)) { bt = t; best = (int)i; }
+        if (sphere_accept<FAST>(ld3(sph[i].center), sph[i].radius, ro, rd, a, two_a, y, rtmin, bt, t)) {
+            bt = t;
+            best = (int)i;
+        }
     }
+#endif
 }
 
 // The hit record of the nearest hit `best` (spheres first, then faces) of ray (ro, rd) at time
@@ -2832,7 +2853,7 @@ __device__ __forceinline__ void legacy_body(
     const rvcp_sphere_t *__restrict__ sph, const rvcp_material_t *__restrict__ mats,
     const float *__restrict__ unorm_t, uint32_t *__restrict__ out_rgba,
     float *__restrict__ out_lin, unsigned long long *__restrict__ counters,
-    uint8_t (*coop_tab)[kWave], StartSlot (*start_slots)[kWave])
+    uint8_t (*coop_tab)[kWave], StartSlot (*start_slots)[kWave], float *prim_lds = nullptr)
 {
     uint8_t *tab = coop_tab[threadIdx.x / kWave];
     const uint32_t lane = lane_id();
@@ -2865,9 +2886,23 @@ __device__ __forceinline__ void legacy_body(
     uint32_t pix = 0, k = 0, left = 0, trav = 0, iters = 0;
     float seed = 0.0f, ridx = 0.0f;
     f3 acc = mk(0, 0, 0), att = mk(1, 1, 1), col = mk(0, 0, 0);
+#ifdef RVCP_LEGACY_LDS_PRIMARY
+    // the cached primary hit in this lane's LDS column (prim_lds[f * kBlock], f = 0..10:
+    // position, normal, direction, material | front-face bit 31) instead of 11 VGPRs held for
+    // the whole pixel: it is written once per pixel and read once per sample
+    float *const pcol = prim_lds + threadIdx.x;
+    auto prim_put = [&](f3 p, f3 n, f3 d, uint32_t m, bool out) {
+        pcol[0 * kBlock] = p.x; pcol[1 * kBlock] = p.y; pcol[2 * kBlock] = p.z;
+        pcol[3 * kBlock] = n.x; pcol[4 * kBlock] = n.y; pcol[5 * kBlock] = n.z;
+        pcol[6 * kBlock] = d.x; pcol[7 * kBlock] = d.y; pcol[8 * kBlock] = d.z;
+        pcol[9 * kBlock] = __uint_as_float(m | (out ? 0x80000000u : 0u));
+    };
+#else
+    (void)prim_lds;
     f3 P_pos = mk(0, 0, 0), P_nrm = mk(0, 0, 0), P_dir = mk(0, 0, 1);   // cached primary hit
     uint32_t P_mat = 0;
     bool P_out = true;
+#endif
     f3 H_pos = mk(0, 0, 0), H_nrm = mk(0, 0, 0), H_dir = mk(0, 0, 1);   // hit being scattered
     uint32_t H_mat = 0;
     bool H_out = true;
@@ -2892,7 +2927,16 @@ __device__ __forceinline__ void legacy_body(
                     att = mk(1, 1, 1);
                     col = mk(0, 0, 0);
                     left = A.max_bounces - 1u;
+#ifdef RVCP_LEGACY_LDS_PRIMARY
+                    H_pos = mk(pcol[0 * kBlock], pcol[1 * kBlock], pcol[2 * kBlock]);
+                    H_nrm = mk(pcol[3 * kBlock], pcol[4 * kBlock], pcol[5 * kBlock]);
+                    H_dir = mk(pcol[6 * kBlock], pcol[7 * kBlock], pcol[8 * kBlock]);
+                    const uint32_t mo = __float_as_uint(pcol[9 * kBlock]);
+                    H_mat = mo & 0x7FFFFFFFu;
+                    H_out = (mo >> 31) != 0u;
+#else
                     H_pos = P_pos; H_nrm = P_nrm; H_dir = P_dir; H_mat = P_mat; H_out = P_out;
+#endif
                     st = L_SCATTER;
                 }
             }
@@ -3076,7 +3120,11 @@ __device__ __forceinline__ void legacy_body(
                     need_pixel = true;
                     st = L_IDLE;
                 } else {
+#ifdef RVCP_LEGACY_LDS_PRIMARY
+                    prim_put(H_pos, H_nrm, H_dir, H_mat, H_out);
+#else
                     P_pos = H_pos; P_nrm = H_nrm; P_dir = H_dir; P_mat = H_mat; P_out = H_out;
+#endif
                     left = A.max_bounces - 1u;
                 }
             }
@@ -3136,25 +3184,41 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
     // scenes of at most 64 spheres, materials and faces (rvcp_jit.cpp, lds_fits): the per-lane
     // gathers of the hit record, the spheres and the scatter's material read LDS copies
     // instead of global memory (sphere room -3.5 %, mode 2 on the C3 frame -2 %)
-    __shared__ TriRecord sh_tri[64];
-    __shared__ FaceShade sh_shade[64];
-    __shared__ rvcp_sphere_t sh_sph[64];
-    __shared__ rvcp_material_t sh_mat[64];
+    // (sized to the uploaded scene: the module's RVCP_LDS_FACES / _SPHERES / _MATS, rvcp_jit.cpp
+    // jit_legacy_source, so that the block's LDS leaves room for more resident blocks)
+#ifndef RVCP_LDS_FACES
+#define RVCP_LDS_FACES 64
+#define RVCP_LDS_SPHERES 64
+#define RVCP_LDS_MATS 64
+#endif
+    __shared__ TriRecord sh_tri[RVCP_LDS_FACES];
+    __shared__ FaceShade sh_shade[RVCP_LDS_FACES];
+    __shared__ rvcp_sphere_t sh_sph[RVCP_LDS_SPHERES];
+    __shared__ rvcp_material_t sh_mat[RVCP_LDS_MATS];
     {
         auto cp = [](float4 *dst, const float4 *src, uint32_t n) {
             for (uint32_t e = threadIdx.x; e < n; e += kBlock) dst[e] = src[e];
         };
-        const uint32_t nm = A.n_mats < 64u ? A.n_mats : 64u;
-        cp(reinterpret_cast<float4 *>(sh_tri), reinterpret_cast<const float4 *>(tri), 3u * A.n_faces);
-        cp(reinterpret_cast<float4 *>(sh_shade), reinterpret_cast<const float4 *>(shade), 4u * A.n_faces);
-        cp(reinterpret_cast<float4 *>(sh_sph), reinterpret_cast<const float4 *>(sph), 2u * A.n_spheres);
+        // (the module is built for this scene, so the counts fit; the minima only keep the
+        // copies inside the arrays)
+        const uint32_t nf = min(A.n_faces, (uint32_t)RVCP_LDS_FACES);
+        const uint32_t ns = min(A.n_spheres, (uint32_t)RVCP_LDS_SPHERES);
+        const uint32_t nm = min(A.n_mats, (uint32_t)RVCP_LDS_MATS);
+        cp(reinterpret_cast<float4 *>(sh_tri), reinterpret_cast<const float4 *>(tri), 3u * nf);
+        cp(reinterpret_cast<float4 *>(sh_shade), reinterpret_cast<const float4 *>(shade), 4u * nf);
+        cp(reinterpret_cast<float4 *>(sh_sph), reinterpret_cast<const float4 *>(sph), 2u * ns);
         cp(reinterpret_cast<float4 *>(sh_mat), reinterpret_cast<const float4 *>(mats), 2u * nm);
         __syncthreads();
     }
     // (the sphere loop's wave-uniform records read from global memory by scalar loads instead,
     // beside the LDS copies for the per-lane gathers: 0.2855 vs 0.2814 ms, profiles/r04i_ab_m2c.log)
+#ifdef RVCP_LEGACY_LDS_PRIMARY
+    __shared__ float prim_lds[10 * kBlock];
+#else
+    float *const prim_lds = nullptr;
+#endif
     legacy_body(A, sh_tri, sh_shade, sh_sph, sh_mat, unorm_t, out_rgba, out_lin, counters, coop_tab,
-                start_slots);
+                start_slots, prim_lds);
 #else
     legacy_body(A, tri, shade, sph, mats, unorm_t, out_rgba, out_lin, counters, coop_tab,
                 start_slots);

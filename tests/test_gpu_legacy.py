@@ -108,6 +108,29 @@ def test_bitexact_sphere_field(seed):
     _check(sc, _cfg(spp=3, max_bounces=6), 64, 48, time=float(seed))
 
 
+def test_bitexact_sphere_field_beyond_literals():
+    """68 spheres: more than the specialised module writes as literals (rvcp_jit.cpp
+    kJitMaxSpheres = 64), so its kernel keeps the loop over the records (and, with 68
+    materials, reads them from global memory instead of LDS copies)."""
+    sc = sphere_field(60, 4, extra_types=True)
+    assert len(sc.spheres) > 64
+    _check(sc, _cfg(spp=2, max_bounces=6), 48, 40, time=4.0)
+
+
+def test_bitexact_sphere_literal_edge_values():
+    """Sphere records the literal form must carry bit for bit: signed-zero centres, a negative
+    and a zero radius, a subnormal coordinate (rvcp_jit.cpp jit_sphere_source)."""
+    base = rvcp_amd.scene.sphere_scene()
+    sph = list(base.spheres)
+    vec3 = rvcp_amd.scene.vec3
+    sph.append(rvcp_amd.Sphere(vec3(-0.0, 0.5, -0.0), 0.5, sph[0].material_id))
+    sph.append(rvcp_amd.Sphere(vec3(0.75, 0.3, 0.5), -0.3, sph[1].material_id))
+    sph.append(rvcp_amd.Sphere(vec3(-0.75, 0.3, 1e-40), 0.0, sph[2].material_id))
+    sph.append(rvcp_amd.Sphere(vec3(-1.25, 0.35, 0.75), 0.35, sph[3].material_id))
+    sc = rvcp_amd.Scene(base.camera, base.materials, sph, base.mesh)
+    _check(sc, _cfg(spp=3, max_bounces=6), 56, 40, time=2.5)
+
+
 def test_bitexact_camera_inside_dielectric(spheres):
     """The camera inside a glass sphere: is_normal_outward = false on the first hit
     (ray_tracer.comp:316-319), refraction_ratio not inverted (:562)."""

@@ -370,6 +370,55 @@ def test_hiprtc_compiles_specialised_mode2_module():
     assert size.value > 10000
 
 
+def test_mode2_sphere_literals():
+    """Mode 2's spheres as literals (rvcp_jit.cpp jit_sphere_source): the X-macro carries every
+    sphere's center and radius bit for bit, in index order; the mode-2 module compiles with it
+    (the kernel's unrolled sphere tests, rvcp_kernels.hip legacy_spheres); none for a scene
+    without spheres or with more than 64 (the kernel keeps its loop over the records)."""
+    import re
+    L = rvcp_amd.abi.load()
+    src = L.rvcp_internal_jit_sphere_source
+    src.restype = ctypes.c_size_t
+    src.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+
+    def text(sph):
+        n = src(sph.ctypes.data if len(sph) else None, len(sph), None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        src(sph.ctypes.data if len(sph) else None, len(sph), buf, n + 1)
+        return buf.value.decode()
+    sc = rvcp_amd.scene.sphere_scene()
+    sph = np.ascontiguousarray(sc.aligned_spheres())
+    rng = np.random.default_rng(5)
+    odd = sph.copy()                     # signed zeros, subnormals, huge and negative values
+    odd["center"][:, 0] = np.array([-0.0, 1e-40, -3e38, 7.25, 0.0, -1.5, 2.0 ** -126, 1e30][:len(odd)], np.float32)
+    odd["radius"] = rng.standard_normal(len(odd)).astype(np.float32)
+    for recs in (sph, odd):
+        t = text(recs)
+        rows = re.findall(r"X\((\d+), ([^X]*)\)", t)
+        assert [int(i) for i, _ in rows] == list(range(len(recs)))
+        for (_, args), rec in zip(rows, recs):
+            bits = [int(b, 16) for b in re.findall(r"RVCP_F32\(0x([0-9a-f]{8})u\)", args)]
+            want = np.concatenate([rec["center"], [rec["radius"]]]).astype(np.float32).view(np.uint32)
+            assert bits == want.tolist()
+    assert text(sph[:0]) == ""
+    big = np.zeros(65, dtype=sph.dtype)
+    assert text(big) == "" and text(big[:64]).count("X(") == 64
+    fn = L.rvcp_internal_jit_compile_check_spheres
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                   ctypes.POINTER(ctypes.c_size_t), ctypes.c_char_p, ctypes.c_size_t]
+    verts = sc.mesh.aligned_vertices()["position"][:, :3]
+    faces = sc.mesh.aligned_faces()["vertices"]
+    rec = _tri_records(verts[faces].astype(np.float32))
+    size = ctypes.c_size_t(0)
+    err = ctypes.create_string_buffer(4096)
+    rc = fn(rec.ctypes.data, len(rec), sph.ctypes.data, len(sph), ctypes.byref(size), err, 4096)
+    if rc != 0 and b"libhiprtc not found" in err.value:
+        pytest.skip("hipRTC not installed")
+    assert rc == 0, err.value.decode()
+    assert size.value > 10000
+
+
 def _in_range(rec):
     L = rvcp_amd.abi.load()
     fn = L.rvcp_internal_jit_scene_in_range

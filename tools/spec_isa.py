@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres"])
     ap.add_argument("--legacy", action="store_true", help="the mode-2 module (RVCP_JIT_LEGACY)")
     ap.add_argument("--opts", type=int, default=0, help="generator options (rvcp_jit.h kScan*)")
+    ap.add_argument("--no-sphere-literals", action="store_true",
+                    help="--legacy: the module without the spheres as literals (the record loop)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     sc = rvcp_amd.Scene.default() if a.scene == "cornell" else rvcp_amd.scene.sphere_scene()
@@ -40,9 +42,19 @@ def main():
     n = fn(rec.ctypes.data, len(rec), a.opts, None, 0)
     buf = ctypes.create_string_buffer(n + 1)
     fn(rec.ctypes.data, len(rec), a.opts, buf, n + 1)
+    text = buf.value.decode()
+    if a.legacy and not a.no_sphere_literals:      # the mode-2 module's sphere literals
+        sph = np.ascontiguousarray(sc.aligned_spheres())
+        fs = L.rvcp_internal_jit_sphere_source
+        fs.restype = ctypes.c_size_t
+        fs.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+        m = fs(sph.ctypes.data, len(sph), None, 0)
+        sb = ctypes.create_string_buffer(m + 1)
+        fs(sph.ctypes.data, len(sph), sb, m + 1)
+        text += sb.value.decode()
     inc = os.path.join(a.out, "spec_scan.inc")
     with open(inc, "w") as f:
-        f.write(buf.value.decode())
+        f.write(text)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
            "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-fast-math", "-fno-slp-vectorize",
            "-DRVCP_JIT", f'-DRVCP_SPEC_SCAN="{inc}"', "--cuda-device-only", "-S",
