@@ -151,7 +151,11 @@ def profile_summary(kind, workload_name, kernel_name):
     relative to the repo or None, the build it measured -- {"source", "module"} from the PMC
     pass's own bench line, tools/pmc_*.py --bench-log -- or None for a summary without one)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{kind}_{workload_name}.json")))
+    # profiles/ holds this round's summaries, profiles/history/ the earlier rounds'; the tag
+    # (r01 ... r06...) sorts by round, so the newest is the last by file name
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{kind}_{workload_name}.json")) +
+                   glob.glob(os.path.join(ROOT, "profiles", "history", f"*_{kind}_{workload_name}.json")),
+                   key=os.path.basename)
     if not files:
         return None, None, None
     with open(files[-1]) as f:
@@ -371,7 +375,7 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
     (rvcp.h), so launch f waits, at its enqueue, for the one its context ran fif launches
     earlier.  A pixel is a serial chain of SPP samples: a frame of P surface pixels on L
     resident lanes ends in a tail once P/L is small (C3: ~2.6 pixels per lane, the N=8 share of
-    C4: ~1.3).  Two remedies, measured (profiles/r03zt_batch_sweep.log, r03zu_batch_sweep2.log,
+    C4: ~1.3).  Two remedies, measured (profiles/history/r03zt_batch_sweep.log, r03zu_batch_sweep2.log,
     r03zp_grid_bench_ab.log): a batch of frames in one path kernel, whose lanes take frame k+1's
     pixels while frame k's last chains finish (games101 pre-pass schedules), and else a smaller
     grid per frame with a third frame beside it, whose waves start in the tail:
@@ -379,7 +383,7 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
         below 4 Msamples: batches of about 3 Mpixel, 4 Mpixel for frames of 1 Mpixel and more
         (at most 32 frames -- 16 before round 4, C2 0.1652 -> 0.1606 / 0.1596 ms with 20 / 25,
         r04c2b2_ab_c2batch2.log -- and at most a quarter of the timed steps), 2 in flight.  Round 4
-        (profiles/r04b20b_ab_b20b.log, r04shb_ab_share_b.log, r04c5b_ab_c5b.log): C3 2.910 ->
+        (profiles/history/r04b20b_ab_b20b.log, r04shb_ab_share_b.log, r04c5b_ab_c5b.log): C3 2.910 ->
         2.871 ms at 20 frames and 2.819 -> 2.799 at 60 with 4 frames instead of 3, the N=4
         share 5.990 -> 5.961 ms, C5 with the BVH 70.32 -> 69.21 ms; the N=8 share keeps 6
         (3.020 vs 3.034 ms with 8).  Batches of 3 against 3 single frames in flight on
@@ -387,7 +391,7 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
         0.232 -> 0.208 ms (batches of 2: 3.24 / 3.56 / 0.226); deeper batches for smaller
         launches (r03zx_batch_sweep3.log): the N=8 share 3.42 / 3.37 / 3.33 ms with 3 / 4 / 6
         frames, C2 0.195 / 0.173 / 0.162 / 0.158 ms with 3 / 6 / 10 / 16; C5 with the BVH
-        97.6 -> 92.0 ms with 3 (profiles/r03zw_bvh_batch_ab.log); and 2 for larger frames
+        97.6 -> 92.0 ms with 3 (profiles/history/r03zw_bvh_batch_ab.log); and 2 for larger frames
         (r03zze_batch_sweep4.log): the N=2 share of C4 13.47 -> 13.29-13.36 ms, the whole C4
         frame 26.28-26.30 -> 26.13-26.15 ms;
       - runs with too few steps for a batch (fewer than 8): frames up to 1.5 Mpixel as mode 2
@@ -395,14 +399,14 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
       - mode 2 (no pre-pass), up to 1.5 Mpixel and at least 16 Msamples per frame: batches of
         up to 8 frames (at most a quarter of the timed steps), 2 in flight, full grid -- round 4,
         mode 2 on the C3 frame 1.667 -> 1.595 ms at 40 frames, 1.710 -> 1.633 ms at 20 with 5
-        (profiles/r04m2p2_ab_m2pipe2.log);
+        (profiles/history/r04m2p2_ab_m2pipe2.log);
       - other mode-2 frames up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD -- mode 2 on the
         C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms (round 4: batches of 4 / 8 for
         the sphere room 0.2654 / 0.2621 vs 0.2544 ms, r04m2p_ab_m2pipe.log);
       - larger mode-2 frames and meshes: full grid, one frame per launch, 2 in flight (3 in
         mode 2: one kernel per frame, no pre-pass);
       - other small frames (below 4 Msamples): 4 in flight (C2 0.59/0.32/0.27/0.33 ms for
-        1/2/3/4 in flight, profiles/r02_fif_sweep.log).
+        1/2/3/4 in flight, profiles/history/r02_fif_sweep.log).
     Contexts beyond the hardware queues minus one contend for queues."""
     if not legacy and (small_scene or accel == "bvh"):
         # about 3 Mpixel per launch (4 for frames of 1 Mpixel and more) and at least 2 frames,
@@ -521,7 +525,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     # 60 frames by default: the pipeline's fill and drain (the last launch's tail, which no
     # later frame overlaps) spread over 60 frames instead of 20 -- C3 2.848 / 2.775 / 2.750 ms
-    # per frame at 20 / 40 / 60 (profiles/r05zt_ab_steps.log); the run still takes well under
+    # per frame at 20 / 40 / 60 (profiles/history/r05zt_ab_steps.log); the run still takes well under
     # a second of GPU time
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=3)
@@ -629,12 +633,12 @@ def main():
     # idle -- the per-image fences of the reference's swapchain loop (vulkan.rs:367-369).  A
     # context holds one frame at a time (rvcp.h), so frame f waits, at its enqueue, for the
     # frame its context rendered fif steps earlier.
-    # (measured, profiles/r02_fif_sweep.log: C3 1/2/3/4 in flight 4.35/3.83/3.83/3.95 ms,
+    # (measured, profiles/history/r02_fif_sweep.log: C3 1/2/3/4 in flight 4.35/3.83/3.83/3.95 ms,
     # C2 0.59/0.32/0.27/0.33 ms -- a small frame is mostly tail, so it gains from a third)
     # (mode 2 -- one kernel per frame, no pre-pass -- gains from a third frame at every size:
-    # C3 frame 2.84/2.40/2.29/2.46 ms for 1/2/3/4 in flight, profiles/r02_m2_fif_sweep.log)
+    # C3 frame 2.84/2.40/2.29/2.46 ms for 1/2/3/4 in flight, profiles/history/r02_m2_fif_sweep.log)
     # (small frames, 8 hardware queues: C2 4 in flight 0.269 ms vs 3 in flight 0.284 ms,
-    # profiles/r02_hwq_fif_sweep.log; C3 2 and 3 equal)
+    # profiles/history/r02_hwq_fif_sweep.log; C3 2 and 3 equal)
     small_scene = args.accel == "none" and not wl["extra_tris"]
     # from the largest shard's size, so that every rank picks the same pipeline: the contexts'
     # communicators must see the ranks' gathers in the same order
@@ -851,7 +855,7 @@ def main():
             # the timed contexts are not used again at world 1: freed first, so that the new
             # ones get hardware queues of their own (GPU_MAX_HW_QUEUES is 4; contexts sharing a
             # queue run their frames one after another: C3 3.66 vs 2.91 ms per frame,
-            # profiles/r05zn_ovli.log; 3 in flight on 3 waves per SIMD: 2.82 ms,
+            # profiles/history/r05zn_ovli.log; 3 in flight on 3 waves per SIMD: 2.82 ms,
             # r05zzj_ab_c3interactive.log)
             for r in rts:
                 r.close()

@@ -1447,7 +1447,7 @@ static int wait_comm_ready(rvcp_ctx_t *ctx, ncclComm_t comm, Clock::time_point d
 // and the poll of ncclCommGetAsyncError until the rendezvous completes.  The caller waits for
 // the worker with the deadline, so rvcp_rccl_init returns in time whatever RCCL does inside
 // (on this image's RCCL 2.27.7 the "non-blocking" ncclCommInitRankConfig itself does not return
-// while a peer is absent: profiles/r05g_rccl_diag.log, tools/rccl_timeout_diag.py); a worker left
+// while a peer is absent: profiles/history/r05g_rccl_diag.log, tools/rccl_timeout_diag.py); a worker left
 // behind aborts its half-made communicator if it ever gets control back (detached: the process
 // never waits for it, and exits cleanly, tests/test_gpu_rccl_timeout.py).
 struct CommJob {

@@ -66,11 +66,11 @@ constexpr int variant_block(int v) { return v == kTiledPoolVariant ? kTiledPoolW
 constexpr uint64_t kWideMinSamples = 8ull << 20;   // auto: variant 6 from 8 Msamples per frame
 // auto, scene-specialised scan: its 6-wave build (variant 6) from 256 Msamples per frame -- C4's
 // 2048^2 SPP=64 frame 23.39 -> 23.00 ms, while C3 (31 M) is 0.3 % and C2 6 % slower at 6 waves
-// (profiles/r04z_ab_waves6.log)
+// (profiles/history/r04z_ab_waves6.log)
 // A batch's pre-passes run as one launch (one frame per grid row) for frames up to this many
 // pixels, whose per-frame pre-pass is too small to fill the GPU (C2: 0.1666 -> 0.1645 ms per
 // frame); larger frames keep one launch per frame (C3 at 60 frames: 2.810 vs 2.827 ms,
-// profiles/r04pb_ab_prebatch.log).
+// profiles/history/r04pb_ab_prebatch.log).
 constexpr uint32_t kPrepassBatchMaxPixels = 512u * 1024u;
 constexpr uint64_t kSpecWideMinSamples = 256ull << 20;
 constexpr int kOccupancyBvh = 100;          // rvcp_games101_occupancy code of the BVH kernel
@@ -169,7 +169,7 @@ struct alignas(16) BvhNode {
 static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
 // at most this many triangles per BVH leaf: 2 since round 5 -- with the node-phase break
 // (rvcp_kernels.hip) the 4-triangle leaves' tests cost more than the extra node steps of 2
-// (C5 BVH 52.0 -> 47.0 ms; 1: 46.5 ms for 1.8x the nodes; profiles/r05zc_ab_bvhleaf.log,
+// (C5 BVH 52.0 -> 47.0 ms; 1: 46.5 ms for 1.8x the nodes; profiles/history/r05zc_ab_bvhleaf.log,
 // r05zd_ab_bvhleaf2.log)
 #ifndef RVCP_BVH_LEAF_MAX
 #define RVCP_BVH_LEAF_MAX 2

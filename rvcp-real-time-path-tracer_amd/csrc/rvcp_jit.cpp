@@ -1024,10 +1024,10 @@ std::shared_ptr<JitKernels> jit_path_kernels(int device, const TriRecord *tri, u
                                              uint32_t n_spheres, uint32_t n_materials)
 {
     // Mode 2 on a scene without spheres (the Cornell frame): 6 waves per SIMD measured 2.5 %
-    // faster than 5, with spheres 5 % slower (profiles/r02_legacy_waves_ab.log).  With the
+    // faster than 5, with spheres 5 % slower (profiles/history/r02_legacy_waves_ab.log).  With the
     // scene in LDS (lds_fits): the sphere room 0.288 -> 0.278 ms at 5 waves (4 and 6: 0.305,
     // 0.308; 5 waves without LDS 0.290), the Cornell frame 1.867 -> 1.831 ms at 6
-    // (profiles/r04d_ab_m2.log, r04e_ab_m2b.log).
+    // (profiles/history/r04d_ab_m2.log, r04e_ab_m2b.log).
     // (debug build: RVCP_JIT_LEGACY_WAVES overrides; 0 = the compiler's choice)
     const bool lds_scene = legacy && lds_fits;
 #ifndef RVCP_SPHERELESS_LEGACY_WAVES   // (A/B variants only, tools/build_variant.sh)

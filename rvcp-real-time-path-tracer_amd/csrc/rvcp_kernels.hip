@@ -615,7 +615,7 @@ __device__ __forceinline__ void bvh4_step(const Bvh4QNode *__restrict__ qn, lds_
 // owners, tab[128]), its (t, face) is left in res[2 owner + (path ray)] and read back by the
 // owner.  Same traversal per ray, so the same nearest hits.
 // (inlined into the path kernel with two-triangle leaf loads: 112 VGPRs without spills, C5
-// BVH 138 -> 97.5 ms per frame, profiles/r03zj_bvh_pool_ab.log, r03zk_bvh_pool_ab.log)
+// BVH 138 -> 97.5 ms per frame, profiles/history/r03zj_bvh_pool_ab.log, r03zk_bvh_pool_ab.log)
 //
 // Carried traversals: once every new ray is taken and at most kBvhCarryMax lanes still hold an
 // unfinished one, the pool may stop and let the wave go on with its next iteration; those lanes
@@ -632,9 +632,9 @@ constexpr uint32_t kBvhPoolChunk = 2;      // leaf triangles loaded together in 
 // parked leaf: the parked lanes test their leaves instead of idling behind the few still
 // descending.  C5 with the BVH 69.16 -> 52.06 ms per frame at 40 / 64 with 4-triangle leaves
 // (32: 53.02, 48: 52.42; the absolute form, at most N stepping lanes: 54.6 ms at N = 36-40,
-// 103 ms at 64 = if-if; profiles/r05u_ab_bvhnb.log, r05v_ab_bvhnb2.log, r05w_ab_bvhnb3.log);
+// 103 ms at 64 = if-if; profiles/history/r05u_ab_bvhnb.log, r05v_ab_bvhnb2.log, r05w_ab_bvhnb3.log);
 // with 2-triangle leaves 48 / 64 is best (46.75 ms; 40: 47.03, 52: 47.36, 56: 49.38,
-// profiles/r05zf_ab_bvhtune2.log, r05zg_ab_bvhtune3.log).  Leaf order does not change a nearest hit (the
+// profiles/history/r05zf_ab_bvhtune2.log, r05zg_ab_bvhtune3.log).  Leaf order does not change a nearest hit (the
 // order rule), so neither does the schedule.
 #ifndef RVCP_BVH_NODE_BREAK_REL
 #define RVCP_BVH_NODE_BREAK_REL 48
@@ -2840,7 +2840,7 @@ __device__ __forceinline__ void legacy_hit(const FrameArgs &A, const TriRecord *
 
 // kLegacyDefer: the most lanes left ending a sample that sit out one trace (below).  16
 // measured best: sphere room 0.367 -> 0.345 ms, mode 2 on the C3 frame 2.237 -> 2.156 ms per
-// frame (profiles/r03v_m2_defer_sweep.log; 8, 24, 32, 40 and 64 less good).
+// frame (profiles/history/r03v_m2_defer_sweep.log; 8, 24, 32, 40 and 64 less good).
 #ifndef RVCP_LEGACY_DEFER
 #define RVCP_LEGACY_DEFER 16
 #endif
@@ -3211,7 +3211,7 @@ extern "C" __global__ __launch_bounds__(kBlock, RVCP_LEGACY_MIN_WAVES) void rvcp
         __syncthreads();
     }
     // (the sphere loop's wave-uniform records read from global memory by scalar loads instead,
-    // beside the LDS copies for the per-lane gathers: 0.2855 vs 0.2814 ms, profiles/r04i_ab_m2c.log)
+    // beside the LDS copies for the per-lane gathers: 0.2855 vs 0.2814 ms, profiles/history/r04i_ab_m2c.log)
 #ifdef RVCP_LEGACY_LDS_PRIMARY
     __shared__ float prim_lds[10 * kBlock];
 #else
@@ -3288,7 +3288,7 @@ extern "C" __global__ __launch_bounds__(kBlock, kPathMinWaves) void rvcp_spec_pa
     // into LDS once per workgroup, so the hit record's per-lane gathers and the tail
     // partition's triangle reads are LDS reads: a small frame's serial chain waits on them
     // every iteration (C2 one frame alone 0.492 -> 0.485 ms, its path kernel 0.470 -> 0.459;
-    // C3 unchanged, profiles/r04g_ab_c2lds*.log).  31.5 KB per workgroup: 5 per CU still fit.
+    // C3 unchanged, profiles/history/r04g_ab_c2lds*.log).  31.5 KB per workgroup: 5 per CU still fit.
     __shared__ TriRecord sh_tri[kJitMaxFaces];
     __shared__ FaceShade sh_shade[kJitMaxFaces];
     static_assert(5 * (sizeof(tail_tab) + sizeof(compact_lds) + sizeof(state_lds) + sizeof(sh_tri) +

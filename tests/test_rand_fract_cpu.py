@@ -2,7 +2,7 @@
 form: the C check (tests/rand_fract_check.c, linked with the CPU oracle's software sin) runs all
 2.1e8 floats y in [1, 2^25] and finds no x = sin(y) * 43758.5453 for which x - floor(x) rounds
 to 1.0, the only input where v_fract_f32 differs.  (The GPU side of the same check, with the
-kernel's own sin and the instruction itself: tools/sqrt_check.hip, profiles/r04c_sqrt_check.log.)"""
+kernel's own sin and the instruction itself: tools/sqrt_check.hip, profiles/history/r04c_sqrt_check.log.)"""
 import os
 import subprocess
 

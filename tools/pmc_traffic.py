@@ -4,7 +4,7 @@ WRITE_SIZE cannot share a pass on gfx950), corrected as MI355X_MICROARCH.md § H
 FETCH_SIZE / WRITE_SIZE are KiB; on gfx950 FETCH_SIZE counts half the bytes of wide reads, so
 it is doubled.  The factor is checked here against kernels with known byte counts
 (tools/traffic_calib.hip: coalesced reads count 0.5x at 4/16/48-B widths, coalesced writes 1x;
-profiles/r02_traffic_calib.json).  Writes the JSON bench.py reads for
+profiles/history/r02_traffic_calib.json).  Writes the JSON bench.py reads for
 `roofline.traffic`.
 
   python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json --workload NAME

@@ -7,7 +7,7 @@
   issue_frac = (SQ_INSTS_VALU / (cycles x SIMDs)) / 0.3888, the wave-instructions per SIMD
               per GRBM clock the chip sustains on independent v_fma_f32 streams with every SIMD
               full, measured in the same clock (tools/valu_rate.hip under the same PMC pass,
-              profiles/r02_valu_rate_pmc.txt): how close the kernel is to the
+              profiles/history/r02_valu_rate_pmc.txt): how close the kernel is to the
               VALU issue rate actually reachable
 
   lane_utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU), when the second pass
