@@ -2759,6 +2759,25 @@ __device__ __forceinline__ bool sphere_accept(f3 ce, float radius, f3 o, f3 d, f
     // takes the IEEE sequence -- not every wave in which some lane misses the sphere
     float sq = sqrt_fast_core(delta);
     if (__builtin_expect((delta >= 0.0f) & !sqrt_fast_ok(delta), 0)) sq = __builtin_sqrtf(delta);
+#ifndef RVCP_SPHERE_SWAP_FORM     // (A/B only: the swap form below for the FAST roots too)
+    if (FAST) {
+        // The swap below always leaves the "- sq" root first: with two_a > 0 (FAST: two_a in
+        // [2^-30, 2^30]) and sq >= 0, RN(-b - sq) <= RN(-b + sq), and the Markstein quotient is
+        // the IEEE one, monotonic in the numerator, wherever the numerator lies in
+        // [2^-60, 2^60]; a root outside that range is below 2^-30 or above 2^30 in magnitude
+        // (or NaN: the quotient overflows past 2^98) in both forms and fails tmin <= t <= bt
+        // either way.  So the shader's choice (the smaller root if it is in [tmin, bt], else the
+        // larger one if that is) is: the smaller root if it is >= tmin, else the larger one,
+        // accepted iff it lies in [tmin, bt] (a smaller root above bt leaves a larger one above
+        // bt too; a NaN root fails its compares, as the IEEE root it stands for, beyond 2^30,
+        // fails them).  4 compares / selects instead of 8.
+        const float ts = quot_markstein(-b - sq, two_a, y);
+        const float tl = quot_markstein(-b + sq, two_a, y);
+        const float tc = (tmin <= ts) ? ts : tl;
+        t_out = tc;
+        return !(delta < 0.0f) & (tmin <= tc) & (tc <= bt);
+    }
+#endif
     float t0 = FAST ? quot_markstein(-b + sq, two_a, y) : (-b + sq) / two_a;
     float t1 = FAST ? quot_markstein(-b - sq, two_a, y) : (-b - sq) / two_a;
     if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
