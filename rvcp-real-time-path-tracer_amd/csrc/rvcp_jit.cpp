@@ -893,7 +893,10 @@ int disk_read(const std::string &dir, const std::string &key, std::vector<char> 
     if (buf.size() < 8 + sizeof(hdr) || std::memcmp(buf.data(), kCoMagic, 8) != 0) return -1;
     std::memcpy(hdr, buf.data() + 8, sizeof(hdr));
     const size_t off = 8 + sizeof(hdr);
-    if (hdr[0] != key.size() || hdr[1] == 0 || buf.size() != off + hdr[0] + hdr[1] ||
+    // (the lengths are compared without forming off + hdr[0] + hdr[1], which a damaged or
+    // crafted header could wrap past 2^64 onto the file size)
+    if (hdr[0] != key.size() || hdr[1] == 0 || buf.size() - off < hdr[0] ||
+        buf.size() - off - hdr[0] != hdr[1] ||
         hdr[3] != fnv1a(key) || std::memcmp(buf.data() + off, key.data(), key.size()) != 0)
         return -1;
     const char *c = buf.data() + off + hdr[0];

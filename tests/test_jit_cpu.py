@@ -324,17 +324,25 @@ def test_code_object_disk_cache(tmp_path):
         assert len(files) == 1 and not list(cache.glob("*.tmp.*"))
         assert get() == (1, size)                                 # read back
         blob = files[0].read_bytes()
+        # a file cut inside its key whose code length is the wrapped difference, so that
+        # header + key + code "adds up" to the file size modulo 2^64 (must be rejected before
+        # the key is compared: the comparison would read past the end of the file's bytes)
+        key_len = int.from_bytes(blob[8:16], "little")
+        cut = 40 + key_len // 2
+        wrapped = (cut - 40 - key_len) % (1 << 64)
+        cut_key = blob[:16] + wrapped.to_bytes(8, "little") + blob[24:cut]
         for bad in (blob[:-1] + bytes([blob[-1] ^ 1]),            # code bit flipped
                     blob[: len(blob) // 2],                       # truncated
                     b"RVCPCO01" + blob[8:40] + b"X" + blob[41:],  # key text altered
+                    cut_key,                                      # length wraps past 2^64
                     b"garbage"):
             files[0].write_bytes(bad)
             assert get() == (0, size)                             # rejected -> recompiled
             assert files[0].read_bytes() == blob                  # ... and rewritten
             assert get() == (1, size)
         c1 = rvcp_amd.abi.code_cache_counts()
-        assert c1["rejects"] - c0["rejects"] == 4
-        assert c1["loads"] - c0["loads"] == 5 and c1["compiles"] - c0["compiles"] == 5
+        assert c1["rejects"] - c0["rejects"] == 5
+        assert c1["loads"] - c0["loads"] == 6 and c1["compiles"] - c0["compiles"] == 6
         rvcp_amd.abi.set_code_cache_dir("")                       # off: compiles, stores nothing
         files[0].unlink()
         assert get() == (0, size) and not list(cache.glob("*.rvcpco"))
