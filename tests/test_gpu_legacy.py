@@ -131,6 +131,34 @@ def test_bitexact_sphere_literal_edge_values():
     _check(sc, _cfg(spp=3, max_bounces=6), 56, 40, time=2.5)
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_bitexact_extreme_sphere_roots(seed):
+    """The FAST sphere roots (rvcp_kernels.hip sphere_accept: Markstein quotients, no swap) on
+    spheres whose root numerators -b -+ sq leave [2^-60, 2^60]: a ground sphere of radius
+    1e19 whose surface passes near the room's floor (cancellation, |b| ~ 2e19), spheres 3e18
+    and 1e19 away (roots beyond 2^30 in both forms, b^2 overflowing to inf so that sq = inf and
+    the Markstein quotients are NaN where the IEEE roots are +-inf), a sphere of radius 2^-70
+    (delta ~ 0) and one of radius 0 -- each decision and accepted t must be the shader's."""
+    base = rvcp_amd.scene.sphere_scene()
+    vec3 = rvcp_amd.scene.vec3
+    mats = list(base.materials)
+    sph = list(base.spheres)
+    m0 = sph[0].material_id
+    rng = np.random.default_rng(seed)
+    sph.append(rvcp_amd.Sphere(vec3(0.0, -1e19, 0.0), 1e19, sph[1].material_id))
+    sph.append(rvcp_amd.Sphere(vec3(3e18, 0.5, 0.0), 1.0, m0))
+    sph.append(rvcp_amd.Sphere(vec3(0.0, 1e19, 1e19), 2.0, m0))
+    sph.append(rvcp_amd.Sphere(vec3(-2.5, 1.0, 0.5), 2.0 ** -70, m0))
+    sph.append(rvcp_amd.Sphere(vec3(2.5, 1.5, 1.0), 0.0, m0))
+    for _ in range(6):                     # and ordinary ones of every material around them
+        sph.append(rvcp_amd.Sphere(vec3(rng.uniform(-4, 4), rng.uniform(0.2, 2.5),
+                                        rng.uniform(-4, 2.5)),
+                                   float(np.float32(rng.uniform(0.2, 0.9))),
+                                   int(rng.integers(1, len(mats)))))
+    sc = rvcp_amd.Scene(base.camera, mats, sph, base.mesh)
+    _check(sc, _cfg(spp=3, max_bounces=6), 56, 40, time=1.75 + seed)
+
+
 def test_bitexact_camera_inside_dielectric(spheres):
     """The camera inside a glass sphere: is_normal_outward = false on the first hit
     (ray_tracer.comp:316-319), refraction_ratio not inverted (:562)."""
