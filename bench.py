@@ -403,10 +403,11 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
       - other mode-2 frames up to 1.5 Mpixel: 3 in flight on 3 waves per SIMD -- mode 2 on the
         C3 frame 1.96 -> 1.88 ms, sphere room 0.308 -> 0.269 ms (round 4: batches of 4 / 8 for
         the sphere room 0.2654 / 0.2621 vs 0.2544 ms with 2 in flight on the full grid,
-        r04m2p_ab_m2pipe.log) -- and since round 6 in batches of up to 4 frames (at most a
-        quarter of the timed steps): the sphere room 0.2363 -> 0.2247 ms at 60 frames (batches
-        of 2 / 6 / 8: 0.2308 / 0.2261 / 0.2214, on 2 waves per SIMD 0.2241), 0.2603 -> 0.2558
-        ms at 20 with 5 (profiles/r06v_ab_m2pipe6.log, r06w_ab_m2pipe7.log, r06x_ab_m2pipe8.log);
+        r04m2p_ab_m2pipe.log) -- and since round 6 in batches of up to 8 frames (at most a
+        quarter of the timed steps): the sphere room 0.2363 -> 0.2194 ms at 60 frames (batches
+        of 2 / 4 / 6 / 10: 0.2308 / 0.2253 / 0.2261 / 0.2242, on 2 waves per SIMD 0.2241),
+        0.2603 -> 0.2558 ms at 20 with 5 (profiles/r06v_ab_m2pipe6.log, r06w_ab_m2pipe7.log,
+        r06x_ab_m2pipe8.log, r06za_ab_m2pipe9.log);
       - larger mode-2 frames and meshes: full grid, one frame per launch, 2 in flight (3 in
         mode 2: one kernel per frame, no pre-pass);
       - other small frames (below 4 Msamples): 4 in flight (C2 0.59/0.32/0.27/0.33 ms for
@@ -428,8 +429,8 @@ def auto_pipeline(pixels, spp, legacy, small_scene, hw_queues, accel="none", ste
         # mode 2 with long pixel chains (the C3 frame): batches of up to 8 frames, 2 in flight
         fif, grid, batch = 2, 0, min(8, steps // 4 if steps else 8)
     elif small_scene and pixels <= 1536 * 1024:
-        # (mode 2 only: games101 small scenes took the first branch) batches of up to 4 frames
-        fif, grid, batch = 3, 3, max(1, min(4, steps // 4 if steps else 4))
+        # (mode 2 only: games101 small scenes took the first branch) batches of up to 8 frames
+        fif, grid, batch = 3, 3, max(1, min(8, steps // 4 if steps else 8))
     else:
         fif, grid, batch = (3 if legacy else 2), 0, 1
     try:

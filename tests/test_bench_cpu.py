@@ -38,7 +38,7 @@ def test_auto_pipeline():
     small scene (or the BVH) in batches of about 3 Mpixel (4 from 1-Mpixel frames) and at least 2 frames (at most 32,
     at most a quarter of the timed steps), 2 in flight; mode 2 up to 1.5 Mpixel with at least 16
     Msamples per frame in batches of up to 8, 2 in flight, other mode-2 frames up to 1.5 Mpixel
-    3 in flight on 3 waves per SIMD in batches of up to 4; larger mode-2 frames and meshes the full grid, one frame per launch;
+    3 in flight on 3 waves per SIMD in batches of up to 8; larger mode-2 frames and meshes the full grid, one frame per launch;
     never more contexts than the hardware queues minus one."""
     ap = bench.auto_pipeline
     assert ap(1024 * 1024, 30, False, True, "4", "none", 20) == (2, 0, 4)          # C3
@@ -58,8 +58,8 @@ def test_auto_pipeline():
     assert ap(1024 * 1024, 30, True, True, "4", "none", 20) == (2, 0, 5)           # mode 2, C3 frame
     assert ap(1024 * 1024, 30, True, True, "4", "none", 40) == (2, 0, 8)
     assert ap(1024 * 1024, 30, True, True, "4", "none", 5) == (3, 3, 1)            # too few steps
-    assert ap(1024 * 1024, 5, True, True, "4", "none", 20) == (3, 3, 4)            # sphere room
-    assert ap(1024 * 1024, 5, True, True, "4", "none", 60) == (3, 3, 4)
+    assert ap(1024 * 1024, 5, True, True, "4", "none", 20) == (3, 3, 5)            # sphere room
+    assert ap(1024 * 1024, 5, True, True, "4", "none", 60) == (3, 3, 8)
     assert ap(1024 * 1024, 5, True, True, "4", "none", 8) == (3, 3, 2)
     assert ap(1024 * 1024, 5, True, True, "4", "none", 3) == (3, 3, 1)             # too few steps
     assert ap(384 * 384, 5, True, True, "8", "none", 20) == (4, 0, 1)              # small mode-2 frame
