@@ -2833,13 +2833,23 @@ __device__ __forceinline__ void legacy_hit(const FrameArgs &A, const TriRecord *
                                            bool &ho) {
     ho = true;
     hpos = add(ro, muls(rd, bt));
-    if ((uint32_t)best < A.n_spheres) {                         // :314-319
+    // The vector each kind of hit normalises -- hpos - centre (:314), or the interpolated vertex
+    // normal (:352-356) -- is chosen per lane and normalised once after the branch: a wave
+    // whose lanes hit both kinds runs one normalize instead of two (the same operations on
+    // the same value per lane).
+    const bool is_sphere = (uint32_t)best < A.n_spheres;
+    f3 nv;
+    bool inside = false;
+    if (is_sphere) {                                            // :314-319
         const rvcp_sphere_t S = sph[best];
         const f3 ce = ld3(S.center);
-        hn = normalize(sub(hpos, ce));
+        nv = sub(hpos, ce);
         const f3 oc = sub(ro, ce);
-        if (dot(oc, oc) < S.radius * S.radius) { hn = neg(hn); ho = false; }
+        inside = dot(oc, oc) < S.radius * S.radius;
         hm = S.material_id;
+#ifdef RVCP_HIT_SPLIT_NORMALIZE     // (A/B only: a normalize in each branch, as before round 6)
+        hn = normalize(nv);
+#endif
     } else {                                                    // :348-363
         const int fi = best - (int)A.n_spheres;
         const TriRecord T = tri[fi];
@@ -2850,11 +2860,16 @@ __device__ __forceinline__ void legacy_hit(const FrameArgs &A, const TriRecord *
         const float f = rcp_ieee(dot(s1, ld3(T.e1)));
         const float b1 = f * dot(s1, s);
         const float b2 = f * dot(s2, rd);
-        hn = normalize(add(add(muls(ld3(fs.n0), 1.0f - b1 - b2), muls(ld3(fs.n1), b1)),
-                           muls(ld3(fs.n2), b2)));
-        if (dot(hn, rd) > 0.0f) { hn = neg(hn); ho = false; }
+        nv = add(add(muls(ld3(fs.n0), 1.0f - b1 - b2), muls(ld3(fs.n1), b1)), muls(ld3(fs.n2), b2));
         hm = fs.mat;
+#ifdef RVCP_HIT_SPLIT_NORMALIZE
+        hn = normalize(nv);
+#endif
     }
+#ifndef RVCP_HIT_SPLIT_NORMALIZE
+    hn = normalize(nv);
+#endif
+    if (is_sphere ? inside : dot(hn, rd) > 0.0f) { hn = neg(hn); ho = false; }
 }
 
 // kLegacyDefer: the most lanes left ending a sample that sit out one trace (below).  16
